@@ -1,0 +1,175 @@
+/*
+ * mpcqp.h -- C ABI of libmpcqp.so, the MI355X-native batched condensed-QP
+ * MPC solver (gfx950 / CDNA4, HIP).
+ *
+ * The reference (konnpaku-youmu/Model_Predictive_Control) has no FFI: its hot
+ * path is a set of Python call surfaces that today reach NumPy and
+ * CasADi/IPOPT.  Each entry point below replaces one of them; the Python
+ * shim in model_predictive_control_amd/ keeps the reference's call surface
+ * and calls these through ctypes:
+ *
+ *   mpcqp_condense   <- the symbolic single-shooting elimination of
+ *                       session_4/main.py:86-106 (and session4_sol.py:195-204)
+ *                       written as dense H, F, f, Gamma, Phi, xbar.
+ *   mpcqp_solve_box  <- the per-step IPOPT call of session_4/main.py:115-116
+ *                       (session4_sol.py:128-129) for an input box
+ *                       (lbx/ubx, main.py:68-69,97-98).
+ *   mpcqp_solve_poly <- the same call with general rows hl <= G z <= hu (state box
+ *                       lbg/ubg of main.py:58-61,99-100 after condensing, or
+ *                       arbitrary polytopes -- BASELINE config 4).
+ *   mpcqp_riccati    <- ricatti_recursion(A,B,Q,R,P_f,N), session_1/FHC.py:51-61
+ *                       (and riccati_recursion, session1_sol.py:44-65).
+ *   mpcqp_gemv       <- the batched  f = F x0  /  z = -W x0 - U lambda  products
+ *                       that sit between condense and solve.
+ *   mpcqp_rollout    <- LinearSystem.simulate (session_1/LinearSystem.py:20-26)
+ *                       under a linear state-feedback policy
+ *                       (AutoCruising.control_law, FHC.py:25-26).
+ *
+ * Conventions (all entry points):
+ *  - dtype: MPCQP_F64 or MPCQP_F32; every floating buffer of a call has it.
+ *  - Buffers are caller-owned DEVICE pointers (hipMalloc / torch tensors),
+ *    row-major, batch-outermost.  A "stride" is the element distance between
+ *    consecutive instances; stride 0 means one buffer shared by the batch.
+ *    The library keeps no pointer after the call returns.
+ *  - z is stage-major: z = [u_0; u_1; ...; u_{N-1}] (main.py:46,110).
+ *  - Symmetric n x n matrices (H, the dual M) are stored PACKED LOWER,
+ *    row-major: element (i, j<=i) at i*(i+1)/2 + j, n(n+1)/2 per instance.
+ *  - stream is a hipStream_t (NULL = default stream).  Calls only enqueue
+ *    work; they never synchronise, allocate or free (graph-capturable).
+ *  - Return value: MPCQP_OK (0) or a negative error code; the message is
+ *    available from mpcqp_last_error() (thread-local).
+ *  - Per-instance outcome goes to status[b]: low byte = MPCQP_STATUS_*, bits
+ *    8..23 = active-set iterations used.
+ *    This mirrors the per-step ``solver_success`` of session_2/log.py:10.
+ */
+#ifndef MPCQP_H
+#define MPCQP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCQP_ABI_VERSION 1
+
+/* dtypes */
+#define MPCQP_F64 0
+#define MPCQP_F32 1
+
+/* return codes */
+#define MPCQP_OK 0
+#define MPCQP_EINVAL (-1)   /* bad argument (shape, pointer, dtype) */
+#define MPCQP_EHIP (-2)     /* HIP runtime error (launch / no device) */
+#define MPCQP_ENOTSUP (-3)  /* size outside the compiled kernel set */
+
+/* per-instance status (low byte of status[b]) */
+#define MPCQP_STATUS_OPTIMAL 0
+#define MPCQP_STATUS_MAXITER 1
+#define MPCQP_STATUS_NOT_CONVEX 2  /* non-positive pivot: H not positive definite */
+#define MPCQP_STATUS_INFEASIBLE 3  /* lb > ub, or polytope empty */
+#define MPCQP_STATUS_NONFINITE 4   /* NaN/Inf in the data */
+
+/* condense flags */
+#define MPCQP_TV 1 /* A, B are per-stage: N*nx*nx / N*nx*nu per instance */
+
+int mpcqp_abi_version(void);
+const char* mpcqp_last_error(void);
+/* Largest n (= N*nu) accepted by mpcqp_solve_box and the dual size accepted
+ * by mpcqp_solve_poly for the given dtype. */
+int mpcqp_max_box_n(int dtype);
+
+/*
+ * Batched condensing of  x_{k+1} = A_k x_k + B_k u_k + c_k,  k = 0..N-1, with
+ * cost  sum_{k<N} x_k'Q x_k + u_k'R u_k + x_N'Qf x_N  (session_4/main.py:86-106):
+ *
+ *   X = [x_1;..;x_N] = Phi x0 + Gam z + w,   xbar = Phi x0 + w
+ *   H = Gam' Qhat Gam + Rhat  (packed lower, n(n+1)/2),   n = N*nu
+ *   F = Gam' Qhat Phi  (n x nx),   f = Gam' Qhat xbar (n)
+ *
+ * Inputs (per-instance strides in elements; 0 = shared):
+ *   A  nx*nx (or N*nx*nx with MPCQP_TV), Bm nx*nu (or N*nx*nu), Q nx*nx,
+ *   R nu*nu, Qf nx*nx, c (optional, N*nx), x0 (optional, nx).
+ * Outputs (NULL to skip; per-instance, densely packed):
+ *   H (required), F, f (uses x0 and c; x0 = NULL means x0 = 0),
+ *   Gam (N*nx x n), Phi (N*nx x nx), xbar (N*nx).
+ * Limits: 1 <= nx <= 16, 1 <= nu <= 16, N >= 1.
+ */
+int mpcqp_condense(int dtype, int batch, int nx, int nu, int N, int flags,
+                   const void* A, int64_t strideA, const void* Bm, int64_t strideB,
+                   const void* Q, int64_t strideQ, const void* R, int64_t strideR,
+                   const void* Qf, int64_t strideQf, const void* c, int64_t strideC,
+                   const void* x0, int64_t strideX0,
+                   void* H, void* F, void* f, void* Gam, void* Phi, void* xbar,
+                   void* stream);
+
+/*
+ * Batched box QP:  min 1/2 z'Hz + f'z   s.t.  lb <= z <= ub   (n <= 64).
+ * H packed lower (stride 0 = shared), f/lb/ub per instance or shared
+ * (lb/ub NULL = -inf/+inf).  One QP per wavefront: Goldfarb-Idnani dual
+ * active set specialised to bounds, on H swept over the free set (one row per
+ * lane, pivot rows broadcast by v_readlane).  Finite termination; iterations
+ * ~ number of active bounds.  max_iter <= 0 selects the default (3n + 30);
+ * tol <= 0 the default relative feasibility tolerance (1e-12 f64, 1e-6 f32).
+ */
+int mpcqp_solve_box(int dtype, int batch, int n,
+                    const void* H, int64_t strideH, const void* f, int64_t stridef,
+                    const void* lb, int64_t strideLb, const void* ub, int64_t strideUb,
+                    void* z, int32_t* status, int max_iter, double tol, void* stream);
+
+/*
+ * Batched polytope QP:
+ *     min 1/2 z'Hz + f'z   s.t.  hl <= G z <= hu,   lbz <= z <= ubz
+ * H (n x n, packed lower) and G (m x n) are SHARED by the batch (the
+ * shared-structure form of BASELINE config 4 and of LTI state boxes);
+ * f (n) and the row bounds hl/hu (m) vary per instance (stride 0 = shared;
+ * NULL = -inf / +inf).  The box rows are appended to C = [G; I] when lbz or
+ * ubz is given (then m_total = m + n, else m_total = m; m_total <= 64).
+ * Solved through the dual: Hinv, Ut = C Hinv and M = C Hinv C' are formed once
+ * per call on device; per instance a wavefront runs a dual range active set
+ * (Goldfarb-Idnani in the row space, tolerant of linearly dependent rows) and
+ * recovers z = -Hinv f - Ut' y.  y (batch x m_total): row multipliers,
+ * y > 0 at the upper bound, y < 0 at the lower bound.
+ * workspace: device scratch of at least mpcqp_solve_poly_workspace() bytes
+ * (nbox = 1 when lbz or ubz is given).
+ */
+int64_t mpcqp_solve_poly_workspace(int dtype, int batch, int n, int m, int nbox);
+int mpcqp_solve_poly(int dtype, int batch, int n, int m,
+                     const void* H, const void* f, int64_t stridef,
+                     const void* G, const void* hl, const void* hu, int64_t strideh,
+                     const void* lbz, const void* ubz,
+                     void* z, void* y, int32_t* status, int max_iter, double tol,
+                     void* workspace, int64_t workspace_bytes, void* stream);
+
+/*
+ * Batched finite-horizon Riccati recursion, FHC.py:51-61:
+ *   K_k = -(R + B'P B)^{-1} B'P A,  P_k = Q + A'P A + A'P B K_k,  P_N = Pf
+ * Outputs in the reference's order (lists reversed: K[0] is the first-stage
+ * gain): P (N+1)*nx*nx, K N*nu*nx per instance.  nx, nu <= 4.
+ */
+int mpcqp_riccati(int dtype, int batch, int nx, int nu, int N,
+                  const void* A, int64_t strideA, const void* Bm, int64_t strideB,
+                  const void* Q, int64_t strideQ, const void* R, int64_t strideR,
+                  const void* Pf, int64_t stridePf, void* P, void* K, void* stream);
+
+/* Batched  y_b = alpha * M_b x_b + beta * y_b,  M_b (rows x cols) row-major. */
+int mpcqp_gemv(int dtype, int batch, int rows, int cols, double alpha,
+               const void* M, int64_t strideM, const void* x, int64_t strideX,
+               double beta, void* y, int64_t strideY, void* stream);
+
+/*
+ * Batched closed-loop rollout of LinearSystem.simulate (LinearSystem.py:20-26)
+ * with u_t = K x_t (AutoCruising.control_law, FHC.py:25-26):
+ *   x_{t+1} = A x_t + B K x_t,  t = 1..steps-1.
+ * A, Bm, K shared; x0 (batch x nx); xs out TIME-MAJOR (steps x batch x nx),
+ * whose (2,1,0) permutation is the reference's (nx, batch, steps) state
+ * tensor (LinearSystem.py:21,26).  nx, nu <= 16.
+ */
+int mpcqp_rollout(int dtype, int batch, int nx, int nu, int steps,
+                  const void* A, const void* Bm, const void* K,
+                  const void* x0, void* xs, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCQP_H */

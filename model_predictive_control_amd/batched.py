@@ -1,0 +1,301 @@
+"""Batched device API over libmpcqp (torch tensors on the GPU).
+
+This is the layer the reference-shaped surfaces (``fhc``, ``linear_system``,
+``session1``, ``mpc``) and ``bench.py`` call.  Every function enqueues HIP
+kernels on torch's current stream through the C ABI of include/mpcqp.h; no
+computation happens on the host.
+
+Shape conventions (batch-outermost, row-major):
+
+* a per-instance input carries a leading batch dimension, a shared input
+  does not (it is passed with stride 0);
+* ``z`` is stage-major  [u_0; ...; u_{N-1}]  (session_4/main.py:46,110);
+* symmetric matrices (H) are packed lower, n(n+1)/2 per instance
+  (``pack_lower`` / ``unpack_lower`` convert).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _native as nat
+
+__all__ = [
+    "condense", "solve_box", "solve_poly", "riccati", "gemv", "rollout",
+    "pack_lower", "unpack_lower", "status_code", "status_iters",
+]
+
+
+def _lib():
+    return nat.load()
+
+
+def _code(dtype: torch.dtype) -> int:
+    if dtype == torch.float64:
+        return nat.F64
+    if dtype == torch.float32:
+        return nat.F32
+    raise TypeError(f"libmpcqp supports float64/float32, got {dtype}")
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _dev(x, dtype, device):
+    if x is None:
+        return None
+    t = torch.as_tensor(x, dtype=dtype, device=device)
+    if t.device.type != "cuda":
+        raise ValueError("libmpcqp needs CUDA(HIP) tensors")
+    return t.contiguous()
+
+
+def _inst(t, base_ndim: int, name: str):
+    """(stride, batch) of an input that is shared (ndim == base) or batched."""
+    if t is None:
+        return 0, None
+    if t.ndim == base_ndim:
+        return 0, None
+    if t.ndim == base_ndim + 1:
+        return int(t[0].numel()), int(t.shape[0])
+    raise ValueError(f"{name}: expected {base_ndim} or {base_ndim + 1} dims, got {tuple(t.shape)}")
+
+
+def _batch_of(*pairs):
+    bs = {b for _, b in pairs if b is not None}
+    if len(bs) > 1:
+        raise ValueError(f"inconsistent batch sizes {sorted(bs)}")
+    return bs.pop() if bs else 1
+
+
+def status_code(status: torch.Tensor) -> torch.Tensor:
+    return status & 0xFF
+
+
+def status_iters(status: torch.Tensor) -> torch.Tensor:
+    return (status >> 8) & 0xFFFF
+
+
+# ----------------------------------------------------------------- packing
+def _tril_index(n: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    r, c = torch.tril_indices(n, n, device=device)
+    return r, c
+
+
+def pack_lower(H: torch.Tensor) -> torch.Tensor:
+    """(..., n, n) symmetric -> (..., n(n+1)/2) row-major packed lower."""
+    n = H.shape[-1]
+    r, c = _tril_index(n, H.device)
+    return H[..., r, c].contiguous()
+
+
+def unpack_lower(P: torch.Tensor, n: int) -> torch.Tensor:
+    """(..., n(n+1)/2) packed lower -> (..., n, n) symmetric."""
+    r, c = _tril_index(n, P.device)
+    out = P.new_zeros(P.shape[:-1] + (n, n))
+    out[..., r, c] = P
+    out[..., c, r] = P
+    return out
+
+
+# ---------------------------------------------------------------- condense
+def condense(A, B, Q, R, Qf, N: int, x0=None, c=None, *, tv: bool = False,
+             outputs=("H", "f"), out: dict | None = None) -> dict:
+    """Batched condensing (include/mpcqp.h ``mpcqp_condense``).
+
+    A: (nx,nx) | (b,nx,nx) | with ``tv``: (N,nx,nx) | (b,N,nx,nx); B likewise
+    with nu columns; Q/Qf (nx,nx) | (b,nx,nx); R (nu,nu) | (b,nu,nu);
+    x0 (nx,) | (b,nx); c (N,nx) | (b,N,nx).  Returns a dict with the requested
+    ``outputs`` among H (packed), F, f, Gam, Phi, xbar.
+    """
+    dt = A.dtype if isinstance(A, torch.Tensor) else torch.float64
+    dev = A.device if isinstance(A, torch.Tensor) else torch.device("cuda")
+    A, B, Q, R, Qf = (_dev(v, dt, dev) for v in (A, B, Q, R, Qf))
+    x0, c = _dev(x0, dt, dev), _dev(c, dt, dev)
+    nx, nu = int(B.shape[-2]), int(B.shape[-1])
+    if R.ndim == 1 or (R.ndim == 2 and R.shape != (nu, nu) and R.shape[-1] == nu):
+        # FHC.py:141 passes R with shape (1,); numpy broadcasting semantics
+        R = R.expand(nu, nu).contiguous() if R.ndim == 1 else R
+    base = 3 if tv else 2
+    sA, bA = _inst(A, base, "A")
+    sB, bB = _inst(B, base, "B")
+    sQ, bQ = _inst(Q, 2, "Q")
+    sR, bR = _inst(R, 2, "R")
+    sQf, bQf = _inst(Qf, 2, "Qf")
+    sC, bC = _inst(c, 2, "c")
+    sX, bX = _inst(x0, 1, "x0")
+    batch = _batch_of((sA, bA), (sB, bB), (sQ, bQ), (sR, bR), (sQf, bQf), (sC, bC), (sX, bX))
+    n = N * nu
+    want = set(outputs) | {"H"}
+    out = dict(out or {})
+    shapes = {"H": (batch, n * (n + 1) // 2), "F": (batch, n, nx), "f": (batch, n),
+              "Gam": (batch, N * nx, n), "Phi": (batch, N * nx, nx), "xbar": (batch, N * nx)}
+    for k in want:
+        if k not in out:
+            out[k] = torch.empty(shapes[k], dtype=dt, device=dev)
+    rc = _lib().mpcqp_condense(
+        _code(dt), batch, nx, nu, N, nat.TV if tv else 0,
+        _ptr(A), sA, _ptr(B), sB, _ptr(Q), sQ, _ptr(R), sR, _ptr(Qf), sQf, _ptr(c), sC,
+        _ptr(x0), sX, _ptr(out.get("H")), _ptr(out.get("F")), _ptr(out.get("f")),
+        _ptr(out.get("Gam")), _ptr(out.get("Phi")), _ptr(out.get("xbar")), _stream())
+    nat.check(rc, "mpcqp_condense")
+    return {k: out[k] for k in want}
+
+
+# ----------------------------------------------------------------- box QP
+def _bound(v, n, dt, dev):
+    if v is None:
+        return None, 0
+    if not isinstance(v, torch.Tensor) and (isinstance(v, (int, float))):
+        return torch.full((n,), float(v), dtype=dt, device=dev), 0
+    t = _dev(v, dt, dev)
+    if t.ndim == 0:
+        return t.expand(n).contiguous(), 0
+    s, _ = _inst(t, 1, "bound")
+    return t, s
+
+
+def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, tol: float = 0.0,
+              out: tuple | None = None):
+    """Batched  min 1/2 z'Hz + f'z  s.t.  lb <= z <= ub.  Returns (z, status)."""
+    dt, dev = f.dtype, f.device
+    f = _dev(f, dt, dev)
+    H = _dev(H, dt, dev)
+    n = int(f.shape[-1])
+    if H.shape[-1] != n * (n + 1) // 2:
+        raise ValueError(f"H must be packed lower with {n * (n + 1) // 2} entries, got {tuple(H.shape)}")
+    sH, bH = _inst(H, 1, "H")
+    sf, bf = _inst(f, 1, "f")
+    lbt, slb = _bound(lb, n, dt, dev)
+    ubt, sub = _bound(ub, n, dt, dev)
+    batch = _batch_of((sH, bH), (sf, bf),
+                      (slb, lbt.shape[0] if lbt is not None and lbt.ndim == 2 else None),
+                      (sub, ubt.shape[0] if ubt is not None and ubt.ndim == 2 else None))
+    if out is None:
+        z = torch.empty((batch, n), dtype=dt, device=dev)
+        status = torch.empty((batch,), dtype=torch.int32, device=dev)
+    else:
+        z, status = out
+    rc = _lib().mpcqp_solve_box(_code(dt), batch, n, _ptr(H), sH, _ptr(f), sf, _ptr(lbt), slb,
+                                _ptr(ubt), sub, _ptr(z), _ptr(status), int(max_iter), float(tol),
+                                _stream())
+    nat.check(rc, "mpcqp_solve_box")
+    return z, status
+
+
+# ------------------------------------------------------------- polytope QP
+def solve_poly(H, f, G=None, hl=None, hu=None, lbz=None, ubz=None, *, max_iter: int = 0,
+               tol: float = 0.0):
+    """Batched  min 1/2 z'Hz + f'z  s.t.  hl <= G z <= hu,  lbz <= z <= ubz.
+
+    H (packed, shared) and G (m, n) shared; f, hl, hu per instance or shared.
+    Returns (z, y, status); y are the multipliers of the rows [G; I].
+    """
+    dt, dev = f.dtype, f.device
+    f = _dev(f, dt, dev)
+    H = _dev(H, dt, dev)
+    n = int(f.shape[-1])
+    if H.ndim != 1:
+        raise ValueError("solve_poly: H must be shared (packed, 1-D)")
+    m = 0 if G is None else int(G.shape[0])
+    G = _dev(G, dt, dev)
+    sf, bf = _inst(f, 1, "f")
+    hl = _dev(hl, dt, dev)
+    hu = _dev(hu, dt, dev)
+    sh, bh = 0, None
+    for h in (hl, hu):
+        if h is not None:
+            s, b = _inst(h, 1, "h")
+            sh, bh = max(sh, s), b if b is not None else bh
+    if hl is not None and hu is not None and hl.shape != hu.shape:
+        raise ValueError("hl and hu must have the same shape")
+    lbz_t, _ = _bound(lbz, n, dt, dev)
+    ubz_t, _ = _bound(ubz, n, dt, dev)
+    nbox = 1 if (lbz_t is not None or ubz_t is not None) else 0
+    mt = m + (n if nbox else 0)
+    batch = _batch_of((sf, bf), (sh, bh))
+    lib = _lib()
+    wsb = int(lib.mpcqp_solve_poly_workspace(_code(dt), batch, n, m, nbox))
+    ws = torch.empty((wsb,), dtype=torch.uint8, device=dev)
+    z = torch.empty((batch, n), dtype=dt, device=dev)
+    y = torch.empty((batch, mt), dtype=dt, device=dev)
+    status = torch.empty((batch,), dtype=torch.int32, device=dev)
+    rc = lib.mpcqp_solve_poly(_code(dt), batch, n, m, _ptr(H), _ptr(f), sf, _ptr(G), _ptr(hl),
+                              _ptr(hu), sh, _ptr(lbz_t), _ptr(ubz_t), _ptr(z), _ptr(y),
+                              _ptr(status), int(max_iter), float(tol), _ptr(ws), wsb, _stream())
+    nat.check(rc, "mpcqp_solve_poly")
+    return z, y, status
+
+
+# ---------------------------------------------------------------- Riccati
+def riccati(A, B, Q, R, Pf, N: int):
+    """Batched FHC.ricatti_recursion: returns P (b,N+1,nx,nx), K (b,N,nu,nx)."""
+    dt = A.dtype
+    dev = A.device
+    A, B, Q, R, Pf = (_dev(v, dt, dev) for v in (A, B, Q, R, Pf))
+    nx, nu = int(B.shape[-2]), int(B.shape[-1])
+    if R.ndim == 1:
+        R = R.expand(nu, nu).contiguous()
+    sA, bA = _inst(A, 2, "A")
+    sB, bB = _inst(B, 2, "B")
+    sQ, bQ = _inst(Q, 2, "Q")
+    sR, bR = _inst(R, 2, "R")
+    sP, bP = _inst(Pf, 2, "Pf")
+    batch = _batch_of((sA, bA), (sB, bB), (sQ, bQ), (sR, bR), (sP, bP))
+    P = torch.empty((batch, N + 1, nx, nx), dtype=dt, device=dev)
+    K = torch.empty((batch, N, nu, nx), dtype=dt, device=dev)
+    rc = _lib().mpcqp_riccati(_code(dt), batch, nx, nu, N, _ptr(A), sA, _ptr(B), sB, _ptr(Q), sQ,
+                              _ptr(R), sR, _ptr(Pf), sP, _ptr(P), _ptr(K), _stream())
+    nat.check(rc, "mpcqp_riccati")
+    return P, K
+
+
+# ------------------------------------------------------------------ gemv
+def gemv(M, x, alpha: float = 1.0, beta: float = 0.0, y=None):
+    """Batched y = alpha M x + beta y; M (r,c) shared or (b,r,c); x (c,) or (b,c)."""
+    dt, dev = x.dtype, x.device
+    M, x = _dev(M, dt, dev), _dev(x, dt, dev)
+    rows, cols = int(M.shape[-2]), int(M.shape[-1])
+    sM, bM = _inst(M, 2, "M")
+    sX, bX = _inst(x, 1, "x")
+    batch = _batch_of((sM, bM), (sX, bX))
+    if y is None:
+        y = torch.zeros((batch, rows), dtype=dt, device=dev)
+    rc = _lib().mpcqp_gemv(_code(dt), batch, rows, cols, float(alpha), _ptr(M), sM, _ptr(x), sX,
+                           float(beta), _ptr(y), rows, _stream())
+    nat.check(rc, "mpcqp_gemv")
+    return y
+
+
+# --------------------------------------------------------------- rollout
+def rollout(A, B, K, x0, steps: int):
+    """Closed loop x_{t+1} = (A + B K) x_t for a batch of x0 (b,nx).
+
+    Returns xs (steps, b, nx) time-major; ``xs.permute(2, 1, 0)`` is the
+    reference's (nx, batch, steps) state tensor (LinearSystem.py:21,26).
+    """
+    dt, dev = x0.dtype, x0.device
+    A, B, K, x0 = (_dev(v, dt, dev) for v in (A, B, K, x0))
+    nx, nu = int(B.shape[-2]), int(B.shape[-1])
+    batch = int(x0.shape[0])
+    xs = torch.empty((steps, batch, nx), dtype=dt, device=dev)
+    rc = _lib().mpcqp_rollout(_code(dt), batch, nx, nu, steps, _ptr(A), _ptr(B), _ptr(K), _ptr(x0),
+                              _ptr(xs), _stream())
+    nat.check(rc, "mpcqp_rollout")
+    return xs
+
+
+def n_packed(n: int) -> int:
+    return n * (n + 1) // 2
+
+
+def isqrt_packed(p: int) -> int:
+    n = int((math.isqrt(8 * p + 1) - 1) // 2)
+    assert n * (n + 1) // 2 == p
+    return n

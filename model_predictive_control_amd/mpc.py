@@ -1,0 +1,125 @@
+"""MPCController -- the per-step OCP of session_4 on the MI355X path.
+
+Reference: ``MPCController`` in session_4/main.py:29-129 (and the box-only
+variant session4_sol.py:113-230).  The reference builds a single-shooting
+NLP in CasADi (z = [u_0..u_{N-1}], main.py:46; cost main.py:86-106) and calls
+IPOPT every closed-loop step (``solve`` main.py:115-116, ``__call__``
+main.py:121-129).  Here each ``solve`` is a real-time-iteration SQP step on
+device:
+
+  1. nominal rollout of the forward-Euler model from x0 with the warm-started
+     input sequence (previous solution shifted one stage),
+  2. per-stage linearisation (A_k, B_k, c_k)  (bicycle.fe_linearize_batched),
+  3. time-varying condensing  -> H, f        (libmpcqp ``mpcqp_condense``, TV),
+  4. input-box QP                            (libmpcqp ``mpcqp_solve_box``),
+
+repeated ``sqp_iters`` times.  Any number of initial states is solved in one
+batch (``solve`` accepts x of shape (nx,) or (batch, nx)).
+
+Scope notes: the collision rows of main.py:95-104 are non-convex and out of
+scope; the state box (main.py:58-61) needs per-instance constraint rows and
+is not enforced by this controller yet ("next").
+"""
+from __future__ import annotations
+
+import inspect
+
+import numpy as np
+import torch
+
+from . import batched
+from .bicycle import KinematicBicycle, fe_linearize_batched, fe_step_batched
+from .parameters import VehicleParameters
+
+
+class MPCController:
+    def __init__(self, N: int, ts: float, params: VehicleParameters | None = None, model=None,
+                 x_obs=None, *, Q=None, QN=None, R=None, sqp_iters: int = 3,
+                 dtype=torch.float64, device=None) -> None:
+        self.N = N
+        self.ts = ts
+        self.params = params or VehicleParameters()
+        self.model = model or KinematicBicycle(self.params)
+        self.x_obs = x_obs
+        self.nx, self.nu = 4, 2
+        # weights of main.py:72-74
+        Q = np.diag([1., 6., 0.2, 0.05]) if Q is None else np.asarray(Q, float)
+        QN = 100 * Q if QN is None else np.asarray(QN, float)
+        R = np.diag([1, 0.01]) if R is None else np.asarray(R, float)
+        self.dtype = dtype
+        self.device = device or torch.device("cuda")
+        if not torch.cuda.is_available():
+            raise RuntimeError("MPCController needs a ROCm GPU (no CPU fallback)")
+        t = lambda a: torch.as_tensor(a, dtype=dtype, device=self.device)  # noqa: E731
+        self.Q, self.QN, self.R = t(Q), t(QN), t(R)
+        p = self.params
+        # input box of main.py:68-69 (drive, steer), repeated over the horizon
+        self.lb_inputs = np.array([p.min_drive, -p.max_steer])
+        self.ub_inputs = np.array([p.max_drive, p.max_steer])
+        self.lbz = t(np.tile(self.lb_inputs, N))
+        self.ubz = t(np.tile(self.ub_inputs, N))
+        self.bounds = dict(lbx=np.tile(self.lb_inputs, N), ubx=np.tile(self.ub_inputs, N))
+        self.sqp_iters = sqp_iters
+        self._warm = None
+        self.last_status = None
+
+    # ------------------------------------------------------------- solve
+    def solve_batch(self, X0: torch.Tensor):
+        """X0 (batch, 4) device tensor -> (z (batch, N*nu), status (batch,))."""
+        N, nu = self.N, self.nu
+        X0 = X0.to(self.dtype).contiguous()
+        b = X0.shape[0]
+        if self._warm is not None and self._warm.shape[0] == b:
+            U = self._warm
+        else:
+            U = torch.zeros((b, N, nu), dtype=self.dtype, device=self.device)
+        z = status = None
+        for _ in range(self.sqp_iters):
+            xs = [X0]
+            for k in range(N - 1):
+                xs.append(fe_step_batched(xs[-1], U[:, k], self.params, self.ts))
+            Xn = torch.stack(xs, 1)
+            A, B, c = fe_linearize_batched(Xn, U, self.params, self.ts)
+            d = batched.condense(A.contiguous(), B.contiguous(), self.Q, self.R, self.QN, N,
+                                 x0=X0, c=c.contiguous(), tv=True, outputs=("H", "f"))
+            z, status = batched.solve_box(d["H"], d["f"], self.lbz, self.ubz)
+            U = z.view(b, N, nu)
+        self._warm = torch.cat([U[:, 1:], U[:, -1:]], 1).contiguous()
+        self.last_status = status
+        return z, status
+
+    def solve(self, x) -> dict:
+        """main.py:115-116: returns {"x": (N*nu, 1)} (or (batch, N*nu))."""
+        xa = np.asarray(x, dtype=float)
+        single = xa.ndim == 1
+        X0 = torch.as_tensor(xa.reshape(-1, self.nx), dtype=self.dtype, device=self.device)
+        z, status = self.solve_batch(X0)
+        zn = z.cpu().numpy()
+        st = batched.status_code(status).cpu().numpy()
+        return {"x": zn.reshape(-1, 1) if single else zn,
+                "status": st[0] if single else st,
+                "success": bool(st[0] == 0) if single else st == 0}
+
+    def reshape_input(self, sol):
+        """main.py:118-119."""
+        return np.reshape(sol["x"], (-1, 2))
+
+    def __call__(self, y):
+        """main.py:121-129: solve for measured state y, return u[0]."""
+        return self.reshape_input(self.solve(y))[0]
+
+
+def simulate(x0, dynamics, n_steps: int, policy):
+    """Restatement of ``rcracers.simulator.simulate`` as used at main.py:270-271
+    (source unavailable): returns the (n_steps+1, nx) state sequence; the
+    policy is called as policy(x, t) when it accepts two arguments, else
+    policy(x) (MPCController.__call__, main.py:121)."""
+    try:
+        two = len(inspect.signature(policy).parameters) >= 2
+    except (TypeError, ValueError):
+        two = False
+    xs = [np.asarray(x0, dtype=float)]
+    for t in range(n_steps):
+        u = policy(xs[-1], t) if two else policy(xs[-1])
+        xs.append(np.asarray(dynamics(xs[-1], u), dtype=float))
+    return np.array(xs)

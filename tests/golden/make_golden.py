@@ -1,0 +1,214 @@
+"""Generate the golden fixtures in tests/golden/ (run in the build container).
+
+session1.npz  -- outputs of the *reference's own code*, imported from
+                 /root/reference/session_1 (FHC.py, LinearSystem.py,
+                 session1_sol.py).  FHC.py imports ``casadi`` (FHC.py:1) and
+                 ``rcracers`` (FHC.py:5) without using them; both are absent
+                 here, so empty placeholder modules are registered before the
+                 import.  Nothing else is stubbed.
+problems.npz  -- the session 2/3 ``Problem`` dataclass values, imported from
+                 /root/reference/session_2/problem.py and session_3/problem.py.
+boxqp_cfg2.npz -- config 2 (double integrator of FHC.py:136-142, N=20,
+                 |u|<=1, 64 seeded x0 ~ U(-10,10)^2): condensed (H, f) from
+                 the explicit-matrix oracle and the minimiser from SciPy BVLS,
+                 cross-checked against the oracle active-set solver and
+                 certified by KKT residuals (the reference's own solver,
+                 CasADi/IPOPT, is not installed: parity vs IPOPT unpinned).
+polyqp_s2.npz -- session-2/3 problem data with input box and state box
+                 (x_1..x_N), solved by the Goldfarb-Idnani oracle, KKT
+                 certified.
+
+The reference's source never travels: only these .npz data files are
+committed.  Re-run with:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+
+def _import_session1():
+    import matplotlib
+
+    matplotlib.use("Agg")
+    for name in ("casadi", "rcracers"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.path.insert(0, os.path.join(REF, "session_1"))
+    import FHC  # noqa: E402
+    import LinearSystem  # noqa: E402
+    import session1_sol  # noqa: E402
+    return FHC, LinearSystem, session1_sol
+
+
+def make_session1():
+    FHC, LinearSystem, s1 = _import_session1()
+    from scipy import linalg
+
+    out = {}
+    # --- FHC.main data (FHC.py:136-144)
+    A, B = FHC.get_dynamics_discrete(0.5)
+    C = np.array([[1], [-2 / 3]])
+    Q = np.matmul(C, C.T) + 1e-3 * np.eye(2, 2)
+    R = np.array([0.1])
+    P_f = Q
+    x0 = np.array([[10.], [10.]])
+    out.update(fhc_A=A, fhc_B=B, fhc_Q=Q, fhc_R=R, fhc_Pf=P_f, fhc_x0=x0)
+    Ac, Bc = FHC.get_dynamics_continuous()
+    out.update(fhc_Ac=Ac, fhc_Bc=Bc)
+    # --- ricatti_recursion (FHC.py:51-61)
+    for N in list(range(1, 11)) + [20]:
+        P, K = FHC.ricatti_recursion(A, B, Q, R, P_f, N)
+        out[f"fhc_P_N{N}"] = np.array(P)
+        out[f"fhc_K_N{N}"] = np.array(K)
+    # --- compare_term_cost values (FHC.py:117-127)
+    VN = []
+    for N in range(1, 10):
+        P_n, _ = FHC.ricatti_recursion(A, B, Q, R, P_f, N)
+        VN.append(np.squeeze(x0.T @ P_n[0] @ x0))
+    P_inf = linalg.solve_discrete_are(A, B, Q, R)
+    out["fhc_VN"] = np.array(VN)
+    out["fhc_Vinf"] = np.squeeze(x0.T @ P_inf @ x0)
+    out["fhc_Pinf"] = P_inf
+    # --- AutoCruising closed loop + predictions (FHC.py:64-101)
+    rng = np.random.default_rng(20261015)
+    xb = rng.uniform(-10, 10, size=(2, 8))
+    out["fhc_xbatch"] = xb
+    for N in (4, 6, 10):
+        _, gains = FHC.ricatti_recursion(A, B, Q, R, P_f, N)
+        sys_ = FHC.AutoCruising(A, B)
+        sys_.set_opti_gain(gains)
+        sys_.simulate(x0, sys_.control_law, 30)
+        out[f"fhc_sim_N{N}"] = sys_.x.copy()
+        preds = np.stack([sys_.prediction(sys_.x[:, :, t], sys_.pred, N) for t in range(30)])
+        out[f"fhc_pred_N{N}"] = preds
+        sys_.simulate(xb, sys_.control_law, 30)
+        out[f"fhc_simbatch_N{N}"] = sys_.x.copy()
+    K_inf = -np.linalg.inv(R + B.T @ P_inf @ B) @ B.T @ P_inf @ A
+    sys_ = FHC.AutoCruising(A, B)
+    sys_.set_opti_gain([K_inf] * 10)
+    sys_.simulate(x0, sys_.control_law, 30)
+    out["fhc_Kinf"] = K_inf
+    out["fhc_sim_inf"] = sys_.x.copy()
+    # --- session1_sol (session1_sol.py:44-91, 136-170)
+    A2, B2, Q2, R2 = s1.setup()
+    out.update(s1_A=A2, s1_B=B2, s1_Q=Q2, s1_R=R2)
+    x0s = 10 * np.ones(2)
+    for N in (4, 6, 10, 20):
+        P, K = s1.riccati_recursion(A2, B2, R2, Q2, Q2, N)
+        out[f"s1_P_N{N}"] = np.array(P)
+        out[f"s1_K_N{N}"] = np.array(K)
+
+        def f(x, u, A2=A2, B2=B2):
+            return A2 @ x + B2 @ u
+
+        def kappa(x, t, K=K):
+            return K[0] @ x
+
+        def kappa_pred(x, t, K=K):
+            return K[t] @ x
+
+        xcl, flag = s1.simulate(x0s, f, kappa, 30)
+        out[f"s1_sim_N{N}"] = xcl
+        out[f"s1_flag_N{N}"] = np.array(flag)
+        out[f"s1_pred_N{N}"] = np.stack([s1.simulate(xt, f, kappa_pred, N)[0] for xt in xcl])
+    # an unstable closed loop to exercise the instability flag (session1_sol.py:86-89)
+    _, Kbad = s1.riccati_recursion(A2, B2, R2, Q2, Q2, 1)
+    xbad, flag_bad = s1.simulate(x0s, lambda x, u: A2 @ x + B2 @ u, lambda x, t: -Kbad[0] @ x, 30)
+    out["s1_sim_bad"] = xbad
+    out["s1_flag_bad"] = np.array(flag_bad)
+    # --- LinearSystem.f on a batch (LinearSystem.py:16-18)
+    ls = LinearSystem.LinearSystem(A, B)
+    ub = rng.uniform(-1, 1, size=(1, 8))
+    out["ls_f_x"] = xb
+    out["ls_f_u"] = ub
+    out["ls_f_out"] = ls.f(xb, ub)
+    np.savez_compressed(os.path.join(HERE, "session1.npz"), **out)
+    return out
+
+
+def make_problems():
+    out = {}
+    for tag in ("session_2", "session_3"):
+        sys.path.insert(0, os.path.join(REF, tag))
+        import importlib
+
+        mod = importlib.import_module("problem")
+        p = mod.Problem()
+        for k in ("Ts", "p_min", "p_max", "v_min", "v_max", "u_min", "u_max", "N"):
+            out[f"{tag}_{k}"] = np.array(getattr(p, k))
+        for k in ("Q", "R", "A", "B"):
+            out[f"{tag}_{k}"] = np.asarray(getattr(p, k), dtype=float)
+        out[f"{tag}_n_state"] = np.array(p.n_state)
+        out[f"{tag}_n_input"] = np.array(p.n_input)
+        del sys.modules["problem"]
+        sys.path.pop(0)
+    np.savez_compressed(os.path.join(HERE, "problems.npz"), **out)
+    return out
+
+
+def make_boxqp_cfg2(s1):
+    from oracle import condense as oc
+    from oracle import qp as oq
+
+    A, B, Q, R, Pf = s1["fhc_A"], s1["fhc_B"], s1["fhc_Q"], s1["fhc_R"].reshape(1, 1), s1["fhc_Pf"]
+    N, nb = 20, 64
+    rng = np.random.default_rng(20261015 + 2)
+    X0 = rng.uniform(-10, 10, size=(nb, 2))
+    Hs, fs, Zs = [], [], []
+    for x0 in X0:
+        d = oc.condense(A, B, Q, R, Pf, N, x0=x0)
+        z_b = oq.box_qp_bvls(d["H"], d["f"], -1.0, 1.0)
+        z_a, _, _ = oq.box_qp(d["H"], d["f"], -np.ones(N), np.ones(N))
+        assert np.abs(z_a - z_b).max() < 1e-8, np.abs(z_a - z_b).max()
+        assert oq.kkt_box(d["H"], d["f"], -1.0, 1.0, z_a) < 1e-9
+        Hs.append(d["H"]); fs.append(d["f"]); Zs.append(z_a)
+    np.savez_compressed(os.path.join(HERE, "boxqp_cfg2.npz"), A=A, B=B, Q=Q, R=R, Pf=Pf, N=N,
+                        x0=X0, H=np.array(Hs), f=np.array(fs), z=np.array(Zs))
+
+
+def make_polyqp_s2(pr):
+    from oracle import condense as oc
+    from oracle import qp as oq
+
+    out = {}
+    for tag in ("session_2", "session_3"):
+        A, B = pr[f"{tag}_A"], pr[f"{tag}_B"]
+        Q, R, N = pr[f"{tag}_Q"], pr[f"{tag}_R"], int(pr[f"{tag}_N"])
+        xmin = np.array([pr[f"{tag}_p_min"], pr[f"{tag}_v_min"]], float)
+        xmax = np.array([pr[f"{tag}_p_max"], pr[f"{tag}_v_max"]], float)
+        umin, umax = float(pr[f"{tag}_u_min"]), float(pr[f"{tag}_u_max"])
+        rng = np.random.default_rng(20261015 + (22 if tag == "session_2" else 33))
+        X0 = np.column_stack([rng.uniform(-100, 0, 32), rng.uniform(-15, 20, 32)])
+        Zs, ok = [], []
+        for x0 in X0:
+            d = oc.condense(A, B, Q, R, Q, N, x0=x0)
+            G = np.vstack([d["Gam"], -d["Gam"]])
+            h = np.concatenate([np.tile(xmax, N) - d["xbar"], -np.tile(xmin, N) + d["xbar"]])
+            try:
+                z, lam, _ = oq.poly_qp(d["H"], d["f"], G, h, lb=np.full(N, umin), ub=np.full(N, umax))
+                C = np.vstack([G, np.eye(N), -np.eye(N)])
+                dd = np.concatenate([h, np.full(N, umax), -np.full(N, umin)])
+                assert oq.kkt_poly(d["H"], d["f"], C, dd, z, lam) < 1e-7
+                Zs.append(z); ok.append(True)
+            except ValueError:
+                Zs.append(np.full(N, np.nan)); ok.append(False)
+        out[f"{tag}_x0"] = X0
+        out[f"{tag}_z"] = np.array(Zs)
+        out[f"{tag}_feasible"] = np.array(ok)
+    np.savez_compressed(os.path.join(HERE, "polyqp_s2.npz"), **out)
+
+
+if __name__ == "__main__":
+    s1 = make_session1()
+    pr = make_problems()
+    make_boxqp_cfg2(s1)
+    make_polyqp_s2(pr)
+    print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

@@ -1,0 +1,71 @@
+"""CPU: the C-ABI library loads, exports every symbol include/mpcqp.h declares,
+and rejects bad arguments before touching the GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from model_predictive_control_amd import _native as nat
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "mpcqp.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mpcqp_[a-z_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return nat.load()
+
+
+def test_every_header_symbol_exported(lib):
+    syms = header_symbols()
+    assert len(syms) >= 10
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(nat.SIGNATURES), set(syms) ^ set(nat.SIGNATURES)
+
+
+def test_abi_version(lib):
+    assert lib.mpcqp_abi_version() == nat.ABI_VERSION == 1
+    assert lib.mpcqp_max_box_n(nat.F64) == 64
+
+
+def test_invalid_args_rejected_without_gpu(lib):
+    rc = lib.mpcqp_solve_box(7, 1, 4, None, 0, None, 0, None, 0, None, 0, None, None, 0, 0.0, None)
+    assert rc == -1 and b"dtype" in lib.mpcqp_last_error()
+    rc = lib.mpcqp_solve_box(nat.F64, 1, 65, 1, 0, 1, 0, None, 0, None, 0, 1, 1, 0, 0.0, None)
+    assert rc == -1 and b"n=65" in lib.mpcqp_last_error()
+    rc = lib.mpcqp_condense(nat.F64, 4, 17, 1, 10, 0, 1, 0, 1, 0, 1, 0, 1, 0, 1, 0, None, 0,
+                            None, 0, 1, None, None, None, None, None, None)
+    assert rc == -1 and b"nx=17" in lib.mpcqp_last_error()
+    rc = lib.mpcqp_condense(nat.F64, 4, 2, 1, 10, 0, None, 0, 1, 0, 1, 0, 1, 0, 1, 0, None, 0,
+                            None, 0, 1, None, None, None, None, None, None)
+    assert rc == -1 and b"required" in lib.mpcqp_last_error()
+    rc = lib.mpcqp_riccati(nat.F64, 1, 5, 1, 3, 1, 0, 1, 0, 1, 0, 1, 0, 1, 0, 1, 1, None)
+    assert rc == -1
+    rc = lib.mpcqp_solve_poly(nat.F64, 2, 10, 70, 1, 1, 0, 1, None, None, 0, None, None, 1, 1, 1,
+                              0, 0.0, 1, 1 << 20, None)
+    assert rc == -1 and b"m_total" in lib.mpcqp_last_error()
+    rc = lib.mpcqp_rollout(nat.F64, 1, 2, 1, 0, 1, 1, 1, 1, 1, None)
+    assert rc == -1
+    rc = lib.mpcqp_gemv(nat.F32, 1, 3, 3, 1.0, None, 0, 1, 0, 0.0, 1, 3, None)
+    assert rc == -1
+
+
+def test_zero_batch_is_noop(lib):
+    assert lib.mpcqp_solve_box(nat.F64, 0, 4, 1, 0, 1, 0, None, 0, None, 0, 1, 1, 0, 0.0, None) == 0
+
+
+def test_workspace_query(lib):
+    w = lib.mpcqp_solve_poly_workspace(nat.F64, 1024, 200, 40, 0)
+    assert w >= (200 * 200 * 2 + 40 * 200 + 40 * 41 // 2 + 1024 * 40) * 8
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(ImportError):
+        nat.load(str(tmp_path / "nope.so"))

@@ -1,0 +1,134 @@
+"""GPU parity: mpcqp_condense vs the explicit-matrix oracle (oracle/condense.py).
+
+Tolerances: fp64 1e-10 relative to the matrix scale; fp32 2e-5 relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+from model_predictive_control_amd import batched
+from oracle import condense as oc
+from oracle import session1 as s1
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev, dt=torch.float64):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+
+
+def _rand_plant(rng, nx, nu, N, tv, batch):
+    shapeA = (batch, N, nx, nx) if tv else (batch, nx, nx)
+    shapeB = (batch, N, nx, nu) if tv else (batch, nx, nu)
+    A = rng.normal(size=shapeA) * (0.9 / np.sqrt(nx)) + (np.eye(nx) * 0.3)
+    B = rng.normal(size=shapeB)
+    M = rng.normal(size=(nx, nx)); Q = M @ M.T / nx + 0.1 * np.eye(nx)
+    Mr = rng.normal(size=(nu, nu)); R = Mr @ Mr.T / nu + 0.5 * np.eye(nu)
+    Qf = 2.0 * Q
+    return A, B, Q, R, Qf
+
+
+def _check(out, ref, n, rtol):
+    H = batched.unpack_lower(out["H"], n).cpu().numpy()
+    for b, r in enumerate(ref):
+        s = max(1.0, np.abs(r["H"]).max())
+        assert np.abs(H[b] - r["H"]).max() <= rtol * s, ("H", b, np.abs(H[b] - r["H"]).max())
+        for k in ("F", "f", "Gam", "Phi", "xbar"):
+            if k in out:
+                got = out[k][b].cpu().numpy().reshape(r[k].shape)
+                sk = max(1.0, np.abs(r[k]).max())
+                assert np.abs(got - r[k]).max() <= rtol * sk, (k, b, np.abs(got - r[k]).max())
+
+
+@pytest.mark.parametrize("nx,nu,N", [(1, 1, 1), (2, 1, 20), (3, 2, 7), (4, 2, 30), (5, 3, 6),
+                                     (8, 2, 10), (12, 4, 12), (16, 1, 5)])
+@pytest.mark.parametrize("tv", [False, True])
+def test_condense_fp64_random(dev, nx, nu, N, tv):
+    rng = np.random.default_rng(100 * nx + 10 * nu + N + tv)
+    batch = 5
+    A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, tv, batch)
+    x0 = rng.normal(size=(batch, nx))
+    c = rng.normal(size=(batch, N, nx)) if tv else None
+    out = batched.condense(_t(A, dev), _t(B, dev), _t(Q, dev), _t(R, dev), _t(Qf, dev), N,
+                           x0=_t(x0, dev), c=None if c is None else _t(c, dev), tv=tv,
+                           outputs=("H", "F", "f", "Gam", "Phi", "xbar"))
+    torch.cuda.synchronize()
+    ref = [oc.condense(A[b], B[b], Q, R, Qf, N, x0=x0[b], c=None if c is None else c[b])
+           for b in range(batch)]
+    _check(out, ref, N * nu, 1e-10)
+
+
+def test_condense_shared_plant_per_instance_x0(dev):
+    A, B, Q, R, Pf, _ = s1.fhc_setup()
+    R = R.reshape(1, 1)
+    N, batch = 20, 33
+    rng = np.random.default_rng(5)
+    X0 = rng.uniform(-10, 10, (batch, 2))
+    out = batched.condense(_t(A, dev), _t(B, dev), _t(Q, dev), _t(R, dev), _t(Pf, dev), N,
+                           x0=_t(X0, dev), outputs=("H", "F", "f", "xbar"))
+    torch.cuda.synchronize()
+    ref = [oc.condense(A, B, Q, R, Pf, N, x0=X0[b]) for b in range(batch)]
+    _check(out, ref, N, 1e-11)
+
+
+def test_condense_r_shape_1_like_fhc(dev):
+    """FHC.py:141 passes R = np.array([0.1]) (shape (1,))."""
+    A, B, Q, R, Pf, x0 = s1.fhc_setup()
+    out = batched.condense(_t(A, dev), _t(B, dev), _t(Q, dev), _t(R, dev), _t(Pf, dev), 10,
+                           x0=_t(x0.ravel(), dev), outputs=("H", "f"))
+    ref = oc.condense(A, B, Q, R.reshape(1, 1), Pf, 10, x0=x0)
+    H = batched.unpack_lower(out["H"], 10)[0].cpu().numpy()
+    assert np.abs(H - ref["H"]).max() < 1e-11
+
+
+def test_condense_known_answer_riccati(dev, golden):
+    """-H^-1 f from the device condense equals the reference's Riccati rollout."""
+    g = golden("session1.npz")
+    A, B, Q, R, Pf, x0 = g["fhc_A"], g["fhc_B"], g["fhc_Q"], g["fhc_R"], g["fhc_Pf"], g["fhc_x0"]
+    N = 10
+    out = batched.condense(_t(A, dev), _t(B, dev), _t(Q, dev), _t(R.reshape(1, 1), dev),
+                           _t(Pf, dev), N, x0=_t(x0.ravel(), dev), outputs=("H", "f"))
+    H = batched.unpack_lower(out["H"], N)[0].cpu().numpy()
+    z = -np.linalg.solve(H, out["f"][0].cpu().numpy())
+    K = g["fhc_K_N10"]
+    x = x0.ravel()
+    for k in range(N):
+        u = K[k] @ x
+        assert abs(u[0] - z[k]) < 1e-10
+        x = A @ x + B @ u
+
+
+@pytest.mark.parametrize("nx,nu,N", [(2, 1, 20), (4, 2, 30), (12, 4, 40)])
+def test_condense_fp32(dev, nx, nu, N):
+    rng = np.random.default_rng(7 + nx)
+    batch = 4
+    A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, True, batch)
+    A *= 0.8
+    x0 = rng.normal(size=(batch, nx))
+    out = batched.condense(_t(A, dev, torch.float32), _t(B, dev, torch.float32),
+                           _t(Q, dev, torch.float32), _t(R, dev, torch.float32),
+                           _t(Qf, dev, torch.float32), N, x0=_t(x0, dev, torch.float32), tv=True,
+                           outputs=("H", "F", "f"))
+    torch.cuda.synchronize()
+    ref = [oc.condense(A[b], B[b], Q, R, Qf, N, x0=x0[b]) for b in range(batch)]
+    out = {k: v.double() for k, v in out.items()}
+    _check(out, ref, N * nu, 2e-5)
+
+
+def test_condense_large_batch_pointwise(dev):
+    """Config-2 shape at the bench batch: spot-check instances against the oracle."""
+    A, B, Q, R, Pf, _ = s1.fhc_setup()
+    R = R.reshape(1, 1)
+    N, batch = 20, 4096
+    rng = np.random.default_rng(20261017)
+    X0 = rng.uniform(-10, 10, (batch, 2))
+    Ab = np.broadcast_to(A, (batch, 2, 2))
+    Bb = np.broadcast_to(B, (batch, 2, 1))
+    out = batched.condense(_t(Ab, dev), _t(Bb, dev), _t(Q, dev), _t(R, dev), _t(Pf, dev), N,
+                           x0=_t(X0, dev), outputs=("H", "f"))
+    H0 = out["H"][0]
+    # identical plants -> identical H for every instance (bitwise)
+    assert torch.equal(out["H"], H0.expand_as(out["H"]))
+    for b in (0, 1, 777, 4095):
+        ref = oc.condense(A, B, Q, R, Pf, N, x0=X0[b])
+        assert np.abs(out["f"][b].cpu().numpy() - ref["f"]).max() < 1e-10 * max(1, np.abs(ref["f"]).max())

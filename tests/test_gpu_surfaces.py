@@ -1,0 +1,126 @@
+"""GPU: the reference-shaped call surfaces (FHC.py, session1_sol.py,
+LinearSystem.py, main.py MPCController) against the golden vectors captured
+from the reference itself."""
+import numpy as np
+import pytest
+import torch
+
+from model_predictive_control_amd import batched, fhc, mpc, session1
+from model_predictive_control_amd.parameters import VehicleParameters
+from oracle import bicycle as ob
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fhc_ricatti_recursion_matches_reference(dev, golden):
+    g = golden("session1.npz")
+    A, B, Q, R, Pf = g["fhc_A"], g["fhc_B"], g["fhc_Q"], g["fhc_R"], g["fhc_Pf"]
+    for N in list(range(1, 11)) + [20]:
+        P, K = fhc.ricatti_recursion(A, B, Q, R, Pf, N)
+        assert isinstance(P, list) and len(P) == N + 1 and len(K) == N
+        assert P[0].shape == (2, 2) and K[0].shape == (1, 2)
+        assert np.abs(np.array(P) - g[f"fhc_P_N{N}"]).max() < 1e-12
+        assert np.abs(np.array(K) - g[f"fhc_K_N{N}"]).max() < 1e-12
+
+
+def test_session1_riccati_argument_order(dev, golden):
+    g = golden("session1.npz")
+    A, B, Q, R = g["s1_A"], g["s1_B"], g["s1_Q"], g["s1_R"]
+    for N in (4, 6, 10, 20):
+        P, K = session1.riccati_recursion(A, B, R, Q, Q, N)
+        assert np.abs(np.array(P) - g[f"s1_P_N{N}"]).max() < 1e-12
+        assert np.abs(np.array(K) - g[f"s1_K_N{N}"]).max() < 1e-12
+
+
+def test_riccati_batched_many_plants(dev):
+    rng = np.random.default_rng(2)
+    b = 2000
+    ts = rng.uniform(0.1, 1.0, b)
+    A = np.stack([np.array([[1, t], [0, 1]]) for t in ts])
+    B = np.stack([np.array([[0], [-t]]) for t in ts])
+    Q = np.diag([1.0, 0.5]); R = np.array([[0.2]])
+    P, K = fhc.ricatti_recursion_batched(A, B, Q, R, Q, 15)
+    P = P.cpu().numpy(); K = K.cpu().numpy()
+    from oracle import session1 as s1
+    for i in (0, 5, 1999):
+        Pr, Kr = s1.ricatti_recursion(A[i], B[i], Q, R, Q, 15)
+        assert np.abs(P[i] - np.array(Pr)).max() < 1e-10 and np.abs(K[i] - np.array(Kr)).max() < 1e-10
+
+
+def test_autocruising_gpu_rollout_matches_reference(dev, golden):
+    g = golden("session1.npz")
+    A, B, Q, R, Pf, x0 = g["fhc_A"], g["fhc_B"], g["fhc_Q"], g["fhc_R"], g["fhc_Pf"], g["fhc_x0"]
+    for N in (4, 6, 10):
+        _, gains = fhc.ricatti_recursion(A, B, Q, R, Pf, N)
+        sys_ = fhc.AutoCruising(A, B)
+        sys_.set_opti_gain(gains)
+        sys_.simulate(x0, sys_.control_law, 30)
+        assert sys_.x.shape == (2, 1, 30)
+        assert np.abs(sys_.x - g[f"fhc_sim_N{N}"]).max() < 1e-11
+        sys_.simulate(g["fhc_xbatch"], sys_.control_law, 30)
+        assert np.abs(sys_.x - g[f"fhc_simbatch_N{N}"]).max() < 1e-11
+        for t in (0, 13, 29):
+            xp = sys_.prediction(g[f"fhc_sim_N{N}"][:, :, t], sys_.pred, N)
+            assert np.abs(xp - g[f"fhc_pred_N{N}"][t]).max() < 1e-11
+    sys_ = fhc.AutoCruising(A, B)
+    sys_.set_opti_gain([g["fhc_Kinf"]] * 10)
+    sys_.simulate(x0, sys_.control_law, 30)
+    assert np.abs(sys_.x - g["fhc_sim_inf"]).max() < 1e-11
+
+
+def test_compare_term_cost(dev, golden):
+    g = golden("session1.npz")
+    N_lst, VN, Vinf = fhc.compare_term_cost(g["fhc_A"], g["fhc_B"], g["fhc_Q"], g["fhc_R"],
+                                            g["fhc_Pf"], g["fhc_x0"])
+    assert N_lst == list(range(1, 10))
+    assert np.abs(VN - g["fhc_VN"]).max() < 1e-9
+    assert abs(Vinf - g["fhc_Vinf"]) < 1e-7 * abs(g["fhc_Vinf"])
+
+
+def test_rollout_many(dev):
+    A, B = fhc.get_dynamics_discrete(0.5)
+    K = np.array([[1.2, 2.3]])
+    rng = np.random.default_rng(1)
+    x0 = rng.normal(size=(10000, 2))
+    xs = batched.rollout(torch.tensor(A, device=dev), torch.tensor(B, device=dev),
+                         torch.tensor(K, device=dev), torch.tensor(x0, device=dev), 25)
+    Acl = A + B @ K
+    ref = x0.copy()
+    xs = xs.cpu().numpy()
+    for t in range(25):
+        assert np.abs(xs[t] - ref).max() < 1e-10 * max(1, np.abs(ref).max())
+        ref = ref @ Acl.T
+
+
+def test_mpc_controller_rti_matches_oracle(dev):
+    p = VehicleParameters()
+    N, ts = 30, 0.08
+    ctrl = mpc.MPCController(N, ts, p, sqp_iters=1)
+    x0 = np.array([0.3, -0.1, 0.0, 0.0])
+    sol = ctrl.solve(x0)
+    assert sol["x"].shape == (N * 2, 1) and sol["success"]
+    U = ctrl.reshape_input(sol)
+    assert U.shape == (N, 2)
+    Q = np.diag([1., 6., 0.2, 0.05])
+    Uref, _ = ob.rti_step(x0, np.zeros((N, 2)), ts, Q, 100 * Q, np.diag([1, 0.01]),
+                          np.array([-1, -0.384]), np.array([1, 0.384]), N)
+    assert np.abs(U - Uref).max() < 1e-6
+    # batched solve of many initial states == per-instance solves
+    ctrl2 = mpc.MPCController(N, ts, p, sqp_iters=1)
+    X0 = np.array([[0.3, -0.1, 0.0, 0.0], [0.5, 0.2, 0.3, 0.1], [-0.4, 0.1, -0.2, -0.2]])
+    zb = ctrl2.solve(X0)["x"]
+    for i in range(3):
+        Ur, _ = ob.rti_step(X0[i], np.zeros((N, 2)), ts, Q, 100 * Q, np.diag([1, 0.01]),
+                            np.array([-1, -0.384]), np.array([1, 0.384]), N)
+        assert np.abs(zb[i].reshape(N, 2) - Ur).max() < 1e-6
+    u0 = mpc.MPCController(N, ts, p)(x0)
+    assert u0.shape == (2,) and np.all(np.abs(u0) <= [1, 0.384 + 1e-12])
+
+
+def test_mpc_closed_loop_reaches_origin(dev):
+    p = VehicleParameters()
+    ctrl = mpc.MPCController(30, 0.08, p, sqp_iters=2)
+    from model_predictive_control_amd.bicycle import KinematicBicycle, fwd_euler
+    xs = mpc.simulate(np.array([0.3, -0.1, 0.0, 0.0]), fwd_euler(KinematicBicycle(p), 0.08), 60, ctrl)
+    assert xs.shape == (61, 4)
+    assert np.linalg.norm(xs[-1]) < np.linalg.norm(xs[0])
