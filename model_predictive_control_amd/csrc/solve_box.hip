@@ -13,13 +13,13 @@
 // primal-dual active set on non-M-matrix MPC Hessians).
 //
 // Linear algebra: the wavefront keeps M = SWEEP_F(H) -- H swept on the free
-// set F -- one row per lane in registers (lane i owns row i; n <= 64):
+// set F --  as an 8x8 grid of register blocks (sym2d.hpp):
 //     M_FF = -H_FF^{-1},  M_FA = H_FF^{-1} H_FA,  M_AA = Schur complement.
-// Moving one index between F and the active set is one (reverse) sweep: a
-// rank-1 update whose pivot row is broadcast with v_readlane (SGPR lane index,
-// no LDS).  The step directions of the dual method are simply column p of M,
-// and the subspace minimiser / active-set gradient is one mat-vec with M.
-#include "common.hpp"
+// Moving one index between F and the active set is one (reverse) sweep, a
+// rank-1 update whose pivot column is broadcast through LDS; the dual step
+// directions are column p of M; the subspace minimiser and the active-set
+// gradient are one mat-vec  s = M w,  w = (f_F, -z_A).
+#include "sym2d.hpp"
 
 namespace mpcqp {
 
@@ -36,182 +36,186 @@ struct BoxArgs {
   T tol;
 };
 
-// st: 0 free, 1 at lower, 2 at upper, 3 padding lane (never free)
-template <typename T, int NZ>
-__device__ __forceinline__ T select_reg(const T (&m)[NZ], int k) {
-  T r = T(0);
-#pragma unroll
-  for (int j = 0; j < NZ; ++j) r = (j == k) ? m[j] : r;
-  return r;
-}
+// st: 0 free, 1 at lower, 2 at upper, 3 padding row (never free)
+// Occupancy target: 4 waves/SIMD (16 per CU) up to BS = 3 (n <= 24), which
+// keeps a 4096-instance batch resident in one pass over the 256 CUs.
+template <int BS>
+struct BoxOcc {
+  static constexpr int w = BS <= 3 ? 4 : (BS <= 5 ? 2 : 1);
+};
 
-// Goodnight sweep (sigma = +1: k joins F) / reverse sweep (sigma = -1: k
-// leaves F) of the register-resident symmetric matrix, pivot k wave-uniform.
-// Returns the pivot value (sign-checked by the caller).
-template <typename T, int NZ>
-__device__ __forceinline__ T sweep(T (&m)[NZ], int k, T sigma, int lane, int n) {
-  const T mk = select_reg<T, NZ>(m, k);  // M_ik (own row, column k)
-  const T d = readlane(mk, k);           // M_kk
-  const T rd = T(1) / d;
-  const T a = mk * rd;
-  const T beta = (lane == k) ? (sigma * rd - T(1)) : -a;
-#pragma unroll
-  for (int j = 0; j < NZ; ++j) {
-    if (j < n) m[j] = fma(beta, readlane(m[j], k), m[j]);
-  }
-  const T delta = (lane == k) ? (-rd - sigma) : sigma * a;
-#pragma unroll
-  for (int j = 0; j < NZ; ++j) m[j] = (j == k) ? m[j] + delta : m[j];
-  return d;
-}
-
-template <typename T, int NZ>
-__global__ __launch_bounds__(64) void box_gi_kernel(BoxArgs<T> a) {
+template <typename T, int BS>
+__global__ __launch_bounds__(64, BoxOcc<BS>::w) void box_gi_kernel(BoxArgs<T> a) {
+  using S2 = Sym2D<T, BS>;
+  constexpr int NMAX = S2::NMAX;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  T* Ps = reinterpret_cast<T*>(smem_raw);
+  T* buf = reinterpret_cast<T*>(smem_raw);  // Sym2D scratch
+  T* fs = buf + S2::BUF;                    // per-row data by row index
+  T* lbs = fs + NMAX;
+  T* ubs = lbs + NMAX;
+  T* zs = ubs + NMAX;
+  T* Ps = zs + NMAX;                        // packed H
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = a.n;
-  const bool valid = lane < n;
   const int P = n * (n + 1) / 2;
 
-  // ---- stage the packed lower triangle through LDS (coalesced HBM reads)
-  {
-    constexpr int MAXP = (NZ * (NZ + 1) / 2 + kWave - 1) / kWave;
-    const T* Hb = a.H + (int64_t)b * a.sH;
-    T tmp[MAXP];
-#pragma unroll
-    for (int t = 0; t < MAXP; ++t) {
-      const int e = lane + t * kWave;
-      tmp[t] = (e < P) ? Hb[e] : T(0);
-    }
-#pragma unroll
-    for (int t = 0; t < MAXP; ++t) {
-      const int e = lane + t * kWave;
-      if (e < P) Ps[e] = tmp[t];
-    }
-  }
-  T fi = T(0), lbi = -Lim<T>::inf(), ubi = Lim<T>::inf();
-  if (valid) {
-    fi = a.f[(int64_t)b * a.sf + lane];
-    if (a.lb) lbi = a.lb[(int64_t)b * a.slb + lane];
-    if (a.ub) ubi = a.ub[(int64_t)b * a.sub + lane];
+  stage_packed<T, NMAX*(NMAX + 1) / 2>(a.H + (int64_t)b * a.sH, Ps, P, lane);
+  bool nonfinite = false, badbox = false;
+  if (lane < NMAX) {
+    const int i = lane;
+    const bool v = i < n;
+    const T fi = v ? a.f[(int64_t)b * a.sf + i] : T(0);
+    const T li = (v && a.lb) ? a.lb[(int64_t)b * a.slb + i] : -Lim<T>::inf();
+    const T ui = (v && a.ub) ? a.ub[(int64_t)b * a.sub + i] : Lim<T>::inf();
+    fs[i] = fi;
+    lbs[i] = li;
+    ubs[i] = ui;
+    nonfinite = v && !finite(fi);
+    badbox = v && (!(li <= ui) || li == Lim<T>::inf() || ui == -Lim<T>::inf());
   }
   __syncthreads();
 
-  T m[NZ];
-  bool nonfinite = valid && !finite(fi);
+  Sym2D<T, BS> M;
+  M.init(lane);
+  M.load_packed(Ps, n, nonfinite);
+  T zr[BS], gr[BS];
+  int st[BS];
 #pragma unroll
-  for (int j = 0; j < NZ; ++j) {
-    T v = T(0);
-    if (valid && j < n) {
-      const int idx = (j <= lane) ? lane * (lane + 1) / 2 + j : j * (j + 1) / 2 + lane;
-      v = Ps[idx];
-      nonfinite |= !finite(v);
-    }
-    m[j] = v;
+  for (int r = 0; r < BS; ++r) {
+    st[r] = (M.bi * BS + r < n) ? 0 : 3;
+    zr[r] = T(0);
+    gr[r] = T(0);
   }
-  const bool badbox = valid && (!(lbi <= ubi) || lbi == Lim<T>::inf() || ubi == -Lim<T>::inf());
 
   int code = MPCQP_STATUS_MAXITER;
   int iters = 0;
-  T zi = T(0);
-  int st = valid ? 0 : 3;
   const T tol = a.tol;
+  const int max_iter = a.max_iter;
 
   if (__any(nonfinite)) {
     code = MPCQP_STATUS_NONFINITE;
-    zi = __builtin_nan("");
     goto done;
   }
   if (__any(badbox)) {
     code = MPCQP_STATUS_INFEASIBLE;
-    zi = __builtin_nan("");
     goto done;
   }
 
   // ---- M = SWEEP_all(H) = -H^{-1}
   for (int k = 0; k < n; ++k) {
-    const T d = sweep<T, NZ>(m, k, T(1), lane, n);
+    const T d = M.sweep(k, T(1), buf);
     if (!(d > T(0))) {
       code = MPCQP_STATUS_NOT_CONVEX;
-      zi = __builtin_nan("");
       goto done;
     }
   }
 
   {
-    T gi = T(0);
-    // subspace minimiser for the current (F, A): z_F = M_FF f_F - M_FA z_A,
-    // g_A = f_A - M_AF f_F + M_AA z_A  ==  with w = (f_F, -z_A): s = M w.
+    // subspace minimiser for (F, A): with w = (f_F, -z_A), s = M w gives
+    // z_F = s_F and the active-set gradient g_A = f_A - s_A.
     auto refresh = [&]() {
-      const T zA = (st == 1) ? lbi : ((st == 2) ? ubi : T(0));
-      const T w = (st == 0) ? fi : -zA;
-      T s = T(0);
+      T w[BS], s[BS];
 #pragma unroll
-      for (int j = 0; j < NZ; ++j)
-        if (j < n) s = fma(m[j], readlane(w, j), s);
-      zi = (st == 0) ? s : zA;
-      gi = (st == 0) ? T(0) : fi - s;
+      for (int r = 0; r < BS; ++r) {
+        const int i = M.bi * BS + r;
+        const T zA = (st[r] == 1) ? lbs[i] : ((st[r] == 2) ? ubs[i] : T(0));
+        w[r] = (st[r] == 0) ? fs[i] : -zA;
+        zr[r] = zA;
+      }
+      M.matvec(w, buf, s);
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        const int i = M.bi * BS + r;
+        gr[r] = (st[r] == 0) ? T(0) : fs[i] - s[r];
+        zr[r] = (st[r] == 0) ? s[r] : zr[r];
+      }
     };
     refresh();
 
-    const int max_iter = a.max_iter;
     while (true) {
       // most violated free variable (relative to the bound's magnitude)
       T viol = -Lim<T>::inf();
-      if (st == 0) {
-        const T vl = (lbi - zi) / (T(1) + fabs(lbi));
-        const T vu = (zi - ubi) / (T(1) + fabs(ubi));
-        viol = fmax(vl, vu);
+      int p = 0;
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        if (st[r] == 0) {
+          const int i = M.bi * BS + r;
+          const T li = lbs[i], ui = ubs[i];
+          const T vl = finite(li) ? (li - zr[r]) / (T(1) + fabs(li)) : -Lim<T>::inf();
+          const T vu = finite(ui) ? (zr[r] - ui) / (T(1) + fabs(ui)) : -Lim<T>::inf();
+          const T v = fmax(vl, vu);
+          if (v > viol) {
+            viol = v;
+            p = i;
+          }
+        }
       }
-      int p = lane;
-      wave_argmax(viol, p);
+      blocks_argmax(viol, p);
       p = uniform(p);
-      if (!(viol > tol)) {
+      if (!(readlane(viol, 0) > tol)) {
         code = MPCQP_STATUS_OPTIMAL;
         break;
       }
-      const T zp0 = readlane(zi, p);
-      const T lbp = readlane(lbi, p), ubp = readlane(ubi, p);
-      const int side = (zp0 < lbp) ? 1 : 2;
+      publish<T, BS>(zr, zs, M.bi, M.bj);
+      __syncthreads();
+      const T lbp = lbs[p], ubp = ubs[p];
+      T zp = zs[p];
+      __syncthreads();
+      const int side = (zp < lbp) ? 1 : 2;
       const T tgt = (side == 1) ? lbp : ubp;
-      T mu = (st == 1) ? gi : ((st == 2) ? -gi : T(0));
+      T mu[BS];
+#pragma unroll
+      for (int r = 0; r < BS; ++r) mu[r] = (st[r] == 1) ? gr[r] : ((st[r] == 2) ? -gr[r] : T(0));
       bool added = false;
       while (!added) {
         if (++iters > max_iter) goto done;
-        const T c = select_reg<T, NZ>(m, p);  // M_ip
-        const T mpp = readlane(c, p);         // M_pp < 0 (p free)
-        const T zp = readlane(zi, p);
+        T c[BS], cc[BS];
+        const T mpp = M.column(p, buf, c, cc);  // c[r] = M_ip; M_pp < 0 (p free)
+        const T rm = T(1) / mpp;
         const T sgn = (tgt > zp) ? T(1) : T(-1);
         const T t2 = fabs(tgt - zp);
-        const T cr = c / mpp;
-        const T dmu = ((st == 1) ? -cr : ((st == 2) ? cr : T(0))) * sgn;
-        T ti = ((st == 1 || st == 2) && dmu < T(0)) ? mu / (-dmu) : Lim<T>::inf();
-        int k = lane;
-        wave_argmin(ti, k);
+        T ti = Lim<T>::inf();
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+          c[r] *= rm;  // c/M_pp: dz_F per unit step
+          const T dmu = ((st[r] == 1) ? -c[r] : ((st[r] == 2) ? c[r] : T(0))) * sgn;
+          const T t = ((st[r] == 1 || st[r] == 2) && dmu < T(0)) ? mu[r] / (-dmu)
+                                                                  : Lim<T>::inf();
+          if (t < ti) {
+            ti = t;
+            k = M.bi * BS + r;
+          }
+        }
+        blocks_argmin(ti, k);
         k = uniform(k);
+        ti = readlane(ti, 0);
         if (ti < t2) {
           // partial step: the multiplier of bound k reaches zero -> drop k
-          if (st == 0) zi = fma(sgn * ti, cr, zi);
-          mu = fma(ti, dmu, mu);
-          if (lane == k) {
-            mu = T(0);
-            st = 0;
+#pragma unroll
+          for (int r = 0; r < BS; ++r) {
+            const T dmu = ((st[r] == 1) ? -c[r] : ((st[r] == 2) ? c[r] : T(0))) * sgn;
+            if (st[r] == 0) zr[r] = fma(sgn * ti, c[r], zr[r]);
+            mu[r] = fma(ti, dmu, mu[r]);
+            if (M.bi * BS + r == k) {
+              mu[r] = T(0);
+              st[r] = 0;
+            }
           }
-          const T d = sweep<T, NZ>(m, k, T(1), lane, n);
+          const T d = M.sweep(k, T(1), buf);
           if (!(d > T(0))) {
             code = MPCQP_STATUS_NOT_CONVEX;
             goto done;
           }
+          zp = fma(sgn, ti, zp);  // row p moves by sgn*ti*(M_pp/M_pp)
         } else {
           // full step: bound p becomes active
-          if (st == 0) zi = fma(sgn * t2, cr, zi);
-          if (lane == p) {
-            zi = tgt;
-            st = side;
+#pragma unroll
+          for (int r = 0; r < BS; ++r) {
+            if (M.bi * BS + r == p) st[r] = side;
           }
-          const T d = sweep<T, NZ>(m, p, T(-1), lane, n);
+          const T d = M.sweep(p, T(-1), buf);
           if (!(d < T(0))) {
             code = MPCQP_STATUS_NOT_CONVEX;
             goto done;
@@ -222,18 +226,32 @@ __global__ __launch_bounds__(64) void box_gi_kernel(BoxArgs<T> a) {
       }
     }
     // project free variables that sit within tol outside their bounds
-    zi = fmin(fmax(zi, lbi), ubi);
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      zr[r] = fmin(fmax(zr[r], lbs[i]), ubs[i]);
+    }
   }
 
 done:
-  if (valid) a.z[(int64_t)b * n + lane] = zi;
+  if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
+#pragma unroll
+    for (int r = 0; r < BS; ++r) zr[r] = __builtin_nan("");
+  }
+  if (M.bj == 0) {
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      if (i < n) a.z[(int64_t)b * n + i] = zr[r];
+    }
+  }
   if (lane == 0) a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
 }
 
-template <typename T, int NZ>
+template <typename T, int BS>
 static int launch_box(const BoxArgs<T>& a, hipStream_t st) {
-  const size_t bytes = (size_t)(a.n * (a.n + 1) / 2) * sizeof(T);
-  hipLaunchKernelGGL((box_gi_kernel<T, NZ>), dim3(a.batch), dim3(kWave), bytes, st, a);
+  const size_t bytes = (size_t)(Sym2D<T, BS>::BUF + 4 * 8 * BS + a.n * (a.n + 1) / 2) * sizeof(T);
+  hipLaunchKernelGGL((box_gi_kernel<T, BS>), dim3(a.batch), dim3(kWave), bytes, st, a);
   MPCQP_CHECK_LAUNCH("box_gi_kernel");
   return MPCQP_OK;
 }
@@ -249,12 +267,16 @@ static int solve_box_t(int batch, int n, const void* H, int64_t sH, const void* 
   a.z = (T*)z; a.status = status;
   a.max_iter = max_iter > 0 ? max_iter : 3 * n + 30;
   a.tol = tol > 0 ? (T)tol : (sizeof(T) == 8 ? (T)1e-12 : (T)1e-6);
-  if (n <= 8) return launch_box<T, 8>(a, st);
-  if (n <= 16) return launch_box<T, 16>(a, st);
-  if (n <= 24) return launch_box<T, 24>(a, st);
-  if (n <= 32) return launch_box<T, 32>(a, st);
-  if (n <= 48) return launch_box<T, 48>(a, st);
-  return launch_box<T, 64>(a, st);
+  switch ((n + 7) / 8) {
+    case 1: return launch_box<T, 1>(a, st);
+    case 2: return launch_box<T, 2>(a, st);
+    case 3: return launch_box<T, 3>(a, st);
+    case 4: return launch_box<T, 4>(a, st);
+    case 5: return launch_box<T, 5>(a, st);
+    case 6: return launch_box<T, 6>(a, st);
+    case 7: return launch_box<T, 7>(a, st);
+    default: return launch_box<T, 8>(a, st);
+  }
 }
 
 }  // namespace mpcqp

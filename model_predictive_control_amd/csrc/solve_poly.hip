@@ -18,39 +18,15 @@
 //   z  = z0 - Ut' y                               (gemv, transposed)
 //
 // Dual range active set (Goldfarb-Idnani written in the row space): the
-// wavefront keeps W = SWEEP_A(M), M swept on the active rows, one row per
-// lane.  With w = (s0 - b on A, 0 elsewhere), v = W w gives y_A = -v_A and
+// wavefront keeps W = SWEEP_A(M), M swept on the active rows, as an 8x8
+// grid of register blocks (sym2d.hpp).  With w = (s0 - b on A, 0 elsewhere), v = W w gives y_A = -v_A and
 // the inactive row values s_I = s0_I - v_I.  Adding row p is a sweep with
 // pivot W_pp (its Schur complement -- zero when p depends on the active rows,
 // in which case a pure dual step drops rows first), dropping row k is a
 // reverse sweep.  Same register-resident sweep machinery as solve_box.hip.
-#include "common.hpp"
+#include "sym2d.hpp"
 
 namespace mpcqp {
-
-template <typename T, int NZ>
-__device__ __forceinline__ T select_reg_p(const T (&m)[NZ], int k) {
-  T r = T(0);
-#pragma unroll
-  for (int j = 0; j < NZ; ++j) r = (j == k) ? m[j] : r;
-  return r;
-}
-
-template <typename T, int NZ>
-__device__ __forceinline__ T sweep_p(T (&m)[NZ], int k, T sigma, int lane, int n) {
-  const T mk = select_reg_p<T, NZ>(m, k);
-  const T d = readlane(mk, k);
-  const T rd = T(1) / d;
-  const T a = mk * rd;
-  const T beta = (lane == k) ? (sigma * rd - T(1)) : -a;
-#pragma unroll
-  for (int j = 0; j < NZ; ++j)
-    if (j < n) m[j] = fma(beta, readlane(m[j], k), m[j]);
-  const T delta = (lane == k) ? (-rd - sigma) : sigma * a;
-#pragma unroll
-  for (int j = 0; j < NZ; ++j) m[j] = (j == k) ? m[j] + delta : m[j];
-  return d;
-}
 
 template <typename T>
 struct DualArgs {
@@ -65,139 +41,170 @@ struct DualArgs {
   T tol;
 };
 
-template <typename T, int NZ>
+// st: 0 inactive, 1 at lower, 2 at upper, 3 padding row
+template <typename T, int BS>
 __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
+  using S2 = Sym2D<T, BS>;
+  constexpr int NMAX = S2::NMAX;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  T* Ps = reinterpret_cast<T*>(smem_raw);
+  T* buf = reinterpret_cast<T*>(smem_raw);
+  T* lis = buf + S2::BUF;
+  T* uis = lis + NMAX;
+  T* mds = uis + NMAX;
+  T* ss = mds + NMAX;
+  T* Ps = ss + NMAX;
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = a.mt;
-  const bool valid = lane < n;
   const int P = n * (n + 1) / 2;
-  {
-    constexpr int MAXP = (NZ * (NZ + 1) / 2 + kWave - 1) / kWave;
-    const T* Mb = a.M + (int64_t)b * a.sM;
-    T tmp[MAXP];
+  stage_packed<T, NMAX*(NMAX + 1) / 2>(a.M + (int64_t)b * a.sM, Ps, P, lane);
+
+  Sym2D<T, BS> W;
+  W.init(lane);
+  T s0[BS], li[BS], ui[BS], yi[BS], si[BS];
+  int st[BS];
+  bool nonfinite = false, badbox = false;
 #pragma unroll
-    for (int t = 0; t < MAXP; ++t) {
-      const int e = lane + t * kWave;
-      tmp[t] = (e < P) ? Mb[e] : T(0);
+  for (int r = 0; r < BS; ++r) {
+    const int i = W.bi * BS + r;
+    const bool v = i < n;
+    s0[r] = v ? a.s0[(int64_t)b * a.sS0 + i] : T(0);
+    li[r] = -Lim<T>::inf();
+    ui[r] = Lim<T>::inf();
+    if (v) {
+      if (i < a.m1) {
+        if (a.l1) li[r] = a.l1[(int64_t)b * a.s1 + i];
+        if (a.u1) ui[r] = a.u1[(int64_t)b * a.s1 + i];
+      } else {
+        if (a.l2) li[r] = a.l2[i - a.m1];
+        if (a.u2) ui[r] = a.u2[i - a.m1];
+      }
     }
-#pragma unroll
-    for (int t = 0; t < MAXP; ++t) {
-      const int e = lane + t * kWave;
-      if (e < P) Ps[e] = tmp[t];
-    }
+    st[r] = v ? 0 : 3;
+    yi[r] = T(0);
+    si[r] = s0[r];
+    nonfinite |= v && !finite(s0[r]);
+    badbox |= v && (!(li[r] <= ui[r]) || li[r] == Lim<T>::inf() || ui[r] == -Lim<T>::inf());
   }
-  T s0 = T(0), li = -Lim<T>::inf(), ui = Lim<T>::inf();
-  if (valid) {
-    s0 = a.s0[(int64_t)b * a.sS0 + lane];
-    if (lane < a.m1) {
-      if (a.l1) li = a.l1[(int64_t)b * a.s1 + lane];
-      if (a.u1) ui = a.u1[(int64_t)b * a.s1 + lane];
-    } else {
-      if (a.l2) li = a.l2[lane - a.m1];
-      if (a.u2) ui = a.u2[lane - a.m1];
-    }
-  }
+  publish<T, BS>(li, lis, W.bi, W.bj);
+  publish<T, BS>(ui, uis, W.bi, W.bj);
   __syncthreads();
-  T m[NZ];
-  bool nonfinite = valid && !finite(s0);
-#pragma unroll
-  for (int j = 0; j < NZ; ++j) {
-    T v = T(0);
-    if (valid && j < n) {
-      const int idx = (j <= lane) ? lane * (lane + 1) / 2 + j : j * (j + 1) / 2 + lane;
-      v = Ps[idx];
-      nonfinite |= !finite(v);
-    }
-    m[j] = v;
-  }
-  const T mdiag = select_reg_p<T, NZ>(m, lane);
-  const bool badbox = valid && (!(li <= ui) || li == Lim<T>::inf() || ui == -Lim<T>::inf());
+  W.load_packed(Ps, n, nonfinite);
+  // diagonal of M by row (dependency test scale)
+  for (int i = lane; i < n; i += kWave) mds[i] = Ps[i * (i + 1) / 2 + i];
+  __syncthreads();
   int code = MPCQP_STATUS_MAXITER;
   int iters = 0;
-  int st = valid ? 0 : 3;  // 0 inactive, 1 at lower, 2 at upper, 3 padding
-  T yi = T(0), si = s0;
   const T tol = a.tol;
   const T dep_tol = sizeof(T) == 8 ? T(1e-10) : T(1e-5);
+  const int max_iter = a.max_iter;
   if (__any(nonfinite)) {
     code = MPCQP_STATUS_NONFINITE;
-    yi = __builtin_nan("");
     goto done;
   }
   if (__any(badbox)) {
     code = MPCQP_STATUS_INFEASIBLE;
-    yi = __builtin_nan("");
     goto done;
   }
   {
+    // w = (s0 - b on active rows, 0 elsewhere);  v = W w;
+    // active: y = -v, s = bound;  inactive: s = s0 - v
     auto refresh = [&]() {
-      const T bnd = (st == 1) ? li : ((st == 2) ? ui : T(0));
-      const T w = (st == 1 || st == 2) ? s0 - bnd : T(0);
-      T v = T(0);
+      T w[BS], v[BS];
 #pragma unroll
-      for (int j = 0; j < NZ; ++j)
-        if (j < n) v = fma(m[j], readlane(w, j), v);
-      const bool act = (st == 1 || st == 2);
-      yi = act ? -v : T(0);
-      si = act ? bnd : s0 - v;
+      for (int r = 0; r < BS; ++r) {
+        const bool act = st[r] == 1 || st[r] == 2;
+        const T bnd = (st[r] == 1) ? li[r] : ui[r];
+        w[r] = act ? s0[r] - bnd : T(0);
+      }
+      W.matvec(w, buf, v);
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        const bool act = st[r] == 1 || st[r] == 2;
+        const T bnd = (st[r] == 1) ? li[r] : ui[r];
+        yi[r] = act ? -v[r] : T(0);
+        si[r] = act ? bnd : s0[r] - v[r];
+      }
     };
-    const int max_iter = a.max_iter;
     while (true) {
       T viol = -Lim<T>::inf();
-      if (st == 0) {
-        const T vl = finite(li) ? (li - si) / (T(1) + fabs(li)) : -Lim<T>::inf();
-        const T vu = finite(ui) ? (si - ui) / (T(1) + fabs(ui)) : -Lim<T>::inf();
-        viol = fmax(vl, vu);
+      int p = 0;
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        if (st[r] == 0) {
+          const T vl = finite(li[r]) ? (li[r] - si[r]) / (T(1) + fabs(li[r])) : -Lim<T>::inf();
+          const T vu = finite(ui[r]) ? (si[r] - ui[r]) / (T(1) + fabs(ui[r])) : -Lim<T>::inf();
+          const T vv = fmax(vl, vu);
+          if (vv > viol) {
+            viol = vv;
+            p = W.bi * BS + r;
+          }
+        }
       }
-      int p = lane;
-      wave_argmax(viol, p);
+      blocks_argmax(viol, p);
       p = uniform(p);
-      if (!(viol > tol)) {
+      if (!(readlane(viol, 0) > tol)) {
         code = MPCQP_STATUS_OPTIMAL;
         break;
       }
-      const T sp0 = readlane(si, p);
-      const T lp = readlane(li, p), up = readlane(ui, p);
+      publish<T, BS>(si, ss, W.bi, W.bj);
+      __syncthreads();
+      const T sp0 = ss[p];
+      const T lp = lis[p], up = uis[p];
+      const T mpp = mds[p];
+      __syncthreads();
       const int side = (sp0 < lp) ? 1 : 2;
       const T tgt = (side == 1) ? lp : up;
       const T ysgn = (side == 1) ? T(-1) : T(1);
-      const T mpp = readlane(mdiag, p);
       T sp = sp0;
       bool added = false;
       while (!added) {
         if (++iters > max_iter) goto done;
-        const T c = select_reg_p<T, NZ>(m, p);  // W_ip
-        const T wpp = readlane(c, p);
+        T c[BS], cc[BS];
+        const T wpp = W.column(p, buf, c, cc);  // c[r] = W_ip
         const bool dep = !(wpp > dep_tol * fmax(mpp, T(1e-300)));
-        const T dy = -c * ysgn;  // dy_A per unit step
         T ti = Lim<T>::inf();
-        if (st == 2 && dy < T(0)) ti = yi / (-dy);
-        if (st == 1 && dy > T(0)) ti = (-yi) / dy;
-        int k = lane;
-        wave_argmin(ti, k);
+        int k = 0;
+        T dy[BS];
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+          dy[r] = -c[r] * ysgn;
+          T t = Lim<T>::inf();
+          if (st[r] == 2 && dy[r] < T(0)) t = yi[r] / (-dy[r]);
+          if (st[r] == 1 && dy[r] > T(0)) t = (-yi[r]) / dy[r];
+          if (t < ti) {
+            ti = t;
+            k = W.bi * BS + r;
+          }
+        }
+        blocks_argmin(ti, k);
         k = uniform(k);
+        ti = readlane(ti, 0);
         const T t2 = dep ? Lim<T>::inf() : fabs(sp - tgt) / wpp;
         if (!(ti < Lim<T>::inf()) && !(t2 < Lim<T>::inf())) {
           code = MPCQP_STATUS_INFEASIBLE;
           goto done;
         }
         if (ti < t2) {
-          if (st == 1 || st == 2) yi = fma(ti, dy, yi);
-          if (!dep) sp = sp - wpp * ysgn * ti;
-          if (lane == k) {
-            yi = T(0);
-            st = 0;
+#pragma unroll
+          for (int r = 0; r < BS; ++r) {
+            if (st[r] == 1 || st[r] == 2) yi[r] = fma(ti, dy[r], yi[r]);
+            if (W.bi * BS + r == k) {
+              yi[r] = T(0);
+              st[r] = 0;
+            }
           }
-          sweep_p<T, NZ>(m, k, T(-1), lane, n);
+          if (!dep) sp = sp - wpp * ysgn * ti;
+          W.sweep(k, T(-1), buf);
         } else {
-          const T d = sweep_p<T, NZ>(m, p, T(1), lane, n);
+          const T d = W.sweep(p, T(1), buf);
           if (!(d > T(0))) {
             code = MPCQP_STATUS_NOT_CONVEX;
             goto done;
           }
-          if (lane == p) st = side;
+#pragma unroll
+          for (int r = 0; r < BS; ++r)
+            if (W.bi * BS + r == p) st[r] = side;
           refresh();
           added = true;
         }
@@ -205,7 +212,17 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
     }
   }
 done:
-  if (valid && a.y) a.y[(int64_t)b * n + lane] = yi;
+  if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
+#pragma unroll
+    for (int r = 0; r < BS; ++r) yi[r] = __builtin_nan("");
+  }
+  if (a.y && W.bj == 0) {
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = W.bi * BS + r;
+      if (i < n) a.y[(int64_t)b * n + i] = yi[r];
+    }
+  }
   if (lane == 0) a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
 }
 
@@ -325,10 +342,10 @@ static PolyWs poly_ws(size_t es, int batch, int n, int mt) {
   return w;
 }
 
-template <typename T, int NZ>
+template <typename T, int BS>
 static void launch_dual(const DualArgs<T>& a, hipStream_t st) {
-  const size_t bytes = (size_t)(a.mt * (a.mt + 1) / 2) * sizeof(T);
-  hipLaunchKernelGGL((dual_range_kernel<T, NZ>), dim3(a.batch), dim3(kWave), bytes, st, a);
+  const size_t bytes = (size_t)(Sym2D<T, BS>::BUF + 4 * 8 * BS + a.mt * (a.mt + 1) / 2) * sizeof(T);
+  hipLaunchKernelGGL((dual_range_kernel<T, BS>), dim3(a.batch), dim3(kWave), bytes, st, a);
 }
 
 template <typename T>
@@ -382,12 +399,16 @@ static int solve_poly_t(int batch, int n, int m, const void* H, const void* f, i
   a.y = (T*)y; a.status = status;
   a.max_iter = max_iter > 0 ? max_iter : 4 * mt + 40;
   a.tol = tol > 0 ? (T)tol : (sizeof(T) == 8 ? (T)1e-12 : (T)1e-6);
-  if (mt <= 8) launch_dual<T, 8>(a, st);
-  else if (mt <= 16) launch_dual<T, 16>(a, st);
-  else if (mt <= 24) launch_dual<T, 24>(a, st);
-  else if (mt <= 32) launch_dual<T, 32>(a, st);
-  else if (mt <= 48) launch_dual<T, 48>(a, st);
-  else launch_dual<T, 64>(a, st);
+  switch ((mt + 7) / 8) {
+    case 1: launch_dual<T, 1>(a, st); break;
+    case 2: launch_dual<T, 2>(a, st); break;
+    case 3: launch_dual<T, 3>(a, st); break;
+    case 4: launch_dual<T, 4>(a, st); break;
+    case 5: launch_dual<T, 5>(a, st); break;
+    case 6: launch_dual<T, 6>(a, st); break;
+    case 7: launch_dual<T, 7>(a, st); break;
+    default: launch_dual<T, 8>(a, st); break;
+  }
   MPCQP_CHECK_LAUNCH("dual_range_kernel");
   // z = z0 - Ut' y
   hipLaunchKernelGGL(gemv_t_kernel<T>, dim3(batch), dim3(kWave), (size_t)mt * sizeof(T), st, mt,

@@ -1,0 +1,216 @@
+// sym2d.hpp -- a symmetric n x n matrix (n <= 8*BS) distributed over one
+// wavefront as an 8 x 8 grid of BS x BS register blocks, plus the operations
+// the active-set kernels need: Goodnight sweeps, column extraction and a
+// mat-vec.  Lane l owns rows bi*BS..bi*BS+BS-1 and columns bj*BS..bj*BS+BS-1
+// with bi = l >> 3, bj = l & 7; every lane works on every step (no idle
+// lanes as in a row-per-lane layout), pivot columns travel through a 64-entry
+// LDS buffer (broadcast reads) and row sums through DPP butterflies.
+//
+// Vectors indexed by matrix row ("row-block layout") live in T v[BS] on every
+// lane, replicated across the 8 lanes of a row block (bj = 0..7).
+#pragma once
+#include "common.hpp"
+
+namespace mpcqp {
+
+// ---------------------------------------------------------------- DPP
+// dpp_ctrl codes (gfx9 encoding): quad_perm xor1 = 0xB1, xor2 = 0x4E,
+// row_half_mirror = 0x141 (lane i <-> 7-i within 8), row_ror:8 = 0x128
+// (i <-> i+8 within a 16-lane row, i.e. xor 8).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+
+// Sum over the 8 lanes of a row block (lanes bi*8 .. bi*8+7); every lane of
+// the block receives the total.
+template <typename T>
+__device__ __forceinline__ T rowblock_sum(T v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  return v;
+}
+
+// Reduce a (value, index) pair across the 8 row blocks (lanes differing in
+// bits 3..5).  Lanes within one row block hold identical candidates.
+// Arg-max: larger value wins, ties to the smaller index.  NaN never wins.
+template <typename T>
+__device__ __forceinline__ void blocks_argmax(T& v, int& idx) {
+  {
+    const T ov = dpp<0x128>(v);
+    const int oi = dpp<0x128>(idx);
+    const bool take = (ov > v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+  }
+#pragma unroll
+  for (int off = 16; off <= 32; off <<= 1) {
+    const T ov = __shfl_xor(v, off, kWave);
+    const int oi = __shfl_xor(idx, off, kWave);
+    const bool take = (ov > v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void blocks_argmin(T& v, int& idx) {
+  {
+    const T ov = dpp<0x128>(v);
+    const int oi = dpp<0x128>(idx);
+    const bool take = (ov < v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+  }
+#pragma unroll
+  for (int off = 16; off <= 32; off <<= 1) {
+    const T ov = __shfl_xor(v, off, kWave);
+    const int oi = __shfl_xor(idx, off, kWave);
+    const bool take = (ov < v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+  }
+}
+
+// NOTE: no helper here indexes a register array with a runtime value --
+// hipcc turns such selects into scratch-memory indexing (guide rule 20).
+// Dynamic (wave-uniform) element access always goes through LDS instead.
+
+template <typename T, int BS>
+struct Sym2D {
+  static constexpr int NMAX = 8 * BS;
+  // LDS scratch a kernel must provide: BUF elements
+  static constexpr int BUF = NMAX * BS + NMAX;
+  T m[BS][BS];
+  int bi, bj;
+
+  __device__ __forceinline__ void init(int lane) {
+    bi = lane >> 3;
+    bj = lane & 7;
+  }
+
+  // Fill from a packed-lower matrix staged in LDS; entries outside n x n are 0.
+  __device__ __forceinline__ void load_packed(const T* Ps, int n, bool& nonfinite) {
+#pragma unroll
+    for (int r = 0; r < BS; ++r)
+#pragma unroll
+      for (int c = 0; c < BS; ++c) {
+        const int i = bi * BS + r, j = bj * BS + c;
+        T v = T(0);
+        if (i < n && j < n) {
+          const int idx = (j <= i) ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i;
+          v = Ps[idx];
+          nonfinite |= !finite(v);
+        }
+        m[r][c] = v;
+      }
+  }
+
+  // Column k (wave-uniform) of M: colr[r] = M[bi*BS+r][k] for this lane's rows,
+  // colc[c] = M[bj*BS+c][k] (= row k, by symmetry) for its columns; returns
+  // M_kk.  The owning block column publishes its whole BS x BS tile rows so
+  // that the (runtime) column offset is applied to an LDS address, never to a
+  // register index.
+  __device__ __forceinline__ T column(int k, T* buf, T (&colr)[BS], T (&colc)[BS]) {
+    const int kb = k / BS, kc = k - kb * BS;
+    if (bj == kb) {
+#pragma unroll
+      for (int r = 0; r < BS; ++r)
+#pragma unroll
+        for (int c = 0; c < BS; ++c) buf[(bi * BS + r) * BS + c] = m[r][c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < BS; ++r) colr[r] = buf[(bi * BS + r) * BS + kc];
+#pragma unroll
+    for (int c = 0; c < BS; ++c) colc[c] = buf[(bj * BS + c) * BS + kc];
+    const T d = buf[k * BS + kc];
+    __syncthreads();
+    return d;
+  }
+
+  // Goodnight sweep on pivot k: sigma = +1 moves k into the swept set,
+  // sigma = -1 (reverse sweep) moves it out.  Returns the pivot M_kk.
+  __device__ __forceinline__ T sweep(int k, T sigma, T* buf) {
+    T colr[BS], colc[BS];
+    const T d = column(k, buf, colr, colc);
+    const T rd = T(1) / d;
+    T ar[BS];
+#pragma unroll
+    for (int r = 0; r < BS; ++r) ar[r] = colr[r] * rd;
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const bool ik = (bi * BS + r) == k;
+#pragma unroll
+      for (int c = 0; c < BS; ++c) {
+        const bool jk = (bj * BS + c) == k;
+        const T gen = fma(-ar[r], colc[c], m[r][c]);
+        const T spec = ik ? (jk ? -rd : sigma * colc[c] * rd) : sigma * ar[r];
+        m[r][c] = (ik || jk) ? spec : gen;
+      }
+    }
+    return d;
+  }
+
+  // out[r] = sum_j M[i][j] w[j] for this lane's rows; w in row-block layout.
+  __device__ __forceinline__ void matvec(const T (&w)[BS], T* buf, T (&out)[BS]) {
+    T* wb = buf + NMAX * BS;
+    if (bj == 0) {
+#pragma unroll
+      for (int r = 0; r < BS; ++r) wb[bi * BS + r] = w[r];
+    }
+    __syncthreads();
+    T wc[BS];
+#pragma unroll
+    for (int c = 0; c < BS; ++c) wc[c] = wb[bj * BS + c];
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      T s = T(0);
+#pragma unroll
+      for (int c = 0; c < BS; ++c) s = fma(m[r][c], wc[c], s);
+      out[r] = rowblock_sum(s);
+    }
+    __syncthreads();
+  }
+};
+
+// Publish a row-block vector to LDS (vb[0..8*BS)) so that a wave-uniform
+// element can be read back by address.
+template <typename T, int BS>
+__device__ __forceinline__ void publish(const T (&v)[BS], T* vb, int bi, int bj) {
+  if (bj == 0) {
+#pragma unroll
+    for (int r = 0; r < BS; ++r) vb[bi * BS + r] = v[r];
+  }
+}
+
+// Stage a packed lower triangle of P elements into LDS with coalesced loads.
+template <typename T, int MAXE>
+__device__ __forceinline__ void stage_packed(const T* g, T* Ps, int P, int lane) {
+  constexpr int MAXT = (MAXE + kWave - 1) / kWave;
+  T tmp[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int e = lane + t * kWave;
+    tmp[t] = (e < P) ? g[e] : T(0);
+  }
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int e = lane + t * kWave;
+    if (e < P) Ps[e] = tmp[t];
+  }
+}
+
+}  // namespace mpcqp
