@@ -5,6 +5,9 @@ double integrator of session_1/FHC.py:136-142 (Ts=0.5, Q=CC'+1e-3I, R=0.1,
 P_f=Q), horizon N=20, input box |u|<=1, batch 4096 random x0 ~ U(-10,10)^2
 per GPU, fp64.  One step = one pass of the hot path over one batch:
 
+  --mode fused (default)
+    mpcqp_mpc_box    per-instance (A, B, x0) -> z, status          [HIP, 1 launch]
+  --mode split
     mpcqp_condense   per-instance (A, B, x0) -> H (packed), f     [HIP]
     mpcqp_solve_box  -> z, status                                 [HIP]
 
@@ -81,6 +84,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=50)
+    ap.add_argument("--mode", choices=("fused", "split"), default="fused")
+    ap.add_argument("--traffic", default=None,
+                    help="JSON with PMC-measured HBM bytes per launch {kernel: bytes} "
+                         "(tools/prof_counters.sh); fills roofline.traffic")
     args = ap.parse_args()
 
     rank, world, local = mdist.env_rank_world()
@@ -110,10 +117,15 @@ def main():
     Z = torch.empty((S, bsz, n), dtype=dt, device=dev)
     ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
 
-    def step(s):
+    def step_split(s):
         batched.condense(A_b, B_b, Q_t, R_t, Qf_t, N, x0=X0_t[s], outputs=("H", "f"),
                          out={"H": H[s], "f": f[s]})
         batched.solve_box(H[s], f[s], lb, ub, out=(Z[s], ST[s]))
+
+    def step_fused(s):
+        batched.mpc_box(A_b, B_b, Q_t, R_t, Qf_t, N, X0_t[s], lb, ub, out=(Z[s], ST[s]))
+
+    step = step_fused if args.mode == "fused" else step_split
 
     # warm the JIT-free path once per slot, then capture
     for s in range(S):
@@ -162,35 +174,59 @@ def main():
     iters = batched.status_iters(ST).double()
 
     # ---- per-kernel durations with HIP events on the launch stream (eager)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    tc = ts_ = 0.0
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    tc = ts_ = tf = 0.0
     P = args.profile_steps
+    Zc = torch.empty_like(Z[0])
+    STc = torch.empty_like(ST[0])
     for k in range(P):
         s = k % S
         ev[0].record()
         batched.condense(A_b, B_b, Q_t, R_t, Qf_t, N, x0=X0_t[s], outputs=("H", "f"),
                          out={"H": H[s], "f": f[s]})
         ev[1].record()
-        batched.solve_box(H[s], f[s], lb, ub, out=(Z[s], ST[s]))
+        batched.solve_box(H[s], f[s], lb, ub, out=(Zc, STc))
         ev[2].record()
-        ev[2].synchronize()
+        batched.mpc_box(A_b, B_b, Q_t, R_t, Qf_t, N, X0_t[s], lb, ub, out=(Z[s], ST[s]))
+        ev[3].record()
+        ev[3].synchronize()
         tc += ev[0].elapsed_time(ev[1])
         ts_ += ev[1].elapsed_time(ev[2])
-    cond_ms, solve_ms = tc / P, ts_ / P
+        tf += ev[2].elapsed_time(ev[3])
+    cond_ms, solve_ms, fused_ms = tc / P, ts_ / P, tf / P
+    split_vs_fused = float((Zc - Z[(P - 1) % S]).abs().max())
 
     out = None
     if rank == 0:
+        traffic = {}
+        if args.traffic:
+            with open(args.traffic) as fh:
+                traffic = json.load(fh)
         cb_bytes = condense_bytes_per_instance(nx, nu, N) * bsz
         sv_bytes = solve_bytes_per_instance(n) * bsz
         cond_gbs = cb_bytes / (cond_ms * 1e-3) / 1e9
         solve_gbs = sv_bytes / (solve_ms * 1e-3) / 1e9
-        dominant = "solve_box" if solve_ms >= cond_ms else "condense"
         roof_cond = {"kernel": "condense_kernel<double,2>", "bound": "hbm", "achieved": round(cond_gbs, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(cond_gbs / HBM_PEAK_GBS, 4),
-                     "traffic": None, "bytes_per_launch": cb_bytes, "avg_launch_us": round(cond_ms * 1e3, 2)}
-        roof_solve = {"kernel": "box_gi_kernel<double,24>", "bound": "hbm", "achieved": round(solve_gbs, 1),
+                     "traffic": traffic.get("condense"), "bytes_per_launch": cb_bytes,
+                     "avg_launch_us": round(cond_ms * 1e3, 2)}
+        roof_solve = {"kernel": "box_gi_kernel<double,3>", "bound": "hbm", "achieved": round(solve_gbs, 1),
                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(solve_gbs / HBM_PEAK_GBS, 4),
-                      "traffic": None, "bytes_per_launch": sv_bytes, "avg_launch_us": round(solve_ms * 1e3, 2)}
+                      "traffic": traffic.get("solve_box"), "bytes_per_launch": sv_bytes,
+                      "avg_launch_us": round(solve_ms * 1e3, 2)}
+        # fused kernel: SURVEY.md 8(d) per-instance figure (22.0 kflop condense,
+        # config 2) against the fp64 peak; it moves only A, B, x0 in and z out.
+        fl = condense_flops_per_instance(nx, nu, N) * bsz
+        fused_tfs = fl / (fused_ms * 1e-3) / 1e12
+        roof_fused = {"kernel": "mpc_box_kernel<double,2,1,3>", "bound": "mfma", "achieved": round(fused_tfs, 3),
+                      "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": round(fused_tfs / FP64_PEAK_TFS, 4),
+                      "traffic": traffic.get("mpc_box"), "flops_per_launch": fl,
+                      "hbm_bytes_per_launch": (nx * nx + nx * nu + nx + n) * 8 * bsz + 4 * bsz,
+                      "avg_launch_us": round(fused_ms * 1e3, 2)}
+        if args.mode == "fused":
+            roofline = roof_fused
+        else:
+            roofline = roof_solve if solve_ms >= cond_ms else roof_cond
         # oracle spot check of the timed outputs (first 256 instances of slot 0)
         from oracle import cbaseline as cbl
 
@@ -227,14 +263,18 @@ def main():
             "config": {"workload": "cfg2: per-instance condense + box QP, FHC.py double integrator "
                                    "(ts=0.5), N=20, |u|<=1, x0~U(-10,10)^2",
                        "batch_per_gpu": bsz, "horizon": N, "nx": nx, "nu": nu,
-                       "parallelism": f"dp{world}", "graph": graphs is not None},
+                       "parallelism": f"dp{world}", "graph": graphs is not None,
+                       "mode": args.mode},
             "max_abs_u_err_vs_oracle": err,
             "optimal_frac": opt_frac,
             "iters_mean": round(float(iters.mean()), 2),
             "iters_max": int(iters.max()),
-            "kernel_us": {"condense": round(cond_ms * 1e3, 2), "solve_box": round(solve_ms * 1e3, 2)},
-            "roofline": roof_solve if dominant == "solve_box" else roof_cond,
+            "kernel_us": {"mpc_box": round(fused_ms * 1e3, 2), "condense": round(cond_ms * 1e3, 2),
+                          "solve_box": round(solve_ms * 1e3, 2)},
+            "split_vs_fused_max_abs": split_vs_fused,
+            "roofline": roofline,
             "roofline_condense": roof_cond,
+            "roofline_solve_box": roof_solve,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

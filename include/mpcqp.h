@@ -14,6 +14,8 @@
  *   mpcqp_solve_box  <- the per-step IPOPT call of session_4/main.py:115-116
  *                       (session4_sol.py:128-129) for an input box
  *                       (lbx/ubx, main.py:68-69,97-98).
+ *   mpcqp_mpc_box    <- both of the above fused for the input-box OCP
+ *                       (MPCController.solve end to end, one launch).
  *   mpcqp_solve_poly <- the same call with general rows hl <= G z <= hu (state box
  *                       lbg/ubg of main.py:58-61,99-100 after condensing, or
  *                       arbitrary polytopes -- BASELINE config 4).
@@ -116,6 +118,24 @@ int mpcqp_solve_box(int dtype, int batch, int n,
                     const void* H, int64_t strideH, const void* f, int64_t stridef,
                     const void* lb, int64_t strideLb, const void* ub, int64_t strideUb,
                     void* z, int32_t* status, int max_iter, double tol, void* stream);
+
+/*
+ * Fused per-instance condense + input-box QP (the whole MPCController.solve of
+ * session_4/main.py:115-116 for an input-box OCP, session4_sol.py:128-129):
+ * plant (A, B [, c]) per instance or shared exactly as in mpcqp_condense, x0
+ * per instance, bounds lb/ub (N*nu; stride 0 = shared; NULL = +-inf) -> z, status.
+ * -H^{-1} is built from a per-instance Riccati factorisation (one lane per
+ * column) instead of being formed and inverted; nothing but the plant, x0,
+ * the bounds and z cross HBM.  Limits: nx <= 4, nu <= 2, N*nu <= 32 (larger
+ * problems: mpcqp_condense + mpcqp_solve_box).
+ */
+int mpcqp_mpc_box(int dtype, int batch, int nx, int nu, int N, int flags,
+                  const void* A, int64_t strideA, const void* Bm, int64_t strideB,
+                  const void* Q, int64_t strideQ, const void* R, int64_t strideR,
+                  const void* Qf, int64_t strideQf, const void* c, int64_t strideC,
+                  const void* x0, int64_t strideX0,
+                  const void* lb, int64_t strideLb, const void* ub, int64_t strideUb,
+                  void* z, int32_t* status, int max_iter, double tol, void* stream);
 
 /*
  * Batched polytope QP:

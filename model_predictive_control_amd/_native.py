@@ -40,6 +40,9 @@ SIGNATURES = {
                             _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mpcqp_solve_box": (_i, [_i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                              _vp, _vp, _i, _d, _vp]),
+    "mpcqp_mpc_box": (_i, [_i, _i, _i, _i, _i, _i,
+                           _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
+                           _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i, _d, _vp]),
     "mpcqp_solve_poly_workspace": (_i64, [_i, _i, _i, _i, _i]),
     "mpcqp_solve_poly": (_i, [_i, _i, _i, _i, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp,
                               _vp, _vp, _vp, _i, _d, _vp, _i64, _vp]),

@@ -22,7 +22,7 @@ import torch
 from . import _native as nat
 
 __all__ = [
-    "condense", "solve_box", "solve_poly", "riccati", "gemv", "rollout",
+    "condense", "solve_box", "mpc_box", "solve_poly", "riccati", "gemv", "rollout",
     "pack_lower", "unpack_lower", "status_code", "status_iters",
 ]
 
@@ -146,6 +146,47 @@ def condense(A, B, Q, R, Qf, N: int, x0=None, c=None, *, tv: bool = False,
         _ptr(out.get("Gam")), _ptr(out.get("Phi")), _ptr(out.get("xbar")), _stream())
     nat.check(rc, "mpcqp_condense")
     return {k: out[k] for k in want}
+
+
+# ---------------------------------------------------- fused condense + box
+def mpc_box(A, B, Q, R, Qf, N: int, x0, lb=None, ub=None, c=None, *, tv: bool = False,
+            max_iter: int = 0, tol: float = 0.0, out: tuple | None = None):
+    """Fused per-instance condense + input-box QP (include/mpcqp.h
+    ``mpcqp_mpc_box``).  Same plant conventions as ``condense``; lb/ub are
+    scalars, (N*nu,) shared or (b, N*nu).  Returns (z (b, N*nu), status)."""
+    dt = A.dtype if isinstance(A, torch.Tensor) else torch.float64
+    dev = A.device if isinstance(A, torch.Tensor) else torch.device("cuda")
+    A, B, Q, R, Qf = (_dev(v, dt, dev) for v in (A, B, Q, R, Qf))
+    x0, c = _dev(x0, dt, dev), _dev(c, dt, dev)
+    nx, nu = int(B.shape[-2]), int(B.shape[-1])
+    if R.ndim == 1:
+        R = R.expand(nu, nu).contiguous()
+    n = N * nu
+    base = 3 if tv else 2
+    sA, bA = _inst(A, base, "A")
+    sB, bB = _inst(B, base, "B")
+    sQ, bQ = _inst(Q, 2, "Q")
+    sR, bR = _inst(R, 2, "R")
+    sQf, bQf = _inst(Qf, 2, "Qf")
+    sC, bC = _inst(c, 2, "c")
+    sX, bX = _inst(x0, 1, "x0")
+    lbt, slb = _bound(lb, n, dt, dev)
+    ubt, sub = _bound(ub, n, dt, dev)
+    batch = _batch_of((sA, bA), (sB, bB), (sQ, bQ), (sR, bR), (sQf, bQf), (sC, bC), (sX, bX),
+                      (slb, lbt.shape[0] if lbt is not None and lbt.ndim == 2 else None),
+                      (sub, ubt.shape[0] if ubt is not None and ubt.ndim == 2 else None))
+    if out is None:
+        z = torch.empty((batch, n), dtype=dt, device=dev)
+        status = torch.empty((batch,), dtype=torch.int32, device=dev)
+    else:
+        z, status = out
+    rc = _lib().mpcqp_mpc_box(
+        _code(dt), batch, nx, nu, N, nat.TV if tv else 0,
+        _ptr(A), sA, _ptr(B), sB, _ptr(Q), sQ, _ptr(R), sR, _ptr(Qf), sQf, _ptr(c), sC,
+        _ptr(x0), sX, _ptr(lbt), slb, _ptr(ubt), sub, _ptr(z), _ptr(status), int(max_iter),
+        float(tol), _stream())
+    nat.check(rc, "mpcqp_mpc_box")
+    return z, status
 
 
 # ----------------------------------------------------------------- box QP

@@ -92,6 +92,20 @@ struct Lim<float> {
   static __device__ __forceinline__ float inf() { return __builtin_huge_valf(); }
 };
 
+// Reciprocal from the hardware estimate plus Newton steps (~1 ulp), instead of
+// the ~12-instruction IEEE division sequence on the serial pivot chain.
+__device__ __forceinline__ double fast_rcp(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ __forceinline__ float fast_rcp(float d) {
+  float r = __builtin_amdgcn_rcpf(d);
+  return fmaf(r, fmaf(-d, r, 1.0f), r);
+}
+
 template <typename T>
 __device__ __forceinline__ bool finite(T v) {
   return __builtin_isfinite(v);

@@ -19,7 +19,7 @@
 // rank-1 update whose pivot column is broadcast through LDS; the dual step
 // directions are column p of M; the subspace minimiser and the active-set
 // gradient are one mat-vec  s = M w,  w = (f_F, -z_A).
-#include "sym2d.hpp"
+#include "gi_box_core.hpp"
 
 namespace mpcqp {
 
@@ -36,25 +36,18 @@ struct BoxArgs {
   T tol;
 };
 
-// st: 0 free, 1 at lower, 2 at upper, 3 padding row (never free)
-// Occupancy target: 4 waves/SIMD (16 per CU) up to BS = 3 (n <= 24), which
-// keeps a 4096-instance batch resident in one pass over the 256 CUs.
-template <int BS>
-struct BoxOcc {
-  static constexpr int w = BS <= 3 ? 4 : (BS <= 5 ? 2 : 1);
-};
-
 template <typename T, int BS>
 __global__ __launch_bounds__(64, BoxOcc<BS>::w) void box_gi_kernel(BoxArgs<T> a) {
-  using S2 = Sym2D<T, BS>;
-  constexpr int NMAX = S2::NMAX;
+  using L = BoxLds<T, BS>;
+  constexpr int NMAX = L::NMAX;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  T* buf = reinterpret_cast<T*>(smem_raw);  // Sym2D scratch
-  T* fs = buf + S2::BUF;                    // per-row data by row index
-  T* lbs = fs + NMAX;
-  T* ubs = lbs + NMAX;
-  T* zs = ubs + NMAX;
-  T* Ps = zs + NMAX;                        // packed H
+  T* sm = reinterpret_cast<T*>(smem_raw);
+  T* buf = sm + L::oBuf;
+  T* fs = sm + L::oF;
+  T* lbs = sm + L::oLb;
+  T* ubs = sm + L::oUb;
+  T* zs = sm + L::oZ;
+  T* Ps = sm + L::oEnd;  // packed H
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = a.n;
@@ -79,161 +72,26 @@ __global__ __launch_bounds__(64, BoxOcc<BS>::w) void box_gi_kernel(BoxArgs<T> a)
   Sym2D<T, BS> M;
   M.init(lane);
   M.load_packed(Ps, n, nonfinite);
-  T zr[BS], gr[BS];
-  int st[BS];
-#pragma unroll
-  for (int r = 0; r < BS; ++r) {
-    st[r] = (M.bi * BS + r < n) ? 0 : 3;
-    zr[r] = T(0);
-    gr[r] = T(0);
-  }
-
-  int code = MPCQP_STATUS_MAXITER;
+  T zr[BS];
   int iters = 0;
-  const T tol = a.tol;
-  const int max_iter = a.max_iter;
-
+  int code;
   if (__any(nonfinite)) {
     code = MPCQP_STATUS_NONFINITE;
-    goto done;
-  }
-  if (__any(badbox)) {
+  } else if (__any(badbox)) {
     code = MPCQP_STATUS_INFEASIBLE;
-    goto done;
-  }
-
-  // ---- M = SWEEP_all(H) = -H^{-1}
-  for (int k = 0; k < n; ++k) {
-    const T d = M.sweep(k, T(1), buf);
-    if (!(d > T(0))) {
-      code = MPCQP_STATUS_NOT_CONVEX;
-      goto done;
-    }
-  }
-
-  {
-    // subspace minimiser for (F, A): with w = (f_F, -z_A), s = M w gives
-    // z_F = s_F and the active-set gradient g_A = f_A - s_A.
-    auto refresh = [&]() {
-      T w[BS], s[BS];
-#pragma unroll
-      for (int r = 0; r < BS; ++r) {
-        const int i = M.bi * BS + r;
-        const T zA = (st[r] == 1) ? lbs[i] : ((st[r] == 2) ? ubs[i] : T(0));
-        w[r] = (st[r] == 0) ? fs[i] : -zA;
-        zr[r] = zA;
-      }
-      M.matvec(w, buf, s);
-#pragma unroll
-      for (int r = 0; r < BS; ++r) {
-        const int i = M.bi * BS + r;
-        gr[r] = (st[r] == 0) ? T(0) : fs[i] - s[r];
-        zr[r] = (st[r] == 0) ? s[r] : zr[r];
-      }
-    };
-    refresh();
-
-    while (true) {
-      // most violated free variable (relative to the bound's magnitude)
-      T viol = -Lim<T>::inf();
-      int p = 0;
-#pragma unroll
-      for (int r = 0; r < BS; ++r) {
-        if (st[r] == 0) {
-          const int i = M.bi * BS + r;
-          const T li = lbs[i], ui = ubs[i];
-          const T vl = finite(li) ? (li - zr[r]) / (T(1) + fabs(li)) : -Lim<T>::inf();
-          const T vu = finite(ui) ? (zr[r] - ui) / (T(1) + fabs(ui)) : -Lim<T>::inf();
-          const T v = fmax(vl, vu);
-          if (v > viol) {
-            viol = v;
-            p = i;
-          }
-        }
-      }
-      blocks_argmax(viol, p);
-      p = uniform(p);
-      if (!(readlane(viol, 0) > tol)) {
-        code = MPCQP_STATUS_OPTIMAL;
+  } else {
+    code = MPCQP_STATUS_OPTIMAL;
+    // ---- M = SWEEP_all(H) = -H^{-1}
+    for (int k = 0; k < n; ++k) {
+      const T d = M.sweep(k, T(1), buf);
+      if (!(d > T(0))) {
+        code = MPCQP_STATUS_NOT_CONVEX;
         break;
       }
-      publish<T, BS>(zr, zs, M.bi, M.bj);
-      __syncthreads();
-      const T lbp = lbs[p], ubp = ubs[p];
-      T zp = zs[p];
-      __syncthreads();
-      const int side = (zp < lbp) ? 1 : 2;
-      const T tgt = (side == 1) ? lbp : ubp;
-      T mu[BS];
-#pragma unroll
-      for (int r = 0; r < BS; ++r) mu[r] = (st[r] == 1) ? gr[r] : ((st[r] == 2) ? -gr[r] : T(0));
-      bool added = false;
-      while (!added) {
-        if (++iters > max_iter) goto done;
-        T c[BS], cc[BS];
-        const T mpp = M.column(p, buf, c, cc);  // c[r] = M_ip; M_pp < 0 (p free)
-        const T rm = T(1) / mpp;
-        const T sgn = (tgt > zp) ? T(1) : T(-1);
-        const T t2 = fabs(tgt - zp);
-        T ti = Lim<T>::inf();
-        int k = 0;
-#pragma unroll
-        for (int r = 0; r < BS; ++r) {
-          c[r] *= rm;  // c/M_pp: dz_F per unit step
-          const T dmu = ((st[r] == 1) ? -c[r] : ((st[r] == 2) ? c[r] : T(0))) * sgn;
-          const T t = ((st[r] == 1 || st[r] == 2) && dmu < T(0)) ? mu[r] / (-dmu)
-                                                                  : Lim<T>::inf();
-          if (t < ti) {
-            ti = t;
-            k = M.bi * BS + r;
-          }
-        }
-        blocks_argmin(ti, k);
-        k = uniform(k);
-        ti = readlane(ti, 0);
-        if (ti < t2) {
-          // partial step: the multiplier of bound k reaches zero -> drop k
-#pragma unroll
-          for (int r = 0; r < BS; ++r) {
-            const T dmu = ((st[r] == 1) ? -c[r] : ((st[r] == 2) ? c[r] : T(0))) * sgn;
-            if (st[r] == 0) zr[r] = fma(sgn * ti, c[r], zr[r]);
-            mu[r] = fma(ti, dmu, mu[r]);
-            if (M.bi * BS + r == k) {
-              mu[r] = T(0);
-              st[r] = 0;
-            }
-          }
-          const T d = M.sweep(k, T(1), buf);
-          if (!(d > T(0))) {
-            code = MPCQP_STATUS_NOT_CONVEX;
-            goto done;
-          }
-          zp = fma(sgn, ti, zp);  // row p moves by sgn*ti*(M_pp/M_pp)
-        } else {
-          // full step: bound p becomes active
-#pragma unroll
-          for (int r = 0; r < BS; ++r) {
-            if (M.bi * BS + r == p) st[r] = side;
-          }
-          const T d = M.sweep(p, T(-1), buf);
-          if (!(d < T(0))) {
-            code = MPCQP_STATUS_NOT_CONVEX;
-            goto done;
-          }
-          refresh();
-          added = true;
-        }
-      }
     }
-    // project free variables that sit within tol outside their bounds
-#pragma unroll
-    for (int r = 0; r < BS; ++r) {
-      const int i = M.bi * BS + r;
-      zr[r] = fmin(fmax(zr[r], lbs[i]), ubs[i]);
-    }
+    if (code == MPCQP_STATUS_OPTIMAL)
+      code = gi_box_core<T, BS>(M, buf, fs, lbs, ubs, zs, n, a.max_iter, a.tol, zr, iters);
   }
-
-done:
   if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
 #pragma unroll
     for (int r = 0; r < BS; ++r) zr[r] = __builtin_nan("");
@@ -250,7 +108,7 @@ done:
 
 template <typename T, int BS>
 static int launch_box(const BoxArgs<T>& a, hipStream_t st) {
-  const size_t bytes = (size_t)(Sym2D<T, BS>::BUF + 4 * 8 * BS + a.n * (a.n + 1) / 2) * sizeof(T);
+  const size_t bytes = (size_t)(BoxLds<T, BS>::oEnd + a.n * (a.n + 1) / 2) * sizeof(T);
   hipLaunchKernelGGL((box_gi_kernel<T, BS>), dim3(a.batch), dim3(kWave), bytes, st, a);
   MPCQP_CHECK_LAUNCH("box_gi_kernel");
   return MPCQP_OK;

@@ -146,7 +146,7 @@ struct Sym2D {
   __device__ __forceinline__ T sweep(int k, T sigma, T* buf) {
     T colr[BS], colc[BS];
     const T d = column(k, buf, colr, colc);
-    const T rd = T(1) / d;
+    const T rd = fast_rcp(d);
     T ar[BS];
 #pragma unroll
     for (int r = 0; r < BS; ++r) ar[r] = colr[r] * rd;

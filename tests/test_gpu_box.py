@@ -161,3 +161,69 @@ def test_box_cfg2_full_batch_kkt(dev):
         assert np.abs(zc[b] - zr).max() < 1e-9
     it = batched.status_iters(st)
     assert int(it.max()) <= 3 * N + 30
+
+
+# ------------------------------------------------ fused condense + box solve
+@pytest.mark.parametrize("nx,nu,N,tv", [(2, 1, 20, False), (1, 1, 7, False), (2, 2, 16, True),
+                                        (3, 1, 12, True), (4, 2, 16, True), (4, 1, 32, False),
+                                        (2, 1, 1, False)])
+def test_mpc_box_fused_vs_oracle(dev, nx, nu, N, tv):
+    rng = np.random.default_rng(31 * nx + 7 * nu + N)
+    batch = 12
+    shA = (batch, N, nx, nx) if tv else (batch, nx, nx)
+    shB = (batch, N, nx, nu) if tv else (batch, nx, nu)
+    A = rng.normal(size=shA) * (0.8 / np.sqrt(nx)) + 0.4 * np.eye(nx)
+    B = rng.normal(size=shB)
+    M = rng.normal(size=(nx, nx)); Q = M @ M.T / nx + 0.2 * np.eye(nx)
+    R = np.diag(rng.uniform(0.1, 1.0, nu)); Qf = 3 * Q
+    x0 = rng.normal(size=(batch, nx)) * 3
+    c = rng.normal(size=(batch, N, nx)) * 0.3 if tv else None
+    n = N * nu
+    lb = -rng.uniform(0.2, 1.0, (batch, n)); ub = rng.uniform(0.2, 1.0, (batch, n))
+    z, st = batched.mpc_box(_t(A, dev), _t(B, dev), _t(Q, dev), _t(R, dev), _t(Qf, dev), N,
+                            _t(x0, dev), _t(lb, dev), _t(ub, dev),
+                            c=None if c is None else _t(c, dev), tv=tv)
+    z = z.cpu().numpy()
+    assert (batched.status_code(st) == 0).all(), st
+    for b in range(batch):
+        ref = oc.condense(A[b], B[b], Q, R, Qf, N, x0=x0[b], c=None if c is None else c[b])
+        zr, _, _ = oq.box_qp(ref["H"], ref["f"], lb[b], ub[b])
+        assert np.abs(z[b] - zr).max() < 1e-9 * max(1, np.abs(zr).max()), (b, np.abs(z[b] - zr).max())
+
+
+def test_mpc_box_cfg2_golden_and_full_batch(dev, golden):
+    g = golden("boxqp_cfg2.npz")
+    N = int(g["N"])
+    z, st = batched.mpc_box(_t(g["A"], dev), _t(g["B"], dev), _t(g["Q"], dev), _t(g["R"], dev),
+                            _t(g["Pf"], dev), N, _t(g["x0"], dev), -1.0, 1.0)
+    assert (batched.status_code(st) == 0).all()
+    assert np.abs(z.cpu().numpy() - g["z"]).max() < 1e-9
+    # full config-2 batch: fused == split pipeline
+    A, B, Q, R, Pf, _ = s1.fhc_setup()
+    R = R.reshape(1, 1)
+    batch = 4096
+    X0 = np.random.default_rng(5).uniform(-10, 10, (batch, 2))
+    Ab = _t(np.broadcast_to(A, (batch, 2, 2)), dev)
+    Bb = _t(np.broadcast_to(B, (batch, 2, 1)), dev)
+    zf, stf = batched.mpc_box(Ab, Bb, _t(Q, dev), _t(R, dev), _t(Pf, dev), N, _t(X0, dev), -1.0, 1.0)
+    d = batched.condense(Ab, Bb, _t(Q, dev), _t(R, dev), _t(Pf, dev), N, x0=_t(X0, dev))
+    zs, sts = batched.solve_box(d["H"], d["f"], -1.0, 1.0)
+    assert (batched.status_code(stf) == 0).all() and (batched.status_code(sts) == 0).all()
+    assert float((zf - zs).abs().max()) < 1e-9
+
+
+def test_mpc_box_fp32(dev):
+    A, B, Q, R, Pf, _ = s1.fhc_setup()
+    R = R.reshape(1, 1)
+    N, batch = 20, 64
+    X0 = np.random.default_rng(8).uniform(-3, 3, (batch, 2))
+    f32 = torch.float32
+    z, st = batched.mpc_box(_t(A, dev, f32), _t(B, dev, f32), _t(Q, dev, f32), _t(R, dev, f32),
+                            _t(Pf, dev, f32), N, _t(X0, dev, f32), -1.0, 1.0)
+    z = z.double().cpu().numpy()
+    assert (batched.status_code(st) == 0).all()
+    for b in range(0, batch, 5):
+        ref = oc.condense(A, B, Q, R, Pf, N, x0=X0[b])
+        zr, _, _ = oq.box_qp(ref["H"], ref["f"], -np.ones(N), np.ones(N))
+        # fp32 with cond(H) ~ 6e3: 2e-3 absolute on |u| <= 1
+        assert np.abs(z[b] - zr).max() < 2e-3
