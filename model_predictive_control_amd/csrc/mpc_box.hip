@@ -22,6 +22,7 @@
 // linear term f = Gam'Qhat xbar comes from the free response xbar and the
 // adjoint y_k = Q xbar_k + A_k'y_{k+1} (as in condense.hip).
 #include "gi_box_core.hpp"
+#include "quad_api.hpp"
 
 namespace mpcqp {
 
@@ -478,6 +479,12 @@ static int mpc_bs(const MpcBoxArgs<T>& a, hipStream_t st) {
 
 template <typename T>
 static int mpc_box_t(MpcBoxArgs<T>& a, hipStream_t st) {
+  if (!use_wave_kernels()) {
+    MpcArgsQ<T> q{a.batch, a.nx, a.nu, a.N, a.tv, a.A, a.sA, a.B, a.sB, a.Q, a.sQ, a.R, a.sR,
+                  a.Qf, a.sQf, a.c, a.sC, a.x0, a.sX0, a.lb, a.slb, a.ub, a.sub, a.z, a.status,
+                  a.max_iter, a.tol};
+    return mpc_box_quad<T>(q, st);
+  }
   if (a.nx <= 2 && a.nu == 1) return mpc_bs<T, 2, 1>(a, st);
   if (a.nx <= 2) return mpc_bs<T, 2, 2>(a, st);
   if (a.nu == 1) return mpc_bs<T, 4, 1>(a, st);

@@ -1,0 +1,363 @@
+// quad.hpp -- four QPs per wavefront, one per 16-lane DPP row ("group").
+//
+// Lane l: group g = l >> 4, and inside the group q = l & 15, bi = q >> 2,
+// bj = q & 3.  A symmetric n x n matrix (n <= 4*BS) of group g is held as a
+// 4 x 4 grid of BS x BS register blocks over the group's 16 lanes.  All
+// per-QP scalars (pivot index, step lengths, ...) are group-uniform VGPR
+// values; every reduction stays inside a DPP row (quad_perm for the 4 lanes
+// of a row block, row_ror:4/8 across row blocks), so four independent QPs
+// share each instruction and no cross-row traffic (bpermute) is needed.
+//
+// Compared with one QP per wavefront (sym2d.hpp) the per-iteration bookkeeping
+// -- reductions, LDS publishes, waits, scalar control -- is paid once for four
+// problems, which is what bounds the solve at the config-2 sizes (the SIMDs
+// are instruction-issue bound, see profiles/).
+#pragma once
+#include "sym2d.hpp"
+
+namespace mpcqp {
+
+// Max over the 4 row blocks of a group (lanes differing in bits 2..3),
+// carrying an index and one payload value; ties to the smaller index.
+template <typename T>
+__device__ __forceinline__ void group_argmax(T& v, int& idx, T& pay) {
+  {
+    const T ov = dpp<0x124>(v);  // row_ror:4
+    const int oi = dpp<0x124>(idx);
+    const T op = dpp<0x124>(pay);
+    const bool take = (ov > v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+    pay = take ? op : pay;
+  }
+  {
+    const T ov = dpp<0x128>(v);  // row_ror:8
+    const int oi = dpp<0x128>(idx);
+    const T op = dpp<0x128>(pay);
+    const bool take = (ov > v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+    pay = take ? op : pay;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void group_argmin(T& v, int& idx) {
+  {
+    const T ov = dpp<0x124>(v);
+    const int oi = dpp<0x124>(idx);
+    const bool take = (ov < v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+  }
+  {
+    const T ov = dpp<0x128>(v);
+    const int oi = dpp<0x128>(idx);
+    const bool take = (ov < v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+  }
+}
+
+// Sum over the 4 lanes of a row block (bits 0..1).
+template <typename T>
+__device__ __forceinline__ T quad_sum(T v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  return v;
+}
+
+template <typename T, int BS>
+struct QSym {
+  static constexpr int NMAX = 4 * BS;
+  static constexpr int CBUF = NMAX * BS;  // column-publish tile (per group)
+  static constexpr int BUF = CBUF + NMAX;  // + mat-vec vector
+  T m[BS][BS];
+  int bi, bj;
+
+  __device__ __forceinline__ void init(int lane) {
+    const int q = lane & 15;
+    bi = q >> 2;
+    bj = q & 3;
+  }
+
+  // From a dense row-major n x n matrix (leading dim ld) in LDS, symmetrised.
+  __device__ __forceinline__ void load_dense_sym(const T* D, int ld, int n) {
+#pragma unroll
+    for (int r = 0; r < BS; ++r)
+#pragma unroll
+      for (int c = 0; c < BS; ++c) {
+        const int i = bi * BS + r, j = bj * BS + c;
+        m[r][c] = (i < n && j < n) ? T(0.5) * (D[i * ld + j] + D[j * ld + i]) : T(0);
+      }
+  }
+
+  __device__ __forceinline__ void load_packed(const T* Ps, int n, bool& nonfinite) {
+#pragma unroll
+    for (int r = 0; r < BS; ++r)
+#pragma unroll
+      for (int c = 0; c < BS; ++c) {
+        const int i = bi * BS + r, j = bj * BS + c;
+        T v = T(0);
+        if (i < n && j < n) {
+          const int idx = (j <= i) ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i;
+          v = Ps[idx];
+          nonfinite |= !finite(v);
+        }
+        m[r][c] = v;
+      }
+  }
+
+  // Column k (group-uniform) through the group's LDS tile; returns M_kk.
+  __device__ __forceinline__ T column(int k, T* gb, T (&colr)[BS], T (&colc)[BS]) {
+    const int kb = k / BS, kc = k - kb * BS;
+    if (bj == kb) {
+#pragma unroll
+      for (int r = 0; r < BS; ++r)
+#pragma unroll
+        for (int c = 0; c < BS; ++c) gb[(bi * BS + r) * BS + c] = m[r][c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < BS; ++r) colr[r] = gb[(bi * BS + r) * BS + kc];
+#pragma unroll
+    for (int c = 0; c < BS; ++c) colc[c] = gb[(bj * BS + c) * BS + kc];
+    const T d = gb[k * BS + kc];
+    __syncthreads();
+    return d;
+  }
+
+  // Goodnight sweep (sigma = +1) / reverse sweep (sigma = -1) on pivot k with
+  // its column already fetched.  Row/column k are produced by the general
+  // rank-1 formula plus two indicator-weighted rank-1 corrections:
+  //   M' = M - a colc' + e_k w1' + w2 e_k',   a = colr/d, w2 = sigma a,
+  //   w1_j = sigma colc_j / d  (j != k),  w1_k = -1/d - sigma
+  // i.e. three FMAs per element and no per-element selects.
+  __device__ __forceinline__ void sweep_col(int k, T sigma, T d, const T (&colr)[BS],
+                                            const T (&colc)[BS]) {
+    const T rd = fast_rcp(d);
+    T a[BS], ik[BS], w2[BS], jk[BS], w1[BS];
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      a[r] = colr[r] * rd;
+      w2[r] = sigma * a[r];
+      ik[r] = (bi * BS + r == k) ? T(1) : T(0);
+    }
+#pragma unroll
+    for (int c = 0; c < BS; ++c) {
+      const bool isk = (bj * BS + c == k);
+      jk[c] = isk ? T(1) : T(0);
+      w1[c] = isk ? (-rd - sigma) : sigma * colc[c] * rd;
+    }
+#pragma unroll
+    for (int r = 0; r < BS; ++r)
+#pragma unroll
+      for (int c = 0; c < BS; ++c)
+        m[r][c] = fma(ik[r], w1[c], fma(w2[r], jk[c], fma(-a[r], colc[c], m[r][c])));
+  }
+
+  __device__ __forceinline__ T sweep(int k, T sigma, T* gb) {
+    T colr[BS], colc[BS];
+    const T d = column(k, gb, colr, colc);
+    sweep_col(k, sigma, d, colr, colc);
+    return d;
+  }
+
+  // out[r] = sum_j M[i][j] w[j] (w in the group's row-block layout).
+  __device__ __forceinline__ void matvec(const T (&w)[BS], T* gb, T (&out)[BS]) {
+    T* wb = gb + CBUF;
+    if (bj == 0) {
+#pragma unroll
+      for (int r = 0; r < BS; ++r) wb[bi * BS + r] = w[r];
+    }
+    __syncthreads();
+    T wc[BS];
+#pragma unroll
+    for (int c = 0; c < BS; ++c) wc[c] = wb[bj * BS + c];
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      T s = T(0);
+#pragma unroll
+      for (int c = 0; c < BS; ++c) s = fma(m[r][c], wc[c], s);
+      out[r] = quad_sum(s);
+    }
+    __syncthreads();
+  }
+};
+
+// Per-group LDS block for the box active set: [CBUF+NMAX | f | lb | ub].
+template <typename T, int BS>
+struct QBoxLds {
+  static constexpr int NMAX = 4 * BS;
+  static constexpr int oBuf = 0;
+  static constexpr int oF = QSym<T, BS>::BUF;
+  static constexpr int oLb = oF + NMAX;
+  static constexpr int oUb = oLb + NMAX;
+  static constexpr int size = oUb + NMAX;
+};
+
+// Goldfarb-Idnani dual active set for the group's box QP (see gi_box_core.hpp
+// for the method); entry: M = -H^{-1}.  Primal and dual quantities are tracked
+// incrementally along the steps (z_F, the active multipliers, and the
+// multiplier of the bound being added); when every group has settled, one
+// exact mat-vec refresh recomputes z and the multipliers and the bounds are
+// re-checked, so accumulated drift can never hide a violated bound.
+// live = this group holds a real instance.  Returns the status code.
+template <typename T, int BS>
+__device__ __forceinline__ void qscan(const QSym<T, BS>& M, const int (&st)[BS], const T (&zr)[BS],
+                                      const T* lbs, const T* ubs, T& viol, int& pi, T& zv) {
+  viol = -Lim<T>::inf();
+  pi = 0;
+  zv = T(0);
+#pragma unroll
+  for (int r = 0; r < BS; ++r) {
+    const int i = M.bi * BS + r;
+    const T li = lbs[i], ui = ubs[i];
+    const T vl = finite(li) ? (li - zr[r]) / (T(1) + fabs(li)) : -Lim<T>::inf();
+    const T vu = finite(ui) ? (zr[r] - ui) / (T(1) + fabs(ui)) : -Lim<T>::inf();
+    const T v = (st[r] == 0) ? fmax(vl, vu) : -Lim<T>::inf();
+    const bool take = v > viol;
+    viol = take ? v : viol;
+    pi = take ? i : pi;
+    zv = take ? zr[r] : zv;
+  }
+  group_argmax(viol, pi, zv);
+}
+
+template <typename T, int BS>
+__device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, const T* lbs,
+                                           const T* ubs, int n, int max_iter, T tol, bool live,
+                                           T (&zr)[BS], int& iters) {
+  int st[BS];
+  T mu[BS];
+#pragma unroll
+  for (int r = 0; r < BS; ++r) {
+    st[r] = (M.bi * BS + r < n) ? 0 : 3;
+    mu[r] = T(0);
+    zr[r] = T(0);
+  }
+  iters = 0;
+  int code = MPCQP_STATUS_OPTIMAL;
+  auto refresh = [&]() {
+    T w[BS], s[BS];
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      const T zA = (st[r] == 1) ? lbs[i] : ((st[r] == 2) ? ubs[i] : T(0));
+      w[r] = (st[r] == 0) ? fs[i] : -zA;
+      zr[r] = zA;
+    }
+    M.matvec(w, gb, s);
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      const T g = fs[i] - s[r];
+      zr[r] = (st[r] == 0) ? s[r] : zr[r];
+      mu[r] = (st[r] == 1) ? g : ((st[r] == 2) ? -g : T(0));
+    }
+  };
+  refresh();
+  bool active = live;
+  for (int pass = 0; pass < 3; ++pass) {
+    bool need_p = true;
+    int p = 0, side = 1;
+    T tgt = T(0), zp = T(0), gp = T(0);
+    while (true) {
+      if (__any(active && need_p)) {
+        T viol, zv;
+        int pi;
+        qscan<T, BS>(M, st, zr, lbs, ubs, viol, pi, zv);
+        if (active && need_p) {
+          if (!(viol > tol)) {
+            active = false;  // settled (pending the exact re-check)
+          } else {
+            p = pi;
+            zp = zv;
+            const T lbp = lbs[p], ubp = ubs[p];
+            side = (zp < lbp) ? 1 : 2;
+            tgt = (side == 1) ? lbp : ubp;
+            gp = T(0);
+            need_p = false;
+          }
+        }
+      }
+      if (!__any(active)) break;
+      bool stepping = active;
+      if (stepping && ++iters > max_iter) {
+        code = MPCQP_STATUS_MAXITER;
+        active = false;
+        stepping = false;
+      }
+      T c[BS], cc[BS];
+      const T mpp = M.column(p, gb, c, cc);  // c[r] = M_ip, M_pp < 0
+      const T rm = fast_rcp(mpp);
+      const T sgn = (tgt > zp) ? T(1) : T(-1);
+      const T t2 = fabs(tgt - zp);
+      T ti = Lim<T>::inf();
+      int k = 0;
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        c[r] *= rm;  // dz per unit move of z_p
+        const T dmu = ((st[r] == 1) ? -c[r] : ((st[r] == 2) ? c[r] : T(0))) * sgn;
+        const bool cand = (st[r] == 1 || st[r] == 2) && dmu < T(0);
+        const T t = cand ? -mu[r] * fast_rcp(dmu) : Lim<T>::inf();
+        const bool take = t < ti;
+        ti = take ? t : ti;
+        k = take ? (M.bi * BS + r) : k;
+      }
+      group_argmin(ti, k);
+      const bool partial = ti < t2;
+      const T s_eff = stepping ? (partial ? ti : t2) : T(0);
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        const T dmu = ((st[r] == 1) ? -c[r] : ((st[r] == 2) ? c[r] : T(0))) * sgn;
+        zr[r] = (st[r] == 0) ? fma(sgn * s_eff, c[r], zr[r]) : zr[r];
+        mu[r] = fma(s_eff, dmu, mu[r]);
+      }
+      gp = fma(-sgn * s_eff, rm, gp);  // d g_p / d z_p = -1 / M_pp
+      zp = fma(sgn, s_eff, zp);
+      // the index whose state changes: k joins F (partial) or p leaves it (full)
+      const int idx = partial ? k : p;
+      const T sigma = partial ? T(1) : T(-1);
+      T kr[BS], kcol[BS];
+      const T d = M.column(idx, gb, kr, kcol);
+      const bool bad = stepping && (partial ? !(d > T(0)) : !(d < T(0)));
+      if (stepping && !bad) {
+        M.sweep_col(idx, sigma, d, kr, kcol);
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+          const int i = M.bi * BS + r;
+          if (partial && i == k) {
+            st[r] = 0;
+            mu[r] = T(0);
+          }
+          if (!partial && i == p) {
+            st[r] = side;
+            zr[r] = tgt;
+            mu[r] = (side == 1) ? gp : -gp;
+          }
+        }
+        need_p = !partial;
+      }
+      if (bad) {
+        code = MPCQP_STATUS_NOT_CONVEX;
+        active = false;
+      }
+    }
+    // exact refresh for every group, then re-check the bounds
+    refresh();
+    T viol, zv;
+    int pi;
+    qscan<T, BS>(M, st, zr, lbs, ubs, viol, pi, zv);
+    active = live && code == MPCQP_STATUS_OPTIMAL && viol > tol;
+    if (!__any(active)) break;
+  }
+#pragma unroll
+  for (int r = 0; r < BS; ++r) {
+    const int i = M.bi * BS + r;
+    zr[r] = fmin(fmax(zr[r], lbs[i]), ubs[i]);
+  }
+  return code;
+}
+
+}  // namespace mpcqp

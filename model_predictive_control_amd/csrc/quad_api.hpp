@@ -1,0 +1,52 @@
+// quad_api.hpp -- host-side entry points of the 4-QPs-per-wavefront kernels
+// (quad_box.hip), used by the C ABI dispatchers for n <= 32.
+#pragma once
+#include <stdlib.h>
+
+#include "common.hpp"
+
+namespace mpcqp {
+
+template <typename T>
+struct BoxArgsQ {
+  int batch, n;
+  const T* H; int64_t sH;
+  const T* f; int64_t sf;
+  const T* lb; int64_t slb;
+  const T* ub; int64_t sub;
+  T* z;
+  int32_t* status;
+  int max_iter;
+  T tol;
+};
+
+template <typename T>
+struct MpcArgsQ {
+  int batch, nx, nu, N, tv;
+  const T* A; int64_t sA;
+  const T* B; int64_t sB;
+  const T* Q; int64_t sQ;
+  const T* R; int64_t sR;
+  const T* Qf; int64_t sQf;
+  const T* c; int64_t sC;
+  const T* x0; int64_t sX0;
+  const T* lb; int64_t slb;
+  const T* ub; int64_t sub;
+  T* z;
+  int32_t* status;
+  int max_iter;
+  T tol;
+};
+
+template <typename T>
+int solve_box_quad(const BoxArgsQ<T>& a, hipStream_t st);
+template <typename T>
+int mpc_box_quad(const MpcArgsQ<T>& a, hipStream_t st);
+
+// MPCQP_KERNEL=wave forces the one-QP-per-wavefront kernels (A/B runs).
+inline bool use_wave_kernels() {
+  const char* v = getenv("MPCQP_KERNEL");
+  return v && v[0] == 'w';
+}
+
+}  // namespace mpcqp

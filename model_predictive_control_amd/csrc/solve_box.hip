@@ -20,6 +20,7 @@
 // directions are column p of M; the subspace minimiser and the active-set
 // gradient are one mat-vec  s = M w,  w = (f_F, -z_A).
 #include "gi_box_core.hpp"
+#include "quad_api.hpp"
 
 namespace mpcqp {
 
@@ -125,6 +126,10 @@ static int solve_box_t(int batch, int n, const void* H, int64_t sH, const void* 
   a.z = (T*)z; a.status = status;
   a.max_iter = max_iter > 0 ? max_iter : 3 * n + 30;
   a.tol = tol > 0 ? (T)tol : (sizeof(T) == 8 ? (T)1e-12 : (T)1e-6);
+  if (n <= 32 && !use_wave_kernels()) {
+    BoxArgsQ<T> q{batch, n, a.H, sH, a.f, sf, a.lb, slb, a.ub, sub, a.z, status, a.max_iter, a.tol};
+    return solve_box_quad<T>(q, st);
+  }
   switch ((n + 7) / 8) {
     case 1: return launch_box<T, 1>(a, st);
     case 2: return launch_box<T, 2>(a, st);
