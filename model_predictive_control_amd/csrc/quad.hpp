@@ -128,32 +128,33 @@ struct QSym {
   }
 
   // Goodnight sweep (sigma = +1) / reverse sweep (sigma = -1) on pivot k with
-  // its column already fetched.  Row/column k are produced by the general
-  // rank-1 formula plus two indicator-weighted rank-1 corrections:
-  //   M' = M - a colc' + e_k w1' + w2 e_k',   a = colr/d, w2 = sigma a,
-  //   w1_j = sigma colc_j / d  (j != k),  w1_k = -1/d - sigma
-  // i.e. three FMAs per element and no per-element selects.
+  // its column already fetched:  M_ij - M_ik M_kj / d  off row/column k,
+  // sigma M_kj / d on row k, sigma M_ik / d on column k, -1/d at (k, k).
+  // Row/column k are selected, not produced by cancellation (their relative
+  // error would otherwise grow like eps * |d|).
   __device__ __forceinline__ void sweep_col(int k, T sigma, T d, const T (&colr)[BS],
                                             const T (&colc)[BS]) {
     const T rd = fast_rcp(d);
-    T a[BS], ik[BS], w2[BS], jk[BS], w1[BS];
+    T a[BS], scol[BS], srow[BS];
+    bool ik[BS], jk[BS];
 #pragma unroll
     for (int r = 0; r < BS; ++r) {
       a[r] = colr[r] * rd;
-      w2[r] = sigma * a[r];
-      ik[r] = (bi * BS + r == k) ? T(1) : T(0);
+      scol[r] = sigma * a[r];
+      ik[r] = (bi * BS + r == k);
     }
 #pragma unroll
     for (int c = 0; c < BS; ++c) {
-      const bool isk = (bj * BS + c == k);
-      jk[c] = isk ? T(1) : T(0);
-      w1[c] = isk ? (-rd - sigma) : sigma * colc[c] * rd;
+      jk[c] = (bj * BS + c == k);
+      srow[c] = jk[c] ? -rd : sigma * colc[c] * rd;
     }
 #pragma unroll
     for (int r = 0; r < BS; ++r)
 #pragma unroll
-      for (int c = 0; c < BS; ++c)
-        m[r][c] = fma(ik[r], w1[c], fma(w2[r], jk[c], fma(-a[r], colc[c], m[r][c])));
+      for (int c = 0; c < BS; ++c) {
+        const T gen = fma(-a[r], colc[c], m[r][c]);
+        m[r][c] = ik[r] ? srow[c] : (jk[c] ? scol[r] : gen);
+      }
   }
 
   __device__ __forceinline__ T sweep(int k, T sigma, T* gb) {
