@@ -1,9 +1,10 @@
 """Benchmark: QP solves/sec of the batched condensed-QP MPC step on MI355X.
 
-Workload (BASELINE.json configs[1], the config the metric is quoted on):
-double integrator of session_1/FHC.py:136-142 (Ts=0.5, Q=CC'+1e-3I, R=0.1,
-P_f=Q), horizon N=20, input box |u|<=1, batch 4096 random x0 ~ U(-10,10)^2
-per GPU, fp64.  One step = one pass of the hot path over one batch:
+Default workload: BASELINE.json configs[1], the config the metric is quoted on.
+It is the double integrator of session_1/FHC.py:136-142 (Ts=0.5, Q=CC'+1e-3I,
+R=0.1, P_f=Q), horizon N=20, input box |u|<=1, batch 4096 random
+x0 ~ U(-10,10)^2 per GPU, fp64.  One step = one pass of the hot path over one
+batch:
 
   --mode fused (default)
     mpcqp_mpc_box    per-instance (A, B, x0) -> z, status          [HIP, 1 launch]
@@ -11,18 +12,33 @@ per GPU, fp64.  One step = one pass of the hot path over one batch:
     mpcqp_condense   per-instance (A, B, x0) -> H (packed), f     [HIP]
     mpcqp_solve_box  -> z, status                                 [HIP]
 
-A and B are stored per instance (copies of the config-2 plant) so the
+A and B are stored per instance (copies of the config-2 plant), so the
 condensing really runs per instance, as the north star's "synthetic
-(A,B,Q,R,x0)" asks; Q, R, Qf are shared.  Inputs are resident in HBM before
-the timed region; steps cycle over 8 distinct x0 batches.  The step is
-captured once per batch slot into a HIP graph (torch.cuda.CUDAGraph) and
-replayed -- the kernels recompute everything on every replay.
+(A,B,Q,R,x0)" asks.  Q, R and Qf are shared.
 
-Multi-GPU (torchrun): each rank owns its own batch (weak scaling), no
-collective on the solve path; barrier + synchronize around the timed region,
-max over ranks.
+--config 3|4|5 runs the other BASELINE configs with the same
+contract; they are parity/roofline cases and not the headline line:
+  3  FE-linearised bicycle (parameters.py), N=30, ts=0.08, state box (x_1..x_N)
+     + input box, per-instance per-stage (A_k, B_k, c_k), fp32, B=65,536:
+     mpcqp_condense(TV: H, f, Gam, xbar) + row bounds + mpcqp_solve_qp
+  4  random stable LTI nx=12, nu=4, N=50, 40 random polytope rows (h>0),
+     shared condense, fp64, B=131,072 per GPU: f = F x0 + mpcqp_solve_poly
+  5  config-4 plant perturbed per instance and stage, N=40, input box, fp32,
+     B=32,768 per GPU: mpcqp_condense(TV: H, f) + mpcqp_solve_box (n = 160)
 
-Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
+In every config the inputs are resident in HBM before the timed region, and
+steps cycle over distinct x0 batches ("slots").  Each slot's step is captured
+once into a HIP graph (torch.cuda.CUDAGraph) and replayed; the kernels
+recompute everything on every replay.
+
+Per-kernel device times: HIP events around a graph of R back-to-back launches
+of that kernel alone, on the stream the graph runs on.
+
+Multi-GPU (torchrun): each rank owns its own batch (weak scaling), with no
+collective on the solve path.  There is a barrier and a synchronize around
+the timed region, and the time is the max over ranks.
+
+Prints ONE JSON line on rank 0 ("Measurement").
 """
 from __future__ import annotations
 
@@ -43,33 +59,558 @@ from model_predictive_control_amd import distributed as mdist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_PEAK_TFS = 78.6       # FP64 vector/matrix peak
+FP32_PEAK_TFS = 157.3      # FP32 vector/matrix peak
+METRIC = "QP solves/sec (batch, horizon N=20) at 1/2/4/8 MI355X; max|u-u_ref|"
 
 
-def config2_plant():
-    ts = 0.5
-    A = np.array([[1.0, ts], [0.0, 1.0]])
-    B = np.array([[0.0], [-ts]])
-    C = np.array([[1.0], [-2.0 / 3.0]])
-    Q = C @ C.T + 1e-3 * np.eye(2)
-    R = np.array([[0.1]])
-    return A, B, Q, R, Q.copy()
-
-
-def condense_bytes_per_instance(nx, nu, N, es=8):
-    """Algorithmic HBM bytes of mpcqp_condense per instance: in A, B, x0;
-    out H (packed lower), f  (SURVEY.md 8d formula with F replaced by f)."""
-    n = N * nu
-    return (nx * nx + nx * nu + nx + n * (n + 1) // 2 + n) * es
+# ------------------------------------------------------------- algorithmic counts
+def condense_bytes_per_instance(nx, nu, N, es=8, tv=False, gam=False, xbar=False,
+                                F=False, f=True):
+    """HBM bytes of mpcqp_condense per instance (SURVEY.md 8(d) formula):
+    inputs A, B (per stage when TV), x0; outputs packed H, f and whatever
+    else the workload asks for (Gam, xbar, F)."""
+    n, m = N * nu, N * nx
+    S = N if tv else 1
+    inp = S * (nx * nx + nx * nu) + nx + (S * nx if tv else 0)
+    out = n * (n + 1) // 2 + (n if f else 0) + (m * n if gam else 0) + (m if xbar else 0) \
+        + (n * nx if F else 0)
+    return (inp + out) * es
 
 
 def condense_flops_per_instance(nx, nu, N):
-    """SURVEY.md 8d algorithmic flop formula (Gamma recursion + Gam'QGam + F + Phi)."""
+    """SURVEY.md 8(d) algorithmic flop formula (Gamma recursion + Gam'QGam + F + Phi)."""
     n, m = N * nu, N * nx
     return N * (N + 1) // 2 * 2 * nx * nx * nu + m * n + m * n * n + 2 * n * m * nx + 2 * N * nx ** 3
 
 
-def solve_bytes_per_instance(n, es=8):
-    return (n * (n + 1) // 2 + n + n) * es + 4
+def solve_bytes_per_instance(n, es=8, m=0, G=False):
+    """QP solve: packed H, f, bounds in (shared bounds not counted), z +
+    status out; per-instance G rows and row bounds when G."""
+    return (n * (n + 1) // 2 + n + n) * es + 4 + ((m * n + 2 * m) * es if G else 0)
+
+
+def roof(kernel, bound, amount, ms, es_peak, unit, traffic=None, extra=None):
+    achieved = amount / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
+    d = {"kernel": kernel, "bound": bound, "achieved": round(achieved, 3), "peak": es_peak,
+         "unit": unit, "frac": round(achieved / es_peak, 5), "traffic": traffic,
+         "avg_launch_us": round(ms * 1e3, 2)}
+    d.update(extra or {})
+    return d
+
+
+def time_kernel(fn, reps: int, dev) -> float:
+    """Average device time (ms) of fn() from HIP events around a graph of
+    `reps` back-to-back launches replayed on its own stream."""
+    st = torch.cuda.Stream(device=dev)
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        for _ in range(reps):
+            fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = float("inf")
+    with torch.cuda.stream(st):
+        for _ in range(3):
+            e0.record(st)
+            g.replay()
+            e1.record(st)
+            e1.synchronize()
+            best = min(best, e0.elapsed_time(e1) / reps)
+    return best
+
+
+# ---------------------------------------------------------------- workloads
+class Config2:
+    """BASELINE configs[1]: FHC double integrator, N=20, |u|<=1, fp64."""
+
+    dtype = torch.float64
+    dname = "f64"
+    default_batch = 4096
+    default_slots = 8
+
+    def __init__(self, args, dev, rank):
+        self.args, self.dev = args, dev
+        ts = 0.5
+        A = np.array([[1.0, ts], [0.0, 1.0]])
+        B = np.array([[0.0], [-ts]])
+        C = np.array([[1.0], [-2.0 / 3.0]])
+        Q = C @ C.T + 1e-3 * np.eye(2)
+        self.A, self.B, self.Q, self.R, self.Qf = A, B, Q, np.array([[0.1]]), Q.copy()
+        self.nx, self.nu, self.N = 2, 1, args.horizon or 20
+        n = self.n = self.N
+        bsz, S = args.batch, args.slots
+        dt = self.dtype
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)  # noqa: E731
+        rng = np.random.default_rng(20261015 + 2 + 1000 * rank)
+        self.X0 = rng.uniform(-10.0, 10.0, size=(S, bsz, 2))
+        self.A_b = t(np.broadcast_to(A, (bsz, 2, 2)))
+        self.B_b = t(np.broadcast_to(B, (bsz, 2, 1)))
+        self.Q_t, self.R_t, self.Qf_t = t(Q), t(self.R), t(Q)
+        self.X0_t = t(self.X0)
+        self.lb = torch.full((n,), -1.0, dtype=dt, device=dev)
+        self.ub = torch.full((n,), 1.0, dtype=dt, device=dev)
+        self.H = torch.empty((bsz, n * (n + 1) // 2), dtype=dt, device=dev)
+        self.f = torch.empty((bsz, n), dtype=dt, device=dev)
+        self.Z = torch.empty((S, bsz, n), dtype=dt, device=dev)
+        self.ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
+        self.Zs = torch.empty((bsz, n), dtype=dt, device=dev)
+        self.STs = torch.empty((bsz,), dtype=torch.int32, device=dev)
+
+    def workload(self):
+        return {"workload": "cfg2: per-instance condense + box QP, FHC.py double integrator "
+                            "(ts=0.5), N=20, |u|<=1, x0~U(-10,10)^2",
+                "horizon": self.N, "nx": self.nx, "nu": self.nu, "mode": self.args.mode}
+
+    def _condense(self, s):
+        batched.condense(self.A_b, self.B_b, self.Q_t, self.R_t, self.Qf_t, self.N,
+                         x0=self.X0_t[s], outputs=("H", "f"), out={"H": self.H, "f": self.f})
+
+    def _solve(self, s, out):
+        batched.solve_box(self.H, self.f, self.lb, self.ub, out=out)
+
+    def _fused(self, s):
+        batched.mpc_box(self.A_b, self.B_b, self.Q_t, self.R_t, self.Qf_t, self.N, self.X0_t[s],
+                        self.lb, self.ub, out=(self.Z[s], self.ST[s]))
+
+    def step(self, s):
+        if self.args.mode == "fused":
+            self._fused(s)
+        else:
+            self._condense(s)
+            self._solve(s, (self.Z[s], self.ST[s]))
+
+    def status(self):
+        return self.ST
+
+    def kernels(self, traffic):
+        """Per-kernel device times and rooflines; returns (dominant, others)."""
+        R = self.args.reps
+        bsz, nx, nu, N, n = self.args.batch, self.nx, self.nu, self.N, self.n
+        self._condense(0)
+        t_c = time_kernel(lambda: self._condense(0), R, self.dev)
+        t_s = time_kernel(lambda: self._solve(0, (self.Zs, self.STs)), R, self.dev)
+        t_f = time_kernel(lambda: self._fused(0), R, self.dev)
+        cb = condense_bytes_per_instance(nx, nu, N) * bsz
+        sb = solve_bytes_per_instance(n) * bsz
+        fl = condense_flops_per_instance(nx, nu, N) * bsz
+        r_c = roof("condense_kernel<double,2>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
+                   traffic.get("condense"), {"bytes_per_launch": cb})
+        r_s = roof("box_quad_kernel<double,5>", "hbm", sb, t_s, HBM_PEAK_GBS, "GB/s",
+                   traffic.get("solve_box"), {"bytes_per_launch": sb})
+        # fused kernel: SURVEY.md 8(d) per-instance figure (22.0 kflop condense,
+        # config 2) against the fp64 peak; it moves only A, B, x0 in and z out.
+        r_f = roof("mpc_quad_kernel<double,2,1,5>", "mfma", fl, t_f, FP64_PEAK_TFS, "TFLOP/s",
+                   traffic.get("mpc_box"), {"flops_per_launch": fl,
+                                            "hbm_bytes_per_launch": (nx * nx + nx * nu + nx + n) * 8 * bsz + 4 * bsz})
+        # split vs fused agreement on the same slot
+        self._fused(0)
+        self._condense(0)
+        self._solve(0, (self.Zs, self.STs))
+        torch.cuda.synchronize()
+        extra = {"kernel_us": {"mpc_box": round(t_f * 1e3, 2), "condense": round(t_c * 1e3, 2),
+                               "solve_box": round(t_s * 1e3, 2)},
+                 "split_vs_fused_max_abs": float((self.Zs - self.Z[0]).abs().max())}
+        if self.args.mode == "fused":
+            return r_f, {"roofline_condense": r_c, "roofline_solve_box": r_s}, extra
+        dom = r_s if t_s >= t_c else r_c
+        return dom, {"roofline_condense": r_c, "roofline_solve_box": r_s}, extra
+
+    def check(self):
+        from oracle import cbaseline as cbl
+
+        nchk = min(256, self.args.batch)
+        zr, _ = cbl.mpc_box(self.A, self.B, self.Q, self.R, self.Qf, self.N, self.X0[0, :nchk],
+                            -1.0, 1.0, nthreads=1)
+        return float(np.abs(self.Z[0, :nchk].cpu().numpy() - zr).max())
+
+    def cpu_baseline(self, seconds):
+        from oracle import cbaseline as cbl
+
+        bsz = self.args.batch
+        cores = min(16, len(os.sched_getaffinity(0)))
+        Xc = self.X0.reshape(-1, 2)
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            cbl.mpc_box(self.A, np.broadcast_to(self.B, (bsz, 2, 1)), self.Q, self.R, self.Qf,
+                        self.N, Xc[:bsz], -1.0, 1.0, nthreads=cores)
+            done += bsz
+        dt = time.perf_counter() - t0
+        return {"value": round(done / dt, 1), "unit": "solves/s", "cores": cores, "kind": "port",
+                "sample": f"{done} config-2 solves (per-instance condense + GI box QP, C/OpenMP "
+                          f"oracle/c/mpcqp_oracle.c) in {dt:.1f} s on {cores} host threads"}
+
+
+def _stable_plant(rng, nx, nu, rho=0.98):
+    U, _ = np.linalg.qr(rng.normal(size=(nx, nx)))
+    sig = rng.uniform(0.5, rho, size=nx)
+    A = (U * sig) @ U.T
+    B = rng.normal(size=(nx, nu)) / np.sqrt(nx)
+    return A, B
+
+
+class Config3:
+    """FE-linearised bicycle, N=30, state + input box, per-instance TV, fp32."""
+
+    dtype = torch.float32
+    dname = "f32"
+    default_batch = 65536
+    default_slots = 2
+
+    def __init__(self, args, dev, rank):
+        from model_predictive_control_amd.bicycle import fe_linearize_batched, fe_step_batched
+        from model_predictive_control_amd.parameters import VehicleParameters
+
+        self.args, self.dev = args, dev
+        p = self.p = VehicleParameters()
+        self.nx, self.nu, self.N, self.ts = 4, 2, args.horizon or 30, 0.08
+        N, nx, nu = self.N, self.nx, self.nu
+        n, m = N * nu, N * nx
+        self.n, self.m = n, m
+        bsz, S = args.batch, args.slots
+        dt = self.dtype
+        rng = np.random.default_rng(20261015 + 3 + 1000 * rank)
+        X0 = np.stack([rng.uniform(-1, 1, (S, bsz)), rng.uniform(-.5, .5, (S, bsz)),
+                       rng.uniform(-np.pi / 4, np.pi / 4, (S, bsz)), rng.uniform(-.3, .3, (S, bsz))], -1)
+        self.X0 = X0
+        Q = np.diag([1., 6., .2, .05])
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)  # noqa: E731
+        self.Qn, self.QNn, self.Rn = Q, 100 * Q, np.diag([1., .01])
+        self.Q_t, self.QN_t, self.R_t = t(Q), t(100 * Q), t(self.Rn)
+        # per-slot linearisation about the zero-input rollout (RTI first iterate)
+        self.A, self.B, self.c, self.X0_t = [], [], [], []
+        for s in range(S):
+            x = torch.as_tensor(X0[s], dtype=torch.float64, device=dev)
+            u = torch.zeros((bsz, nu), dtype=torch.float64, device=dev)
+            As, Bs, cs = [], [], []
+            for _ in range(N):
+                Ak, Bk, ck = fe_linearize_batched(x, u, p, self.ts)
+                As.append(Ak); Bs.append(Bk); cs.append(ck)
+                x = fe_step_batched(x, u, p, self.ts)
+            self.A.append(torch.stack(As, 1).to(dt).contiguous())
+            self.B.append(torch.stack(Bs, 1).to(dt).contiguous())
+            self.c.append(torch.stack(cs, 1).to(dt).contiguous())
+            self.X0_t.append(t(X0[s]))
+        xmin = np.array([p.min_pos_x, p.min_pos_y, p.min_heading, p.min_vel])
+        xmax = np.array([p.max_pos_x, p.max_pos_y, p.max_heading, p.max_vel])
+        self.xmin_t, self.xmax_t = t(np.tile(xmin, N)), t(np.tile(xmax, N))
+        self.xmin, self.xmax = xmin, xmax
+        self.lbz = t(np.tile([p.min_drive, -p.max_steer], N))
+        self.ubz = t(np.tile([p.max_drive, p.max_steer], N))
+        self.out = {"H": torch.empty((bsz, n * (n + 1) // 2), dtype=dt, device=dev),
+                    "f": torch.empty((bsz, n), dtype=dt, device=dev),
+                    "Gam": torch.empty((bsz, m, n), dtype=dt, device=dev),
+                    "xbar": torch.empty((bsz, m), dtype=dt, device=dev)}
+        self.hl = torch.empty((bsz, m), dtype=dt, device=dev)
+        self.hu = torch.empty((bsz, m), dtype=dt, device=dev)
+        self.Z = torch.empty((S, bsz, n), dtype=dt, device=dev)
+        self.Y = torch.empty((bsz, m), dtype=dt, device=dev)
+        self.ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
+
+    def workload(self):
+        return {"workload": "cfg3: FE-linearised bicycle (parameters.py), ts=0.08, N=30, "
+                            "Q=diag(1,6,.2,.05), QN=100Q, R=diag(1,.01), state box x_1..x_N + "
+                            "input box, per-instance per-stage (A_k,B_k,c_k) about the zero-input "
+                            "rollout; condense(TV) + solve_qp",
+                "horizon": self.N, "nx": self.nx, "nu": self.nu, "rows": self.m}
+
+    def _condense(self, s):
+        batched.condense(self.A[s], self.B[s], self.Q_t, self.R_t, self.QN_t, self.N,
+                         x0=self.X0_t[s], c=self.c[s], tv=True, outputs=("H", "f", "Gam", "xbar"),
+                         out=self.out)
+        torch.sub(self.xmin_t, self.out["xbar"], out=self.hl)
+        torch.sub(self.xmax_t, self.out["xbar"], out=self.hu)
+
+    def _solve(self, s):
+        batched.solve_qp(self.out["H"], self.out["f"], self.out["Gam"], self.hl, self.hu,
+                         self.lbz, self.ubz, out=(self.Z[s], self.Y, self.ST[s]))
+
+    def step(self, s):
+        self._condense(s)
+        self._solve(s)
+
+    def status(self):
+        return self.ST
+
+    def kernels(self, traffic):
+        R = self.args.reps
+        bsz, nx, nu, N, n, m = self.args.batch, self.nx, self.nu, self.N, self.n, self.m
+        self._condense(0)
+        t_c = time_kernel(lambda: batched.condense(
+            self.A[0], self.B[0], self.Q_t, self.R_t, self.QN_t, self.N, x0=self.X0_t[0],
+            c=self.c[0], tv=True, outputs=("H", "f", "Gam", "xbar"), out=self.out), R, self.dev)
+        t_s = time_kernel(lambda: self._solve(0), R, self.dev)
+        cb = condense_bytes_per_instance(nx, nu, N, 4, tv=True, gam=True, xbar=True) * bsz
+        sb = solve_bytes_per_instance(n, 4, m, G=True) * bsz
+        r_c = roof("condense_kernel<float,4>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
+                   traffic.get("condense"), {"bytes_per_launch": cb})
+        r_s = roof("qp_wg_kernel<float,192>", "hbm", sb, t_s, HBM_PEAK_GBS, "GB/s",
+                   traffic.get("solve_qp"), {"bytes_per_launch": sb})
+        extra = {"kernel_us": {"condense": round(t_c * 1e3, 2), "solve_qp": round(t_s * 1e3, 2)}}
+        dom, other = (r_s, r_c) if t_s >= t_c else (r_c, r_s)
+        return dom, {"roofline_other": other}, extra
+
+    def check(self):
+        """fp64 oracle (explicit condensing + Goldfarb-Idnani) on a few
+        instances of slot 0, from the same (A_k, B_k, c_k, x0)."""
+        from oracle import condense as oc
+        from oracle import qp as oq
+
+        N, nu = self.N, self.nu
+        errs = []
+        A, B, c = self.A[0].double().cpu().numpy(), self.B[0].double().cpu().numpy(), \
+            self.c[0].double().cpu().numpy()
+        Z = self.Z[0].double().cpu().numpy()
+        code = batched.status_code(self.ST[0]).cpu().numpy()
+        for i in range(min(4, self.args.batch)):
+            d = oc.condense(A[i], B[i], self.Qn, self.Rn, self.QNn, N, x0=self.X0[0, i], c=c[i])
+            G = np.vstack([d["Gam"], -d["Gam"]])
+            h = np.concatenate([np.tile(self.xmax, N) - d["xbar"], -(np.tile(self.xmin, N) - d["xbar"])])
+            lb = np.tile([self.p.min_drive, -self.p.max_steer], N)
+            ub = np.tile([self.p.max_drive, self.p.max_steer], N)
+            try:
+                zr = oq.poly_qp(d["H"], d["f"], G, h, lb, ub)[0]
+            except ValueError:
+                assert code[i] == 3
+                continue
+            errs.append(np.abs(Z[i] - zr).max())
+        return float(max(errs)) if errs else None
+
+    def cpu_baseline(self, seconds):
+        from oracle import condense as oc
+        from oracle import qp as oq
+
+        N = self.N
+        A, B, c = self.A[0].double().cpu().numpy(), self.B[0].double().cpu().numpy(), \
+            self.c[0].double().cpu().numpy()
+        lb = np.tile([self.p.min_drive, -self.p.max_steer], N)
+        ub = np.tile([self.p.max_drive, self.p.max_steer], N)
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds and done < self.args.batch:
+            d = oc.condense(A[done], B[done], self.Qn, self.Rn, self.QNn, N, x0=self.X0[0, done], c=c[done])
+            G = np.vstack([d["Gam"], -d["Gam"]])
+            h = np.concatenate([np.tile(self.xmax, N) - d["xbar"], -(np.tile(self.xmin, N) - d["xbar"])])
+            try:
+                oq.poly_qp(d["H"], d["f"], G, h, lb, ub)
+            except ValueError:
+                pass
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": round(done / dt, 2), "unit": "solves/s", "cores": 1, "kind": "port",
+                "sample": f"{done} config-3 instances: NumPy explicit condensing (oracle/condense.py) "
+                          f"+ Goldfarb-Idnani (oracle/qp.py) in {dt:.1f} s, 1 thread"}
+
+
+class Config4:
+    """Random stable LTI nx=12, nu=4, N=50, 40 polytope rows; shared condense; fp64."""
+
+    dtype = torch.float64
+    dname = "f64"
+    default_batch = 131072
+    default_slots = 2
+
+    def __init__(self, args, dev, rank):
+        self.args, self.dev = args, dev
+        self.nx, self.nu, self.N, self.m = 12, 4, args.horizon or 50, 40
+        nx, nu, N, m = self.nx, self.nu, self.N, self.m
+        n = self.n = N * nu
+        bsz, S = args.batch, args.slots
+        dt = self.dtype
+        rng = np.random.default_rng(20261015 + 4)          # plant shared by all ranks
+        A, B = _stable_plant(rng, nx, nu)
+        self.A, self.B = A, B
+        self.Qn, self.Rn = np.eye(nx), 0.1 * np.eye(nu)
+        self.G = rng.normal(size=(m, n))
+        self.h = rng.uniform(0.5, 1.5, size=m)
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)  # noqa: E731
+        d = batched.condense(t(A), t(B), t(self.Qn), t(self.Rn), t(self.Qn), N, outputs=("H", "F"))
+        self.Hs, self.F = d["H"][0].contiguous(), d["F"][0].contiguous()
+        self.G_t, self.h_t = t(self.G), t(self.h)
+        xr = np.random.default_rng(20261015 + 4 + 1000 * (rank + 1))
+        self.X0 = xr.normal(size=(S, bsz, nx)) * 3.0
+        self.X0_t = t(self.X0)
+        self.f = torch.empty((bsz, n), dtype=dt, device=dev)
+        self.Z = torch.empty((S, bsz, n), dtype=dt, device=dev)
+        self.ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
+
+    def workload(self):
+        return {"workload": "cfg4: random stable LTI nx=12 nu=4 (rho<=0.98), Q=I, R=0.1I, N=50, "
+                            "40 random polytope rows G z <= h (h>0), shared condense; "
+                            "f = F x0 + solve_poly", "horizon": self.N, "nx": self.nx,
+                "nu": self.nu, "rows": self.m}
+
+    def _f(self, s):
+        batched.gemv(self.F, self.X0_t[s], y=self.f)
+
+    def _solve(self, s):
+        z, y, st = batched.solve_poly(self.Hs, self.f, self.G_t, None, self.h_t)
+        self.Z[s].copy_(z)
+        self.ST[s].copy_(st)
+
+    def step(self, s):
+        self._f(s)
+        self._solve(s)
+
+    def status(self):
+        return self.ST
+
+    def kernels(self, traffic):
+        R = self.args.reps
+        bsz, n, m, nx = self.args.batch, self.n, self.m, self.nx
+        self._f(0)
+        t_f = time_kernel(lambda: self._f(0), R, self.dev)
+        t_s = time_kernel(lambda: self._solve(0), R, self.dev)
+        sb = (nx + n + 4) * 8 * bsz       # x0 in (through f), z + status out
+        r_s = roof("solve_poly (shared phase + dual_range_kernel<double,5> + gemv)", "hbm", sb, t_s,
+                   HBM_PEAK_GBS, "GB/s", traffic.get("solve_poly"), {"bytes_per_launch": sb})
+        fb = (nx + n) * 8 * bsz
+        r_f = roof("gemv_kernel<double>", "hbm", fb, t_f, HBM_PEAK_GBS, "GB/s", None,
+                   {"bytes_per_launch": fb})
+        extra = {"kernel_us": {"gemv_f": round(t_f * 1e3, 2), "solve_poly": round(t_s * 1e3, 2)}}
+        return r_s, {"roofline_other": r_f}, extra
+
+    def check(self):
+        from oracle import condense as oc
+        from oracle import qp as oq
+
+        d = oc.condense(self.A, self.B, self.Qn, self.Rn, self.Qn, self.N)
+        Z = self.Z[0].cpu().numpy()
+        errs = []
+        for i in range(min(4, self.args.batch)):
+            zr = oq.poly_qp(d["H"], d["F"] @ self.X0[0, i], self.G, self.h)[0]
+            errs.append(np.abs(Z[i] - zr).max())
+        return float(max(errs))
+
+    def cpu_baseline(self, seconds):
+        from oracle import condense as oc
+        from oracle import qp as oq
+
+        d = oc.condense(self.A, self.B, self.Qn, self.Rn, self.Qn, self.N)
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds and done < self.args.batch:
+            oq.poly_qp(d["H"], d["F"] @ self.X0[0, done], self.G, self.h)
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": round(done / dt, 2), "unit": "solves/s", "cores": 1, "kind": "port",
+                "sample": f"{done} config-4 instances: NumPy Goldfarb-Idnani (oracle/qp.py) on the "
+                          f"shared condensed QP in {dt:.1f} s, 1 thread"}
+
+
+class Config5:
+    """Config-4 plant perturbed per instance/stage, N=40, input box, fp32."""
+
+    dtype = torch.float32
+    dname = "f32"
+    default_batch = 32768
+    default_slots = 2
+
+    def __init__(self, args, dev, rank):
+        self.args, self.dev = args, dev
+        self.nx, self.nu, self.N = 12, 4, args.horizon or 40
+        nx, nu, N = self.nx, self.nu, self.N
+        n = self.n = N * nu
+        bsz, S = args.batch, args.slots
+        dt = self.dtype
+        rng = np.random.default_rng(20261015 + 4)
+        A, B = _stable_plant(rng, nx, nu)
+        self.Qn, self.Rn = np.eye(nx), 0.1 * np.eye(nu)
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)  # noqa: E731
+        g = torch.Generator(device=dev)
+        g.manual_seed(20261015 + 5 + 1000 * rank)
+        eps = 0.01
+        self.A, self.B, self.X0_t = [], [], []
+        for s in range(S):
+            self.A.append((t(A) + eps * torch.randn((bsz, N, nx, nx), generator=g, device=dev,
+                                                    dtype=dt)).contiguous())
+            self.B.append((t(B) + eps * torch.randn((bsz, N, nx, nu), generator=g, device=dev,
+                                                    dtype=dt)).contiguous())
+            self.X0_t.append((3.0 * torch.randn((bsz, nx), generator=g, device=dev, dtype=dt)).contiguous())
+        self.Q_t, self.R_t = t(self.Qn), t(self.Rn)
+        self.lb, self.ub = -0.5, 0.5
+        self.out = {"H": torch.empty((bsz, n * (n + 1) // 2), dtype=dt, device=dev),
+                    "f": torch.empty((bsz, n), dtype=dt, device=dev)}
+        self.Z = torch.empty((S, bsz, n), dtype=dt, device=dev)
+        self.ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
+        self.lb_t = torch.full((n,), self.lb, dtype=dt, device=dev)
+        self.ub_t = torch.full((n,), self.ub, dtype=dt, device=dev)
+
+    def workload(self):
+        return {"workload": "cfg5: config-4 plant (nx=12, nu=4) with per-instance per-stage "
+                            "perturbation A_k=A+0.01*D_k, B_k=B+0.01*E_k, N=40, |u|<=0.5, "
+                            "re-condensed every step: condense(TV) + solve_box (n=160)",
+                "horizon": self.N, "nx": self.nx, "nu": self.nu}
+
+    def _condense(self, s):
+        batched.condense(self.A[s], self.B[s], self.Q_t, self.R_t, self.Q_t, self.N,
+                         x0=self.X0_t[s], tv=True, outputs=("H", "f"), out=self.out)
+
+    def _solve(self, s):
+        batched.solve_box(self.out["H"], self.out["f"], self.lb_t, self.ub_t, out=(self.Z[s], self.ST[s]))
+
+    def step(self, s):
+        self._condense(s)
+        self._solve(s)
+
+    def status(self):
+        return self.ST
+
+    def kernels(self, traffic):
+        R = self.args.reps
+        bsz, nx, nu, N, n = self.args.batch, self.nx, self.nu, self.N, self.n
+        self._condense(0)
+        t_c = time_kernel(lambda: self._condense(0), R, self.dev)
+        t_s = time_kernel(lambda: self._solve(0), R, self.dev)
+        fl = condense_flops_per_instance(nx, nu, N) * bsz
+        cb = condense_bytes_per_instance(nx, nu, N, 4, tv=True) * bsz
+        r_c = roof("condense_kernel<float,12>", "mfma", fl, t_c, FP32_PEAK_TFS, "TFLOP/s",
+                   traffic.get("condense"), {"flops_per_launch": fl, "hbm_bytes_per_launch": cb,
+                                             "hbm_GBs": round(cb / (t_c * 1e-3) / 1e9, 1)})
+        sb = solve_bytes_per_instance(n, 4) * bsz
+        r_s = roof("qp_wg_kernel<float,160>", "hbm", sb, t_s, HBM_PEAK_GBS, "GB/s",
+                   traffic.get("solve_box"), {"bytes_per_launch": sb})
+        extra = {"kernel_us": {"condense": round(t_c * 1e3, 2), "solve_box": round(t_s * 1e3, 2)}}
+        dom, other = (r_s, r_c) if t_s >= t_c else (r_c, r_s)
+        return dom, {"roofline_other": other}, extra
+
+    def check(self):
+        from oracle import condense as oc
+        from oracle import qp as oq
+
+        N = self.N
+        A, B = self.A[0].double().cpu().numpy(), self.B[0].double().cpu().numpy()
+        X0 = self.X0_t[0].double().cpu().numpy()
+        Z = self.Z[0].double().cpu().numpy()
+        errs = []
+        for i in range(min(2, self.args.batch)):
+            d = oc.condense(A[i], B[i], self.Qn, self.Rn, self.Qn, N, x0=X0[i])
+            zr = oq.box_qp(d["H"], d["f"], np.full(self.n, self.lb), np.full(self.n, self.ub))[0]
+            errs.append(np.abs(Z[i] - zr).max())
+        return float(max(errs))
+
+    def cpu_baseline(self, seconds):
+        from oracle import condense as oc
+        from oracle import qp as oq
+
+        N = self.N
+        A, B = self.A[0].double().cpu().numpy(), self.B[0].double().cpu().numpy()
+        X0 = self.X0_t[0].double().cpu().numpy()
+        done = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds and done < self.args.batch:
+            d = oc.condense(A[done], B[done], self.Qn, self.Rn, self.Qn, N, x0=X0[done])
+            oq.box_qp(d["H"], d["f"], np.full(self.n, self.lb), np.full(self.n, self.ub))
+            done += 1
+        dt = time.perf_counter() - t0
+        return {"value": round(done / dt, 2), "unit": "solves/s", "cores": 1, "kind": "port",
+                "sample": f"{done} config-5 instances: NumPy explicit condensing + primal active "
+                          f"set (oracle/) in {dt:.1f} s, 1 thread"}
+
+
+CONFIGS = {2: Config2, 3: Config3, 4: Config4, 5: Config5}
 
 
 def main():
@@ -77,18 +618,22 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU per step")
-    ap.add_argument("--horizon", type=int, default=20)
-    ap.add_argument("--slots", type=int, default=8, help="distinct x0 batches cycled over")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="instances per GPU per step (0 = config default)")
+    ap.add_argument("--horizon", type=int, default=0, help="N (0 = config default)")
+    ap.add_argument("--slots", type=int, default=0, help="distinct x0 batches cycled over")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--profile-steps", type=int, default=50)
-    ap.add_argument("--mode", choices=("fused", "split"), default="fused")
+    ap.add_argument("--reps", type=int, default=20, help="launches per kernel-timing graph")
+    ap.add_argument("--mode", choices=("fused", "split"), default="fused", help="config 2 only")
     ap.add_argument("--traffic", default=None,
                     help="JSON with PMC-measured HBM bytes per launch {kernel: bytes} "
                          "(tools/prof_counters.sh); fills roofline.traffic")
     args = ap.parse_args()
+    C = CONFIGS[args.config]
+    args.batch = args.batch or C.default_batch
+    args.slots = args.slots or C.default_slots
 
     rank, world, local = mdist.env_rank_world()
     torch.cuda.set_device(local)
@@ -98,38 +643,10 @@ def main():
 
         dist.init_process_group("nccl", device_id=dev)
 
-    A, B, Q, R, Qf = config2_plant()
-    nx, nu, N = 2, 1, args.horizon
-    n = N * nu
-    bsz, S = args.batch, args.slots
-    dt = torch.float64
-    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)  # noqa: E731
-    rng = np.random.default_rng(20261015 + 2 + 1000 * rank)
-    X0 = rng.uniform(-10.0, 10.0, size=(S, bsz, nx))
-    A_b = t(np.broadcast_to(A, (bsz, nx, nx)))
-    B_b = t(np.broadcast_to(B, (bsz, nx, nu)))
-    Q_t, R_t, Qf_t = t(Q), t(R), t(Qf)
-    X0_t = t(X0)
-    lb = torch.full((n,), -1.0, dtype=dt, device=dev)
-    ub = torch.full((n,), 1.0, dtype=dt, device=dev)
-    H = torch.empty((S, bsz, n * (n + 1) // 2), dtype=dt, device=dev)
-    f = torch.empty((S, bsz, n), dtype=dt, device=dev)
-    Z = torch.empty((S, bsz, n), dtype=dt, device=dev)
-    ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
-
-    def step_split(s):
-        batched.condense(A_b, B_b, Q_t, R_t, Qf_t, N, x0=X0_t[s], outputs=("H", "f"),
-                         out={"H": H[s], "f": f[s]})
-        batched.solve_box(H[s], f[s], lb, ub, out=(Z[s], ST[s]))
-
-    def step_fused(s):
-        batched.mpc_box(A_b, B_b, Q_t, R_t, Qf_t, N, X0_t[s], lb, ub, out=(Z[s], ST[s]))
-
-    step = step_fused if args.mode == "fused" else step_split
-
-    # warm the JIT-free path once per slot, then capture
+    wl = C(args, dev, rank)
+    S = args.slots
     for s in range(S):
-        step(s)
+        wl.step(s)
     torch.cuda.synchronize()
     graphs = None
     if not args.no_graph:
@@ -139,7 +656,7 @@ def main():
             for s in range(S):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=cap):
-                    step(s)
+                    wl.step(s)
                 graphs.append(g)
             torch.cuda.synchronize()
         except Exception as e:  # pragma: no cover - reported in the JSON
@@ -150,7 +667,7 @@ def main():
         if graphs is not None:
             graphs[k % S].replay()
         else:
-            step(k % S)
+            wl.step(k % S)
 
     for k in range(args.warmup):
         run(k)
@@ -166,35 +683,13 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = mdist.max_over_ranks(elapsed, dev)
-    value = world * bsz * args.steps / elapsed
+    value = world * args.batch * args.steps / elapsed
 
     # ---- correctness of what was timed: statuses + oracle spot check (rank 0)
-    code = batched.status_code(ST)
+    st = wl.status()
+    code = batched.status_code(st)
     opt_frac = float((code == 0).double().mean())
-    iters = batched.status_iters(ST).double()
-
-    # ---- per-kernel durations with HIP events on the launch stream (eager)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    tc = ts_ = tf = 0.0
-    P = args.profile_steps
-    Zc = torch.empty_like(Z[0])
-    STc = torch.empty_like(ST[0])
-    for k in range(P):
-        s = k % S
-        ev[0].record()
-        batched.condense(A_b, B_b, Q_t, R_t, Qf_t, N, x0=X0_t[s], outputs=("H", "f"),
-                         out={"H": H[s], "f": f[s]})
-        ev[1].record()
-        batched.solve_box(H[s], f[s], lb, ub, out=(Zc, STc))
-        ev[2].record()
-        batched.mpc_box(A_b, B_b, Q_t, R_t, Qf_t, N, X0_t[s], lb, ub, out=(Z[s], ST[s]))
-        ev[3].record()
-        ev[3].synchronize()
-        tc += ev[0].elapsed_time(ev[1])
-        ts_ += ev[1].elapsed_time(ev[2])
-        tf += ev[2].elapsed_time(ev[3])
-    cond_ms, solve_ms, fused_ms = tc / P, ts_ / P, tf / P
-    split_vs_fused = float((Zc - Z[(P - 1) % S]).abs().max())
+    iters = batched.status_iters(st).double()
 
     out = None
     if rank == 0:
@@ -202,53 +697,16 @@ def main():
         if args.traffic:
             with open(args.traffic) as fh:
                 traffic = json.load(fh)
-        cb_bytes = condense_bytes_per_instance(nx, nu, N) * bsz
-        sv_bytes = solve_bytes_per_instance(n) * bsz
-        cond_gbs = cb_bytes / (cond_ms * 1e-3) / 1e9
-        solve_gbs = sv_bytes / (solve_ms * 1e-3) / 1e9
-        roof_cond = {"kernel": "condense_kernel<double,2>", "bound": "hbm", "achieved": round(cond_gbs, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(cond_gbs / HBM_PEAK_GBS, 4),
-                     "traffic": traffic.get("condense"), "bytes_per_launch": cb_bytes,
-                     "avg_launch_us": round(cond_ms * 1e3, 2)}
-        roof_solve = {"kernel": "box_gi_kernel<double,3>", "bound": "hbm", "achieved": round(solve_gbs, 1),
-                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(solve_gbs / HBM_PEAK_GBS, 4),
-                      "traffic": traffic.get("solve_box"), "bytes_per_launch": sv_bytes,
-                      "avg_launch_us": round(solve_ms * 1e3, 2)}
-        # fused kernel: SURVEY.md 8(d) per-instance figure (22.0 kflop condense,
-        # config 2) against the fp64 peak; it moves only A, B, x0 in and z out.
-        fl = condense_flops_per_instance(nx, nu, N) * bsz
-        fused_tfs = fl / (fused_ms * 1e-3) / 1e12
-        roof_fused = {"kernel": "mpc_box_kernel<double,2,1,3>", "bound": "mfma", "achieved": round(fused_tfs, 3),
-                      "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": round(fused_tfs / FP64_PEAK_TFS, 4),
-                      "traffic": traffic.get("mpc_box"), "flops_per_launch": fl,
-                      "hbm_bytes_per_launch": (nx * nx + nx * nu + nx + n) * 8 * bsz + 4 * bsz,
-                      "avg_launch_us": round(fused_ms * 1e3, 2)}
-        if args.mode == "fused":
-            roofline = roof_fused
-        else:
-            roofline = roof_solve if solve_ms >= cond_ms else roof_cond
-        # oracle spot check of the timed outputs (first 256 instances of slot 0)
-        from oracle import cbaseline as cbl
-
-        nchk = min(256, bsz)
-        zr, _ = cbl.mpc_box(A, B, Q, R, Qf, N, X0[0, :nchk], -1.0, 1.0, nthreads=1)
-        err = float(np.abs(Z[0, :nchk].cpu().numpy() - zr).max())
+        err = wl.check()
+        dom, others, extra = wl.kernels(traffic)
         cpu = None
         if not args.no_cpu and world == 1:
-            cores = min(16, len(os.sched_getaffinity(0)))
-            Xc = X0.reshape(-1, nx)
-            done = 0
-            tc0 = time.perf_counter()
-            while time.perf_counter() - tc0 < args.cpu_seconds:
-                cbl.mpc_box(A, np.broadcast_to(B, (bsz, nx, nu)), Q, R, Qf, N, Xc[:bsz], -1.0, 1.0,
-                            nthreads=cores)
-                done += bsz
-            cdt = time.perf_counter() - tc0
-            cpu = {"value": round(done / cdt, 1), "unit": "solves/s", "cores": cores, "kind": "port",
-                   "sample": f"{done} config-2 solves (per-instance condense + GI box QP, C/OpenMP "
-                             f"oracle/c/mpcqp_oracle.c) in {cdt:.1f} s on {cores} host threads"}
+            cpu = wl.cpu_baseline(args.cpu_seconds)
+        cfg = wl.workload()
+        cfg.update({"batch_per_gpu": args.batch, "parallelism": f"dp{world}",
+                    "graph": graphs is not None, "config": args.config})
         out = {
-            "metric": "QP solves/sec (batch, horizon N=20) at 1/2/4/8 MI355X; max|u-u_ref|",
+            "metric": METRIC,
             "value": round(value, 1),
             "unit": "solves/s",
             "n_gpus": world,
@@ -258,25 +716,19 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": wl.dname,
             "data": "synthetic",
-            "config": {"workload": "cfg2: per-instance condense + box QP, FHC.py double integrator "
-                                   "(ts=0.5), N=20, |u|<=1, x0~U(-10,10)^2",
-                       "batch_per_gpu": bsz, "horizon": N, "nx": nx, "nu": nu,
-                       "parallelism": f"dp{world}", "graph": graphs is not None,
-                       "mode": args.mode},
+            "config": cfg,
             "max_abs_u_err_vs_oracle": err,
             "optimal_frac": opt_frac,
+            "status_hist": {int(k): int(v) for k, v in zip(*np.unique(code.cpu().numpy(), return_counts=True))},
             "iters_mean": round(float(iters.mean()), 2),
             "iters_max": int(iters.max()),
-            "kernel_us": {"mpc_box": round(fused_ms * 1e3, 2), "condense": round(cond_ms * 1e3, 2),
-                          "solve_box": round(solve_ms * 1e3, 2)},
-            "split_vs_fused_max_abs": split_vs_fused,
-            "roofline": roofline,
-            "roofline_condense": roof_cond,
-            "roofline_solve_box": roof_solve,
+            "roofline": dom,
             "cpu_baseline": cpu,
         }
+        out.update(others)
+        out.update(extra)
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -106,7 +106,8 @@ int mpcqp_condense(int dtype, int batch, int nx, int nu, int N, int flags,
                    void* stream);
 
 /*
- * Batched box QP:  min 1/2 z'Hz + f'z   s.t.  lb <= z <= ub   (n <= 64).
+ * Batched box QP:  min 1/2 z'Hz + f'z   s.t.  lb <= z <= ub
+ * (n <= mpcqp_max_box_n(dtype); n > 64 runs on the mpcqp_solve_qp kernel).
  * H packed lower (stride 0 = shared), f/lb/ub per instance or shared
  * (lb/ub NULL = -inf/+inf).  One QP per wavefront: Goldfarb-Idnani dual
  * active set specialised to bounds, on H swept over the free set (one row per
@@ -160,6 +161,32 @@ int mpcqp_solve_poly(int dtype, int batch, int n, int m,
                      const void* lbz, const void* ubz,
                      void* z, void* y, int32_t* status, int max_iter, double tol,
                      void* workspace, int64_t workspace_bytes, void* stream);
+
+/*
+ * Batched QP with per-instance data and general rows:
+ *     min 1/2 z'Hz + f'z   s.t.  lb <= z <= ub,   hl <= G z <= hu
+ * (session_4/main.py:115-116 with the input box lbx/ubx, main.py:68-69, AND
+ * the state box lbg/ubg, main.py:58-61, after condensing: G = Gam,
+ * hl/hu = x_min/x_max - xbar -- BASELINE config 3; with m = 0 the large
+ * input-box QPs of config 5).  Every operand has its own per-instance stride
+ * (0 = shared): H packed lower n(n+1)/2, f n, G m*n row-major, hl/hu m,
+ * lb/ub n (NULL = unbounded).  One instance per workgroup: the augmented
+ * matrix [[H, G'], [G, 0]] lives in registers, every z is swept in (which
+ * yields -H^-1 and the dual G H^-1 G' without forming either separately),
+ * then a mixed primal/dual Goldfarb-Idnani active set handles bounds and
+ * rows together, including rows that depend on the active set.
+ * y (batch x m, optional): row multipliers, > 0 at hu, < 0 at hl.
+ * Limits: n + m <= mpcqp_max_qp_size(dtype).  mpcqp_solve_box uses the same
+ * kernel for n > 64.
+ */
+int mpcqp_max_qp_size(int dtype);
+int mpcqp_solve_qp(int dtype, int batch, int n, int m,
+                   const void* H, int64_t strideH, const void* f, int64_t stridef,
+                   const void* G, int64_t strideG, const void* hl, const void* hu,
+                   int64_t strideh, const void* lb, int64_t strideLb,
+                   const void* ub, int64_t strideUb,
+                   void* z, void* y, int32_t* status, int max_iter, double tol,
+                   void* stream);
 
 /*
  * Batched finite-horizon Riccati recursion, FHC.py:51-61:

@@ -274,6 +274,54 @@ def solve_poly(H, f, G=None, hl=None, hu=None, lbz=None, ubz=None, *, max_iter: 
     return z, y, status
 
 
+# ------------------------------------------ general QP, per-instance rows
+def solve_qp(H, f, G=None, hl=None, hu=None, lb=None, ub=None, *, max_iter: int = 0,
+             tol: float = 0.0, out: tuple | None = None):
+    """Batched  min 1/2 z'Hz + f'z  s.t.  lb <= z <= ub,  hl <= G z <= hu.
+
+    Every operand may be per instance (leading batch dim) or shared: H packed
+    lower (n(n+1)/2), G (m, n), hl/hu (m), lb/ub (n).  n + m <= 192.
+    One instance per workgroup (libmpcqp ``mpcqp_solve_qp``).
+    Returns (z, y, status); y (batch, m) are the row multipliers
+    (y > 0 at the upper bound, y < 0 at the lower bound).
+    """
+    dt, dev = f.dtype, f.device
+    f = _dev(f, dt, dev)
+    H = _dev(H, dt, dev)
+    n = int(f.shape[-1])
+    if H.shape[-1] != n * (n + 1) // 2:
+        raise ValueError(f"H must be packed lower with {n * (n + 1) // 2} entries, got {tuple(H.shape)}")
+    sH, bH = _inst(H, 1, "H")
+    sf, bf = _inst(f, 1, "f")
+    m = 0 if G is None else int(G.shape[-2])
+    G = _dev(G, dt, dev)
+    sG, bG = (0, None) if G is None else _inst(G, 2, "G")
+    hl = _dev(hl, dt, dev)
+    hu = _dev(hu, dt, dev)
+    if hl is not None and hu is not None and hl.shape != hu.shape:
+        raise ValueError("hl and hu must have the same shape")
+    sh, bh = 0, None
+    for h in (hl, hu):
+        if h is not None:
+            sh, bh = _inst(h, 1, "h")
+    lbt, slb = _bound(lb, n, dt, dev)
+    ubt, sub = _bound(ub, n, dt, dev)
+    batch = _batch_of((sH, bH), (sf, bf), (sG, bG), (sh, bh),
+                      (slb, lbt.shape[0] if lbt is not None and lbt.ndim == 2 else None),
+                      (sub, ubt.shape[0] if ubt is not None and ubt.ndim == 2 else None))
+    if out is None:
+        z = torch.empty((batch, n), dtype=dt, device=dev)
+        y = torch.empty((batch, m), dtype=dt, device=dev) if m else None
+        status = torch.empty((batch,), dtype=torch.int32, device=dev)
+    else:
+        z, y, status = out
+    rc = _lib().mpcqp_solve_qp(_code(dt), batch, n, m, _ptr(H), sH, _ptr(f), sf, _ptr(G), sG,
+                               _ptr(hl), _ptr(hu), sh, _ptr(lbt), slb, _ptr(ubt), sub, _ptr(z),
+                               _ptr(y), _ptr(status), int(max_iter), float(tol), _stream())
+    nat.check(rc, "mpcqp_solve_qp")
+    return z, y, status
+
+
 # ---------------------------------------------------------------- Riccati
 def riccati(A, B, Q, R, Pf, N: int):
     """Batched FHC.ricatti_recursion: returns P (b,N+1,nx,nx), K (b,N,nu,nx)."""

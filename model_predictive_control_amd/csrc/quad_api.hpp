@@ -48,5 +48,16 @@ inline bool use_wave_kernels() {
   const char* v = getenv("MPCQP_KERNEL");
   return v && v[0] == 'w';
 }
+// MPCQP_KERNEL=block forces the one-QP-per-workgroup kernel (solve_qp.hip).
+inline bool use_block_kernels() {
+  const char* v = getenv("MPCQP_KERNEL");
+  return v && v[0] == 'b';
+}
+
+// solve_qp.hip
+int solve_box_wg(int dtype, int batch, int n, const void* H, int64_t sH, const void* f,
+                 int64_t sf, const void* lb, int64_t sLb, const void* ub, int64_t sUb, void* z,
+                 int32_t* status, int max_iter, double tol, hipStream_t st);
+int max_qp_size_dtype(int dtype);
 
 }  // namespace mpcqp

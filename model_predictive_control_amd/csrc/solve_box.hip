@@ -144,10 +144,7 @@ static int solve_box_t(int batch, int n, const void* H, int64_t sH, const void* 
 
 }  // namespace mpcqp
 
-extern "C" int mpcqp_max_box_n(int dtype) {
-  (void)dtype;
-  return 64;
-}
+extern "C" int mpcqp_max_box_n(int dtype) { return mpcqp::max_qp_size_dtype(dtype); }
 
 extern "C" int mpcqp_solve_box(int dtype, int batch, int n, const void* H, int64_t strideH,
                                const void* f, int64_t stridef, const void* lb, int64_t strideLb,
@@ -156,12 +153,16 @@ extern "C" int mpcqp_solve_box(int dtype, int batch, int n, const void* H, int64
   using namespace mpcqp;
   MPCQP_CHECK_ARG(dtype == MPCQP_F64 || dtype == MPCQP_F32, "mpcqp_solve_box: bad dtype %d", dtype);
   MPCQP_CHECK_ARG(batch >= 0, "mpcqp_solve_box: batch < 0");
-  MPCQP_CHECK_ARG(n >= 1 && n <= 64, "mpcqp_solve_box: n=%d outside [1,64]", n);
+  MPCQP_CHECK_ARG(n >= 1 && n <= max_qp_size_dtype(dtype), "mpcqp_solve_box: n=%d outside [1,%d]",
+                  n, max_qp_size_dtype(dtype));
   MPCQP_CHECK_ARG(H && f && z && status, "mpcqp_solve_box: H, f, z, status are required");
   MPCQP_CHECK_ARG(strideH >= 0 && stridef >= 0 && strideLb >= 0 && strideUb >= 0,
                   "mpcqp_solve_box: negative stride");
   if (batch == 0) return MPCQP_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (n > 64 || use_block_kernels())
+    return solve_box_wg(dtype, batch, n, H, strideH, f, stridef, lb, strideLb, ub, strideUb, z,
+                        status, max_iter, tol, st);
   if (dtype == MPCQP_F64)
     return solve_box_t<double>(batch, n, H, strideH, f, stridef, lb, strideLb, ub, strideUb, z,
                                status, max_iter, tol, st);

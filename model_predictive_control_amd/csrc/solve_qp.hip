@@ -1,0 +1,223 @@
+// solve_qp.hip -- batched QPs with per-instance H and constraint rows, one
+// instance per workgroup (wg.hpp):
+//
+//   min 1/2 z'Hz + f'z   s.t.  lb <= z <= ub,   hl <= G z <= hu
+//
+// This is the per-step QP of session_4/main.py:115-116 with BOTH the input box
+// (lbx/ubx, main.py:68-69) and the state box (lbg/ubg, main.py:58-61) after
+// condensing: G = Gamma (N*nx x N*nu), hl/hu = x_min/x_max - xbar per instance
+// (BASELINE config 3), and the large input-box QPs of config 5 (n = 160,
+// m = 0).  mpcqp_solve_box routes n > 64 here.
+//
+// Per instance: stage K = [[H, G'], [G, 0]] into registers, sweep every z
+// index in (K -> [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']], i.e. the dual
+// matrix comes for free), then run the mixed primal/dual active set.
+#include "wg.hpp"
+
+namespace mpcqp {
+
+template <typename T>
+struct QpArgs {
+  int batch, n, m;
+  const T* H; int64_t sH;  // packed lower n x n
+  const T* f; int64_t sf;
+  const T* G; int64_t sG;  // m x n row-major
+  const T* hl; const T* hu; int64_t sh;
+  const T* lb; int64_t sLb;
+  const T* ub; int64_t sUb;
+  T* z; T* y; int32_t* status;
+  int max_iter;
+  T tol;
+};
+
+// Two waves per SIMD: a 512-thread workgroup fits once per CU, a 256-thread
+// one twice (VGPR budget 256).
+template <typename T, class S>
+__global__ __launch_bounds__(S::threads) __attribute__((amdgpu_waves_per_eu(2)))
+void qp_wg_kernel(QpArgs<T> a) {
+  using L = WLds<T, S>;
+  constexpr int BR = S::BR, BC = S::BC;
+  constexpr int NMAX = L::NMAX;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* sm = reinterpret_cast<T*>(smem_raw);
+  T* lo = sm + L::oLo;
+  T* hi = sm + L::oHi;
+  T* fs = sm + L::oF;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int n = a.n, m = a.m, nt = n + m;
+  const T inf = Lim<T>::inf();
+
+  int bad = 0, nonfin = 0;
+  for (int i = tid; i < NMAX; i += S::threads) {
+    T l = -inf, u = inf, fi = T(0);
+    if (i < n) {
+      if (a.lb) l = a.lb[(int64_t)b * a.sLb + i];
+      if (a.ub) u = a.ub[(int64_t)b * a.sUb + i];
+      fi = a.f[(int64_t)b * a.sf + i];
+      nonfin |= !finite(fi);
+    } else if (i < nt) {
+      if (a.hl) l = a.hl[(int64_t)b * a.sh + (i - n)];
+      if (a.hu) u = a.hu[(int64_t)b * a.sh + (i - n)];
+    }
+    bad |= !(l <= u) || l == inf || u == -inf;
+    lo[i] = l;
+    hi[i] = u;
+    fs[i] = fi;
+  }
+  WSym<T, S> M;
+  M.init(tid);
+  const T* Hb = a.H + (int64_t)b * a.sH;
+  const T* Gb = a.G ? a.G + (int64_t)b * a.sG : nullptr;
+#pragma unroll
+  for (int r = 0; r < BR; ++r)
+#pragma unroll
+    for (int c = 0; c < BC; ++c) {
+      const int i = M.bi * BR + r, j = M.bj * BC + c;
+      T v = T(0);
+      if (i < n && j < n) {
+        v = (j <= i) ? Hb[i * (i + 1) / 2 + j] : Hb[j * (j + 1) / 2 + i];
+      } else if (i < nt && j < n) {
+        v = Gb[(int64_t)(i - n) * n + j];
+      } else if (j < nt && i < n) {
+        v = Gb[(int64_t)(j - n) * n + i];
+      }
+      nonfin |= !finite(v);
+      M.m[r][c] = v;
+    }
+  const int flags = __syncthreads_or((bad ? 1 : 0) | (nonfin ? 2 : 0));
+  int code = MPCQP_STATUS_OPTIMAL;
+  int iters = 0;
+  T val[BR], lam[BR];
+#pragma unroll
+  for (int r = 0; r < BR; ++r) {
+    val[r] = __builtin_nan("");
+    lam[r] = __builtin_nan("");
+  }
+  if (flags & 2) {
+    code = MPCQP_STATUS_NONFINITE;
+  } else if (flags & 1) {
+    code = MPCQP_STATUS_INFEASIBLE;
+  } else {
+    // sweep every z in: M = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']]
+    for (int k = 0; k < n; ++k) {
+      T* cbuf = sm + ((k & 1) ? L::oCol1 : L::oCol0);
+      M.put_col(k, cbuf);
+      __syncthreads();
+      const T d = cbuf[k];
+      if (!(d > T(0))) {
+        code = MPCQP_STATUS_NOT_CONVEX;
+        break;
+      }
+      M.sweep_buf(k, T(1), d, cbuf);
+    }
+    if (code == MPCQP_STATUS_OPTIMAL) {
+      M.diag_abs(sm + L::oScale);
+      __syncthreads();
+      const T dep_tol = sizeof(T) == 8 ? T(1e-10) : T(2e-5);
+      code = gi_mixed<T, S>(M, sm, n, nt, a.max_iter, a.tol, dep_tol, val, lam, iters);
+    }
+  }
+  const bool ok = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
+  if (M.bj == 0) {
+#pragma unroll
+    for (int r = 0; r < BR; ++r) {
+      const int i = M.bi * BR + r;
+      if (i < n) a.z[(int64_t)b * n + i] = ok ? val[r] : __builtin_nan("");
+      if (a.y && i >= n && i < nt) a.y[(int64_t)b * m + (i - n)] = ok ? lam[r] : __builtin_nan("");
+    }
+  }
+  if (tid == 0) a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
+}
+
+template <typename T, class S>
+static int launch_qp_bs(const QpArgs<T>& a, hipStream_t st) {
+  const size_t bytes = (size_t)WLds<T, S>::total * sizeof(T);
+  hipLaunchKernelGGL((qp_wg_kernel<T, S>), dim3(a.batch), dim3(S::threads), bytes, st, a);
+  MPCQP_CHECK_LAUNCH("qp_wg_kernel");
+  return MPCQP_OK;
+}
+
+// Shapes: 256 threads (16 x 16 grid of 4 x 4 blocks) up to 64 indices, then
+// 512 threads (32 x 16 grid of BR x 2BR blocks).
+using Shape64 = WShape<16, 4, 16, 4>;
+using Shape128 = WShape<32, 4, 16, 8>;
+using Shape192 = WShape<32, 6, 16, 12>;
+
+template <typename T>
+int max_qp_size() {
+  return 192;
+}
+
+template <typename T>
+int launch_qp(const QpArgs<T>& a, hipStream_t st) {
+  const int nt = a.n + a.m;
+  if (nt <= 64) return launch_qp_bs<T, Shape64>(a, st);
+  if (nt <= 128) return launch_qp_bs<T, Shape128>(a, st);
+  if (nt <= 192) return launch_qp_bs<T, Shape192>(a, st);
+  set_error("qp_wg: n + m = %d exceeds %d", nt, max_qp_size<T>());
+  return MPCQP_ENOTSUP;
+}
+
+template <typename T>
+static int solve_qp_t(int batch, int n, int m, const void* H, int64_t sH, const void* f,
+                      int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
+                      int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
+                      void* z, void* y, int32_t* status, int max_iter, double tol,
+                      hipStream_t st) {
+  QpArgs<T> a;
+  a.batch = batch; a.n = n; a.m = m;
+  a.H = (const T*)H; a.sH = sH;
+  a.f = (const T*)f; a.sf = sf;
+  a.G = (const T*)G; a.sG = sG;
+  a.hl = (const T*)hl; a.hu = (const T*)hu; a.sh = sh;
+  a.lb = (const T*)lb; a.sLb = sLb;
+  a.ub = (const T*)ub; a.sUb = sUb;
+  a.z = (T*)z; a.y = (T*)y; a.status = status;
+  a.max_iter = max_iter > 0 ? max_iter : 3 * (n + m) + 30;
+  a.tol = tol > 0 ? (T)tol : (sizeof(T) == 8 ? (T)1e-12 : (T)1e-6);
+  return launch_qp<T>(a, st);
+}
+
+// used by mpcqp_solve_box for n > 64
+int solve_box_wg(int dtype, int batch, int n, const void* H, int64_t sH, const void* f,
+                 int64_t sf, const void* lb, int64_t sLb, const void* ub, int64_t sUb, void* z,
+                 int32_t* status, int max_iter, double tol, hipStream_t st) {
+  if (dtype == MPCQP_F64)
+    return solve_qp_t<double>(batch, n, 0, H, sH, f, sf, nullptr, 0, nullptr, nullptr, 0, lb,
+                              sLb, ub, sUb, z, nullptr, status, max_iter, tol, st);
+  return solve_qp_t<float>(batch, n, 0, H, sH, f, sf, nullptr, 0, nullptr, nullptr, 0, lb, sLb,
+                           ub, sUb, z, nullptr, status, max_iter, tol, st);
+}
+
+int max_qp_size_dtype(int dtype) {
+  return dtype == MPCQP_F64 ? max_qp_size<double>() : max_qp_size<float>();
+}
+
+}  // namespace mpcqp
+
+extern "C" int mpcqp_max_qp_size(int dtype) { return mpcqp::max_qp_size_dtype(dtype); }
+
+extern "C" int mpcqp_solve_qp(int dtype, int batch, int n, int m, const void* H, int64_t strideH,
+                              const void* f, int64_t stridef, const void* G, int64_t strideG,
+                              const void* hl, const void* hu, int64_t strideh, const void* lb,
+                              int64_t strideLb, const void* ub, int64_t strideUb, void* z,
+                              void* y, int32_t* status, int max_iter, double tol, void* stream) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64 || dtype == MPCQP_F32, "mpcqp_solve_qp: bad dtype %d", dtype);
+  MPCQP_CHECK_ARG(batch >= 0 && n >= 1 && m >= 0, "mpcqp_solve_qp: bad sizes");
+  MPCQP_CHECK_ARG(n + m <= max_qp_size_dtype(dtype), "mpcqp_solve_qp: n + m = %d exceeds %d",
+                  n + m, max_qp_size_dtype(dtype));
+  MPCQP_CHECK_ARG(H && f && z && status, "mpcqp_solve_qp: H, f, z, status are required");
+  MPCQP_CHECK_ARG(m == 0 || G, "mpcqp_solve_qp: G required when m > 0");
+  MPCQP_CHECK_ARG(strideH >= 0 && stridef >= 0 && strideG >= 0 && strideh >= 0 &&
+                      strideLb >= 0 && strideUb >= 0,
+                  "mpcqp_solve_qp: negative stride");
+  if (batch == 0) return MPCQP_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MPCQP_F64)
+    return solve_qp_t<double>(batch, n, m, H, strideH, f, stridef, G, strideG, hl, hu, strideh,
+                              lb, strideLb, ub, strideUb, z, y, status, max_iter, tol, st);
+  return solve_qp_t<float>(batch, n, m, H, strideH, f, stridef, G, strideG, hl, hu, strideh, lb,
+                           strideLb, ub, strideUb, z, y, status, max_iter, tol, st);
+}

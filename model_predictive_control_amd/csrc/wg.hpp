@@ -1,0 +1,445 @@
+// wg.hpp -- one QP per workgroup of GR*GC threads: a symmetric n x n matrix
+// (n <= GR*BR = GC*BC) held as a GR x GC grid of BR x BC register blocks, and the
+// mixed primal/dual Goldfarb-Idnani active set that runs on it.
+//
+// Thread t owns block (bi, bj) with bi = t % GR and bj = t / GR, so the GR
+// lanes of one (GR = 16) or two (GR = 32) DPP rows hold one block COLUMN.  Vectors
+// indexed by matrix row ("row-block layout", T v[BR] for rows bi*BR..+BR-1)
+// are replicated across bj, and every reduction over rows -- the arg-max of
+// the violation scan, the ratio test -- is a row_ror butterfly inside a DPP
+// row (plus one swizzle step for GR = 32).  Each of the 16 rows of the workgroup reduces identical data
+// in the same total order, so every lane ends with the same scalar and the
+// whole workgroup branches uniformly without a barrier.  Pivot columns travel
+// through a double-buffered LDS vector (one barrier per column).
+//
+// Method.  The QP
+//     min 1/2 z'Hz + f'z   s.t.  lz <= z <= uz,   lr <= C z <= ur
+// is embedded in the augmented symmetric matrix K = [[H, C'], [C, 0]] over
+// the index set {z_0..z_{n-1}, r_0..r_{m-1}}.  A swept set S holds the free
+// z and the ACTIVE rows; M = SWEEP_S(K).  With w_q = c_q on S and -x_q off S
+// (c = f on z, -bound on active rows; x = bound on fixed z, 0 = lambda on
+// inactive rows), s = M w gives every primal/dual quantity:
+//   free z: z = s;      fixed z: g = f - s;    active row: lambda = s;
+//   inactive row: C_r z = -s.
+// Adding constraint p (a violated bound of z_p or of row p) moves one scalar
+// parameter tau in slot p (g_p for a z, lambda_p for a row); every quantity
+// moves along column p of M.  A blocking multiplier is dropped by toggling
+// its index (partial step); when p reaches its bound, p is toggled (full
+// step).  Toggling = Goodnight sweep in (sigma = +1) or out (sigma = -1).
+// A row (or z) that depends on the active set has M_pp ~ 0: the step is then
+// a pure dual step that drops constraints until p becomes independent, or
+// proves the QP infeasible.  Box-only problems (m = 0) reduce exactly to the
+// box GI of gi_box_core.hpp.
+#pragma once
+#include "sym2d.hpp"
+
+namespace mpcqp {
+
+// (value, index[, payload]) reductions over the G lanes that hold one block
+// column (G = 16: one DPP row; G = 32: two DPP rows, joined by a swizzle).
+// NaN must be mapped to -inf / +inf by the caller (every lane must agree).
+template <int G, typename T>
+__device__ __forceinline__ void rowg_argmax(T& v, int& idx, T& pay) {
+#define MPCQP_STEP(CTRL)                                         \
+  {                                                              \
+    const T ov = dpp<CTRL>(v);                                   \
+    const int oi = dpp<CTRL>(idx);                               \
+    const T op = dpp<CTRL>(pay);                                 \
+    const bool take = (ov > v) || (ov == v && oi < idx);         \
+    v = take ? ov : v;                                           \
+    idx = take ? oi : idx;                                       \
+    pay = take ? op : pay;                                       \
+  }
+  MPCQP_STEP(0x121)
+  MPCQP_STEP(0x122)
+  MPCQP_STEP(0x124)
+  MPCQP_STEP(0x128)
+#undef MPCQP_STEP
+  if constexpr (G == 32) {
+    const T ov = __shfl_xor(v, 16, kWave);
+    const int oi = __shfl_xor(idx, 16, kWave);
+    const T op = __shfl_xor(pay, 16, kWave);
+    const bool take = (ov > v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+    pay = take ? op : pay;
+  }
+}
+
+template <int G, typename T>
+__device__ __forceinline__ void rowg_argmin(T& v, int& idx) {
+#define MPCQP_STEP(CTRL)                                         \
+  {                                                              \
+    const T ov = dpp<CTRL>(v);                                   \
+    const int oi = dpp<CTRL>(idx);                               \
+    const bool take = (ov < v) || (ov == v && oi < idx);         \
+    v = take ? ov : v;                                           \
+    idx = take ? oi : idx;                                       \
+  }
+  MPCQP_STEP(0x121)
+  MPCQP_STEP(0x122)
+  MPCQP_STEP(0x124)
+  MPCQP_STEP(0x128)
+#undef MPCQP_STEP
+  if constexpr (G == 32) {
+    const T ov = __shfl_xor(v, 16, kWave);
+    const int oi = __shfl_xor(idx, 16, kWave);
+    const bool take = (ov < v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+  }
+}
+
+// Grid shape: GR x GC threads, BR x BC blocks, GR*BR == GC*BC.
+template <int GR_, int BR_, int GC_, int BC_>
+struct WShape {
+  static constexpr int GR = GR_, BR = BR_, GC = GC_, BC = BC_;
+  static constexpr int NMAX = GR * BR;
+  static constexpr int threads = GR * GC;
+  static_assert(GR * BR == GC * BC, "square matrix");
+  static_assert(GR == 16 || GR == 32, "row reductions cover 16 or 32 lanes");
+};
+
+template <typename T, class S>
+struct WSym {
+  static constexpr int GR = S::GR, BR = S::BR, GC = S::GC, BC = S::BC;
+  static constexpr int NMAX = S::NMAX;
+  T m[BR][BC];
+  int bi, bj;
+
+  __device__ __forceinline__ void init(int tid) {
+    bi = tid % GR;
+    bj = tid / GR;
+  }
+
+  // Column kc (uniform) of this thread's block into buf[row].  A uniform
+  // compile-time switch; the asm marker keeps the cases from being merged
+  // back into one dynamically indexed access (which would live in scratch).
+  template <int C>
+  __device__ __forceinline__ void put_col_sel(int kc, T* buf) {
+    if constexpr (C < BC) {
+      if (kc == C) {
+#pragma unroll
+        for (int r = 0; r < BR; ++r) buf[bi * BR + r] = m[r][C];
+        asm volatile("; col %0" ::"n"(C));
+      } else {
+        put_col_sel<C + 1>(kc, buf);
+      }
+    }
+  }
+  // Publish column k into buf (caller barriers before reading).
+  __device__ __forceinline__ void put_col(int k, T* buf) {
+    const int kb = k / BC;
+    if (bj == kb) put_col_sel<0>(k - kb * BC, buf);
+  }
+  __device__ __forceinline__ void get_col(const T* buf, T (&colr)[BR], T (&colc)[BC]) const {
+#pragma unroll
+    for (int r = 0; r < BR; ++r) colr[r] = buf[bi * BR + r];
+#pragma unroll
+    for (int c = 0; c < BC; ++c) colc[c] = buf[bj * BC + c];
+  }
+
+  // Column kc := sigma*a (owners of column k), row kr := sigma*colc/d with
+  // -1/d on the diagonal (owners of row k).  Uniform compile-time switches
+  // with per-lane selects: no divergent branch writes matrix registers.
+  template <int C>
+  __device__ __forceinline__ void fix_col(int kc, bool own, T sigma, const T (&a)[BR]) {
+    if constexpr (C < BC) {
+      if (kc == C) {
+#pragma unroll
+        for (int r = 0; r < BR; ++r) m[r][C] = own ? sigma * a[r] : m[r][C];
+      } else {
+        fix_col<C + 1>(kc, own, sigma, a);
+      }
+    }
+  }
+  template <int R>
+  __device__ __forceinline__ void fix_row(int kr, int k, bool own, T sigma, T rd,
+                                          const T (&colc)[BC]) {
+    if constexpr (R < BR) {
+      if (kr == R) {
+#pragma unroll
+        for (int c = 0; c < BC; ++c) {
+          const T v = (bj * BC + c == k) ? -rd : sigma * colc[c] * rd;
+          m[R][c] = own ? v : m[R][c];
+        }
+      } else {
+        fix_row<R + 1>(kr, k, own, sigma, rd, colc);
+      }
+    }
+  }
+
+  // Goodnight sweep on pivot k with column k fetched (colr: rows bi*BR+r,
+  // colc: rows bj*BC+c of column k; d = M_kk):
+  //   M_ij -= M_ik M_kj / d;  row/col k := sigma M_.k / d;  M_kk := -1/d.
+  // The generic update runs everywhere; row and column k are then
+  // overwritten by the threads that own them (no cancellation).
+  __device__ __forceinline__ void sweep_col(int k, T sigma, T d, const T (&colr)[BR],
+                                            const T (&colc)[BC]) {
+    const T rd = fast_rcp(d);
+    T a[BR];
+#pragma unroll
+    for (int r = 0; r < BR; ++r) a[r] = colr[r] * rd;
+#pragma unroll
+    for (int r = 0; r < BR; ++r)
+#pragma unroll
+      for (int c = 0; c < BC; ++c) m[r][c] = fma(-a[r], colc[c], m[r][c]);
+    const int kbc = k / BC, kbr = k / BR;
+    fix_col<0>(k - kbc * BC, bj == kbc, sigma, a);
+    fix_row<0>(k - kbr * BR, k, bi == kbr, sigma, rd, colc);
+  }
+
+  // Same, reading column k from its LDS buffer (short live ranges).
+  __device__ __forceinline__ void sweep_buf(int k, T sigma, T d, const T* buf) {
+    T colr[BR], colc[BC];
+    get_col(buf, colr, colc);
+    sweep_col(k, sigma, d, colr, colc);
+  }
+
+  // out[r] = sum_j M[bi*BR+r][j] w[j]; w in row-block layout.  wbuf: NMAX,
+  // red: GC*NMAX.  Three barriers; every thread ends with its rows' sums.
+  __device__ __forceinline__ void matvec(const T (&w)[BR], T* wbuf, T* red, T (&out)[BR]) {
+    if (bj == 0) {
+#pragma unroll
+      for (int r = 0; r < BR; ++r) wbuf[bi * BR + r] = w[r];
+    }
+    __syncthreads();
+    T wc[BC];
+#pragma unroll
+    for (int c = 0; c < BC; ++c) wc[c] = wbuf[bj * BC + c];
+#pragma unroll
+    for (int r = 0; r < BR; ++r) {
+      T s = T(0);
+#pragma unroll
+      for (int c = 0; c < BC; ++c) s = fma(m[r][c], wc[c], s);
+      red[bj * NMAX + bi * BR + r] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < BR; ++r) {
+      T s = T(0);
+#pragma unroll 4
+      for (int g = 0; g < GC; ++g) s += red[g * NMAX + bi * BR + r];
+      out[r] = s;
+    }
+    __syncthreads();
+  }
+
+  // |M_ii| for every i into out[i] (diagonal owners write).
+  __device__ __forceinline__ void diag_abs(T* out) const {
+#pragma unroll
+    for (int r = 0; r < BR; ++r)
+#pragma unroll
+      for (int c = 0; c < BC; ++c)
+        if (bi * BR + r == bj * BC + c) out[bi * BR + r] = fabs(m[r][c]);
+  }
+};
+
+// LDS layout of the workgroup QP kernels (elements of T).
+template <typename T, class S>
+struct WLds {
+  static constexpr int NMAX = S::NMAX;
+  static constexpr int oCol0 = 0;
+  static constexpr int oCol1 = oCol0 + NMAX;
+  static constexpr int oW = oCol1 + NMAX;
+  static constexpr int oLo = oW + NMAX;
+  static constexpr int oHi = oLo + NMAX;
+  static constexpr int oF = oHi + NMAX;
+  static constexpr int oScale = oF + NMAX;
+  static constexpr int oRed = oScale + NMAX;
+  static constexpr int total = oRed + S::GC * NMAX;
+};
+
+// Mixed GI on M (entry: every z swept in, no row active).  nz = n, nt = n+m.
+// lo/hi/f/scale live in LDS (f used for z indices only).  On exit val holds
+// z (clamped to its box) / row values, lam the signed row multipliers
+// (lambda > 0 at the upper bound) and the multipliers of fixed z (g).
+template <typename T, class S>
+__device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, int max_iter,
+                                        T tol, T dep_tol, T (&val)[S::BR], T (&lam)[S::BR],
+                                        int& iters) {
+  constexpr int BS = S::BR;  // row-block length
+  using L = WLds<T, S>;
+  T* lo = sm + L::oLo;
+  T* hi = sm + L::oHi;
+  T* fs = sm + L::oF;
+  T* scale = sm + L::oScale;
+  int st[BS];
+  T mu[BS];
+#pragma unroll
+  for (int r = 0; r < BS; ++r) {
+    const int i = M.bi * BS + r;
+    st[r] = (i < nt) ? 0 : 3;
+    mu[r] = T(0);
+    val[r] = T(0);
+  }
+  iters = 0;
+  int code = MPCQP_STATUS_OPTIMAL;
+  int cb = 0;  // column buffer parity
+
+  // exact state from s = M w
+  auto refresh = [&]() {
+    T w[BS], s[BS];
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      const bool isz = i < nz;
+      const bool act = st[r] == 1 || st[r] == 2;
+      const T bnd = (st[r] == 1) ? lo[i] : hi[i];
+      const bool sw = isz ? (st[r] == 0) : act;
+      const T fi = isz ? fs[i] : T(0);
+      w[r] = (st[r] == 3) ? T(0) : (sw ? (isz ? fi : -bnd) : (isz ? -bnd : T(0)));
+    }
+    M.matvec(w, sm + L::oW, sm + L::oRed, s);
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      const bool isz = i < nz;
+      const bool act = st[r] == 1 || st[r] == 2;
+      const T bnd = (st[r] == 1) ? lo[i] : hi[i];
+      const T fi = isz ? fs[i] : T(0);
+      const T mval = isz ? fi - s[r] : s[r];
+      const T sside = ((st[r] == 1) ? T(1) : T(-1)) * (isz ? T(1) : T(-1));
+      val[r] = act ? bnd : (isz ? s[r] : -s[r]);
+      mu[r] = act ? sside * mval : T(0);
+    }
+  };
+
+  auto scan = [&](T& viol, int& p, T& valp) {
+    viol = -Lim<T>::inf();
+    p = 0;
+    valp = T(0);
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      const T li = lo[i], ui = hi[i];
+      const T vl = finite(li) ? (li - val[r]) / (T(1) + fabs(li)) : -Lim<T>::inf();
+      const T vu = finite(ui) ? (val[r] - ui) / (T(1) + fabs(ui)) : -Lim<T>::inf();
+      T v = (st[r] == 0) ? fmax(vl, vu) : -Lim<T>::inf();
+      v = (v == v) ? v : -Lim<T>::inf();
+      const bool take = v > viol;
+      viol = take ? v : viol;
+      p = take ? i : p;
+      valp = take ? val[r] : valp;
+    }
+    rowg_argmax<S::GR>(viol, p, valp);
+  };
+
+  refresh();
+  bool active = true;
+  for (int pass = 0; pass < 3 && active; ++pass) {
+    while (true) {
+      T viol, valp;
+      int p;
+      scan(viol, p, valp);
+      if (!(viol > tol)) break;
+      const T lop = lo[p], hip = hi[p];
+      const int side = (valp < lop) ? 1 : 2;
+      const T tgt = (side == 1) ? lop : hip;
+      const bool pz = p < nz;
+      const T epsp = pz ? T(-1) : T(1);
+      const T sidesign = ((side == 1) ? T(1) : T(-1)) * (pz ? T(1) : T(-1));
+      const T sgn = (tgt > valp) ? T(1) : T(-1);
+      const T scp = scale[p];
+      T tau = T(0);
+      bool added = false;
+      while (!added) {
+        if (++iters > max_iter) {
+          code = MPCQP_STATUS_MAXITER;
+          goto out;
+        }
+        T* cbuf = sm + (cb ? L::oCol1 : L::oCol0);
+        cb ^= 1;
+        M.put_col(p, cbuf);
+        __syncthreads();
+        const T* crb = cbuf + M.bi * BS;  // column p at this thread's rows
+        const T mpp = cbuf[p];
+        const bool dep = !(-mpp > dep_tol * scp);
+        const T dtds = dep ? sidesign : sgn * epsp * fast_rcp(mpp);
+        const T t2 = dep ? Lim<T>::inf() : fabs(tgt - valp);
+        T ti = Lim<T>::inf();
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+          const int i = M.bi * BS + r;
+          const bool act = st[r] == 1 || st[r] == 2;
+          const T dq = crb[r] * dtds;
+          const T dmu = act ? ((st[r] == 1) ? dq : -dq) : T(0);
+          T t = (act && dmu < T(0)) ? -mu[r] / dmu : Lim<T>::inf();
+          t = (t == t) ? t : Lim<T>::inf();
+          const bool take = t < ti;
+          ti = take ? t : ti;
+          k = take ? i : k;
+        }
+        rowg_argmin<S::GR>(ti, k);
+        if (!(ti < Lim<T>::inf()) && !(t2 < Lim<T>::inf())) {
+          code = MPCQP_STATUS_INFEASIBLE;
+          goto out;
+        }
+        const bool partial = ti < t2;
+        const T s_eff = partial ? ti : t2;
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+          const int i = M.bi * BS + r;
+          const bool act = st[r] == 1 || st[r] == 2;
+          const T dq = crb[r] * dtds;
+          const T dmu = act ? ((st[r] == 1) ? dq : -dq) : T(0);
+          const T dval = (st[r] == 0) ? ((i < nz) ? -dq : dq) : T(0);
+          val[r] = fma(s_eff, dval, val[r]);
+          mu[r] = fma(s_eff, dmu, mu[r]);
+        }
+        tau = fma(s_eff, dtds, tau);
+        // the index whose state toggles: k leaves the active set (partial) or
+        // p joins it (full); one sweep site keeps register pressure down
+        int idx = p;
+        T sigma = pz ? T(-1) : T(1);  // p inactive: swept if z, unswept if row
+        T d = mpp;
+        const T* sbuf = cbuf;
+        if (partial) {
+          if (!dep) valp = fma(sgn, s_eff, valp);
+          T* kbuf = sm + (cb ? L::oCol1 : L::oCol0);
+          cb ^= 1;
+          M.put_col(k, kbuf);
+          __syncthreads();
+          idx = k;
+          sigma = (k < nz) ? T(1) : T(-1);  // k active: unswept if z, swept if row
+          d = kbuf[k];
+          sbuf = kbuf;
+        }
+        if (partial ? !(d > T(0)) : !(d < T(0))) {
+          code = MPCQP_STATUS_NOT_CONVEX;
+          goto out;
+        }
+        M.sweep_buf(idx, sigma, d, sbuf);
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+          const bool me = M.bi * BS + r == idx;
+          st[r] = me ? (partial ? 0 : side) : st[r];
+          mu[r] = me ? (partial ? T(0) : sidesign * tau) : mu[r];
+          val[r] = (me && !partial) ? tgt : val[r];
+        }
+        added = !partial;
+      }
+    }
+    refresh();
+    {
+      T viol, valp;
+      int p;
+      scan(viol, p, valp);
+      active = viol > tol;
+    }
+  }
+  if (active) code = MPCQP_STATUS_MAXITER;
+out:
+#pragma unroll
+  for (int r = 0; r < BS; ++r) {
+    const int i = M.bi * BS + r;
+    const bool isz = i < nz;
+    const T sside = ((st[r] == 1) ? T(1) : T(-1)) * (isz ? T(1) : T(-1));
+    lam[r] = (st[r] == 1 || st[r] == 2) ? sside * mu[r] : T(0);
+    if (isz && i < nt) val[r] = fmin(fmax(val[r], lo[i]), hi[i]);
+  }
+  return code;
+}
+
+}  // namespace mpcqp

@@ -32,14 +32,24 @@ def test_every_header_symbol_exported(lib):
 
 def test_abi_version(lib):
     assert lib.mpcqp_abi_version() == nat.ABI_VERSION == 1
-    assert lib.mpcqp_max_box_n(nat.F64) == 64
+    assert lib.mpcqp_max_box_n(nat.F64) == lib.mpcqp_max_qp_size(nat.F64) == 192
+    assert lib.mpcqp_max_qp_size(nat.F32) == 192
+
+
+def test_solve_qp_args_rejected_without_gpu(lib):
+    rc = lib.mpcqp_solve_qp(nat.F32, 1, 150, 60, None, 0, None, 0, None, 0, None, None, 0,
+                            None, 0, None, 0, None, None, None, 0, 0.0, None)
+    assert rc == -1 and b"exceeds" in lib.mpcqp_last_error()
+    rc = lib.mpcqp_solve_qp(nat.F32, 1, 10, 4, None, 0, None, 0, None, 0, None, None, 0,
+                            None, 0, None, 0, None, None, None, 0, 0.0, None)
+    assert rc == -1 and b"required" in lib.mpcqp_last_error()
 
 
 def test_invalid_args_rejected_without_gpu(lib):
     rc = lib.mpcqp_solve_box(7, 1, 4, None, 0, None, 0, None, 0, None, 0, None, None, 0, 0.0, None)
     assert rc == -1 and b"dtype" in lib.mpcqp_last_error()
-    rc = lib.mpcqp_solve_box(nat.F64, 1, 65, 1, 0, 1, 0, None, 0, None, 0, 1, 1, 0, 0.0, None)
-    assert rc == -1 and b"n=65" in lib.mpcqp_last_error()
+    rc = lib.mpcqp_solve_box(nat.F64, 1, 193, 1, 0, 1, 0, None, 0, None, 0, 1, 1, 0, 0.0, None)
+    assert rc == -1 and b"n=193" in lib.mpcqp_last_error()
     rc = lib.mpcqp_condense(nat.F64, 4, 17, 1, 10, 0, 1, 0, 1, 0, 1, 0, 1, 0, 1, 0, None, 0,
                             None, 0, 1, None, None, None, None, None, None)
     assert rc == -1 and b"nx=17" in lib.mpcqp_last_error()
