@@ -27,6 +27,7 @@ struct QpArgs {
   const T* ub; int64_t sUb;
   T* z; T* y; int32_t* status;
   int max_iter;
+  int refine;
   T tol;
 };
 
@@ -84,6 +85,7 @@ void qp_wg_kernel(QpArgs<T> a) {
       }
       nonfin |= !finite(v);
       M.m[r][c] = v;
+      if (c == BC - 1) asm volatile("" ::: "memory");  // one row of loads in flight
     }
   const int flags = __syncthreads_or((bad ? 1 : 0) | (nonfin ? 2 : 0));
   int code = MPCQP_STATUS_OPTIMAL;
@@ -115,7 +117,18 @@ void qp_wg_kernel(QpArgs<T> a) {
       M.diag_abs(sm + L::oScale);
       __syncthreads();
       const T dep_tol = sizeof(T) == 8 ? T(1e-10) : T(2e-5);
-      code = gi_mixed<T, S>(M, sm, n, nt, a.max_iter, a.tol, dep_tol, val, lam, iters);
+      // original K_ij = [[H, G'], [G, 0]] for the refinement residual
+      auto kel = [&](int i, int j) -> T {
+        // opaque indices: stop the compiler from keeping the staging loads'
+        // addresses alive across the whole solve (CSE with the K load above)
+        asm volatile("" : "+v"(i), "+v"(j));
+        if (i < n && j < n) return (j <= i) ? Hb[i * (i + 1) / 2 + j] : Hb[j * (j + 1) / 2 + i];
+        if (i < nt && j < n) return Gb[(int64_t)(i - n) * n + j];
+        if (j < nt && i < n) return Gb[(int64_t)(j - n) * n + i];
+        return T(0);
+      };
+      code = gi_mixed<T, S>(M, sm, n, nt, a.max_iter, a.tol, dep_tol, val, lam, iters, kel,
+                            a.refine);
     }
   }
   const bool ok = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
@@ -175,6 +188,8 @@ static int solve_qp_t(int batch, int n, int m, const void* H, int64_t sH, const 
   a.ub = (const T*)ub; a.sUb = sUb;
   a.z = (T*)z; a.y = (T*)y; a.status = status;
   a.max_iter = max_iter > 0 ? max_iter : 3 * (n + m) + 30;
+  // fp32: two refinement steps against the original data; fp64: one
+  a.refine = sizeof(T) == 4 ? 2 : 1;
   a.tol = tol > 0 ? (T)tol : (sizeof(T) == 8 ? (T)1e-12 : (T)1e-6);
   return launch_qp<T>(a, st);
 }

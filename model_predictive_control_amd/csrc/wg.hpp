@@ -225,6 +225,39 @@ struct WSym {
     __syncthreads();
   }
 
+  // out[r] = sum_j K[bi*BR+r][j] x[j] in fp64 for an ORIGINAL matrix K given
+  // element-wise by kel(i, j) (re-read from global memory), x in row-block
+  // layout.  Used for the iterative-refinement residual.
+  template <class KEl>
+  __device__ __forceinline__ void matvec_orig(KEl&& kel, const T (&x)[BR], T* wbuf, double* redd,
+                                              double (&out)[BR]) {
+    if (bj == 0) {
+#pragma unroll
+      for (int r = 0; r < BR; ++r) wbuf[bi * BR + r] = x[r];
+    }
+    __syncthreads();
+    T xc[BC];
+#pragma unroll
+    for (int c = 0; c < BC; ++c) xc[c] = wbuf[bj * BC + c];
+#pragma unroll
+    for (int r = 0; r < BR; ++r) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < BC; ++c) s = fma((double)kel(bi * BR + r, bj * BC + c), (double)xc[c], s);
+      redd[bj * NMAX + bi * BR + r] = s;
+      asm volatile("" ::: "memory");  // one row of loads in flight (register pressure)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < BR; ++r) {
+      double s = 0.0;
+#pragma unroll 4
+      for (int g = 0; g < GC; ++g) s += redd[g * NMAX + bi * BR + r];
+      out[r] = s;
+    }
+    __syncthreads();
+  }
+
   // |M_ii| for every i into out[i] (diagonal owners write).
   __device__ __forceinline__ void diag_abs(T* out) const {
 #pragma unroll
@@ -246,18 +279,23 @@ struct WLds {
   static constexpr int oHi = oLo + NMAX;
   static constexpr int oF = oHi + NMAX;
   static constexpr int oScale = oF + NMAX;
-  static constexpr int oRed = oScale + NMAX;
-  static constexpr int total = oRed + S::GC * NMAX;
+  static constexpr int oRed = oScale + NMAX;  // GC*NMAX doubles (8-byte aligned)
+  static constexpr int total = oRed + S::GC * NMAX * (int)(sizeof(double) / sizeof(T));
 };
 
 // Mixed GI on M (entry: every z swept in, no row active).  nz = n, nt = n+m.
 // lo/hi/f/scale live in LDS (f used for z indices only).  On exit val holds
 // z (clamped to its box) / row values, lam the signed row multipliers
 // (lambda > 0 at the upper bound) and the multipliers of fixed z (g).
-template <typename T, class S>
+// After convergence, `refine` steps of iterative refinement on the final
+// active set S: e = (K x + c)_S from the ORIGINAL K (kel, fp64 accumulation),
+// x_S -= K_SS^-1 e = x_S + M_SS e.  The swept matrix carries ~cond(H)*eps
+// relative error (fp32: up to 1e-3); the residual from the original data
+// brings z back to the accuracy of the data itself.
+template <typename T, class S, class KEl>
 __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, int max_iter,
                                         T tol, T dep_tol, T (&val)[S::BR], T (&lam)[S::BR],
-                                        int& iters) {
+                                        int& iters, KEl&& kel, int refine) {
   constexpr int BS = S::BR;  // row-block length
   using L = WLds<T, S>;
   T* lo = sm + L::oLo;
@@ -430,6 +468,42 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
     }
   }
   if (active) code = MPCQP_STATUS_MAXITER;
+  for (int it = 0; it < refine; ++it) {
+    T x[BS];
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      const bool isz = i < nz;
+      const bool act = st[r] == 1 || st[r] == 2;
+      const T sside = ((st[r] == 1) ? T(1) : T(-1)) * (isz ? T(1) : T(-1));
+      x[r] = (st[r] == 3) ? T(0) : (isz ? val[r] : (act ? sside * mu[r] : T(0)));
+    }
+    double y[BS];
+    M.matvec_orig(kel, x, sm + L::oW, reinterpret_cast<double*>(sm + L::oRed), y);
+    T w[BS];
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      const bool isz = i < nz;
+      const bool act = st[r] == 1 || st[r] == 2;
+      const double bnd = (st[r] == 1) ? (double)lo[i] : (double)hi[i];
+      const bool inS = isz ? (st[r] == 0) : act;
+      const double e = isz ? y[r] + (double)fs[i] : y[r] - bnd;
+      w[r] = inS ? (T)e : T(0);
+    }
+    T sv[BS];
+    M.matvec(w, sm + L::oW, sm + L::oRed, sv);
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      const bool isz = i < nz;
+      const bool act = st[r] == 1 || st[r] == 2;
+      const T sside = ((st[r] == 1) ? T(1) : T(-1)) * (isz ? T(1) : T(-1));
+      // free z: z += s;  active row: lambda += s  (mu = sside * lambda)
+      val[r] = (isz && st[r] == 0) ? val[r] + sv[r] : val[r];
+      mu[r] = (!isz && act) ? mu[r] + sside * sv[r] : mu[r];
+    }
+  }
 out:
 #pragma unroll
   for (int r = 0; r < BS; ++r) {
