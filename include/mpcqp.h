@@ -163,6 +163,32 @@ int mpcqp_solve_poly(int dtype, int batch, int n, int m,
                      void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
+ * The same polytope QP split into a shared setup and a per-batch solve, for
+ * the receding-horizon loop where H, G (and the condensed x0 -> gradient map
+ * F, n x nx) stay fixed and only x0 changes (BASELINE config 4):
+ *   mpcqp_poly_setup: Hinv, Ut = C Hinv, M = C Hinv C', Kt = (-Hinv F)',
+ *                     L = -Ut F  into the workspace (once);
+ *   mpcqp_poly_solve: gradient f = F x0 + f1 per instance (x0 and/or f1,
+ *                     either may be NULL), rows hl/hu per instance or shared;
+ *                     one wavefront per instance computes s0 = L x0 - Ut f1,
+ *                     runs the dual range active set and writes
+ *                     z = Kt' x0 - Hinv f1 - Ut' y.
+ * nbox = 1 appends the box rows (lbz/ubz given to poly_solve) to C = [G; I].
+ * Limits: m_total <= 64, nx <= 16.  The workspace (mpcqp_poly_workspace
+ * bytes) is read-only during poly_solve, so concurrent solves may share it.
+ */
+int64_t mpcqp_poly_workspace(int dtype, int n, int m, int nbox, int nx);
+int mpcqp_poly_setup(int dtype, int n, int m, int nbox, int nx, const void* H,
+                     const void* G, const void* F, void* workspace,
+                     int64_t workspace_bytes, void* stream);
+int mpcqp_poly_solve(int dtype, int batch, int n, int m, int nbox, int nx,
+                     const void* workspace, const void* x0, int64_t strideX0,
+                     const void* f, int64_t stridef, const void* hl, const void* hu,
+                     int64_t strideh, const void* lbz, const void* ubz,
+                     void* z, void* y, int32_t* status, int max_iter, double tol,
+                     void* stream);
+
+/*
  * Batched QP with per-instance data and general rows:
  *     min 1/2 z'Hz + f'z   s.t.  lb <= z <= ub,   hl <= G z <= hu
  * (session_4/main.py:115-116 with the input box lbx/ubx, main.py:68-69, AND

@@ -46,6 +46,10 @@ SIGNATURES = {
     "mpcqp_solve_poly_workspace": (_i64, [_i, _i, _i, _i, _i]),
     "mpcqp_solve_poly": (_i, [_i, _i, _i, _i, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp,
                               _vp, _vp, _vp, _i, _d, _vp, _i64, _vp]),
+    "mpcqp_poly_workspace": (_i64, [_i, _i, _i, _i, _i]),
+    "mpcqp_poly_setup": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "mpcqp_poly_solve": (_i, [_i, _i, _i, _i, _i, _i, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64,
+                              _vp, _vp, _vp, _vp, _vp, _i, _d, _vp]),
     "mpcqp_max_qp_size": (_i, [_i]),
     "mpcqp_solve_qp": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64,
                             _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i, _d, _vp]),

@@ -274,6 +274,65 @@ def solve_poly(H, f, G=None, hl=None, hu=None, lbz=None, ubz=None, *, max_iter: 
     return z, y, status
 
 
+class PolyQP:
+    """Shared-structure polytope QP for the receding-horizon loop
+    (include/mpcqp.h ``mpcqp_poly_setup`` / ``mpcqp_poly_solve``):
+
+        min 1/2 z'Hz + (F x0 + f)'z   s.t.  hl <= G z <= hu,  lbz <= z <= ubz
+
+    H (packed, n(n+1)/2), G (m, n) and F (n, nx) are fixed at construction
+    (the factors are formed once on device); ``solve`` takes a batch of x0
+    and/or extra gradients f and per-instance or shared row bounds.
+    """
+
+    def __init__(self, H, G=None, F=None, lbz=None, ubz=None, *, dtype=None, device=None):
+        dt = dtype or H.dtype
+        dev = device or H.device
+        self.dtype, self.device = dt, dev
+        self.H = _dev(H, dt, dev)
+        self.n = n = isqrt_packed(int(self.H.shape[-1]))
+        self.G = _dev(G, dt, dev)
+        self.m = 0 if G is None else int(self.G.shape[0])
+        self.F = _dev(F, dt, dev)
+        self.nx = 0 if F is None else int(self.F.shape[-1])
+        self.lbz, _ = _bound(lbz, n, dt, dev)
+        self.ubz, _ = _bound(ubz, n, dt, dev)
+        self.nbox = 1 if (self.lbz is not None or self.ubz is not None) else 0
+        self.mt = self.m + (n if self.nbox else 0)
+        lib = _lib()
+        wsb = int(lib.mpcqp_poly_workspace(_code(dt), n, self.m, self.nbox, self.nx))
+        self.ws = torch.empty((wsb,), dtype=torch.uint8, device=dev)
+        rc = lib.mpcqp_poly_setup(_code(dt), n, self.m, self.nbox, self.nx, _ptr(self.H),
+                                  _ptr(self.G), _ptr(self.F), _ptr(self.ws), wsb, _stream())
+        nat.check(rc, "mpcqp_poly_setup")
+
+    def solve(self, x0=None, f=None, hl=None, hu=None, *, max_iter: int = 0, tol: float = 0.0,
+              out: tuple | None = None):
+        """Returns (z (b, n), y (b, m_total), status (b,))."""
+        dt, dev, n = self.dtype, self.device, self.n
+        x0, f = _dev(x0, dt, dev), _dev(f, dt, dev)
+        hl, hu = _dev(hl, dt, dev), _dev(hu, dt, dev)
+        sX, bX = _inst(x0, 1, "x0")
+        sf, bf = _inst(f, 1, "f")
+        sh, bh = 0, None
+        for h in (hl, hu):
+            if h is not None:
+                sh, bh = _inst(h, 1, "h")
+        batch = _batch_of((sX, bX), (sf, bf), (sh, bh))
+        if out is None:
+            z = torch.empty((batch, n), dtype=dt, device=dev)
+            y = torch.empty((batch, self.mt), dtype=dt, device=dev)
+            status = torch.empty((batch,), dtype=torch.int32, device=dev)
+        else:
+            z, y, status = out
+        rc = _lib().mpcqp_poly_solve(_code(dt), batch, n, self.m, self.nbox, self.nx,
+                                     _ptr(self.ws), _ptr(x0), sX, _ptr(f), sf, _ptr(hl), _ptr(hu),
+                                     sh, _ptr(self.lbz), _ptr(self.ubz), _ptr(z), _ptr(y),
+                                     _ptr(status), int(max_iter), float(tol), _stream())
+        nat.check(rc, "mpcqp_poly_solve")
+        return z, y, status
+
+
 # ------------------------------------------ general QP, per-instance rows
 def solve_qp(H, f, G=None, hl=None, hu=None, lb=None, ub=None, *, max_iter: int = 0,
              tol: float = 0.0, out: tuple | None = None):

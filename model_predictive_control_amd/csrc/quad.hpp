@@ -127,6 +127,17 @@ struct QSym {
     return d;
   }
 
+  // Column k read back from the group's tile left by the last column(k)
+  // call (no publish, no barrier); valid while nothing rewrote the tile.
+  __device__ __forceinline__ T cached_column(int k, const T* gb, T (&colr)[BS], T (&colc)[BS]) const {
+    const int kb = k / BS, kc = k - kb * BS;
+#pragma unroll
+    for (int r = 0; r < BS; ++r) colr[r] = gb[(bi * BS + r) * BS + kc];
+#pragma unroll
+    for (int c = 0; c < BS; ++c) colc[c] = gb[(bj * BS + c) * BS + kc];
+    return gb[k * BS + kc];
+  }
+
   // Goodnight sweep (sigma = +1) / reverse sweep (sigma = -1) on pivot k with
   // its column already fetched:  M_ij - M_ik M_kj / d  off row/column k,
   // sigma M_kj / d on row k, sigma M_ik / d on column k, -1/d at (k, k).
@@ -320,8 +331,11 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
       // the index whose state changes: k joins F (partial) or p leaves it (full)
       const int idx = partial ? k : p;
       const T sigma = partial ? T(1) : T(-1);
+      // full steps sweep on p, whose column is still in the tile: publish
+      // again only when some group of the wave drops a bound
       T kr[BS], kcol[BS];
-      const T d = M.column(idx, gb, kr, kcol);
+      const T d = __any(stepping && partial) ? M.column(idx, gb, kr, kcol)
+                                             : M.cached_column(idx, gb, kr, kcol);
       const bool bad = stepping && (partial ? !(d > T(0)) : !(d < T(0)));
       if (stepping && !bad) {
         M.sweep_col(idx, sigma, d, kr, kcol);

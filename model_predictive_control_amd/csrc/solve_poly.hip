@@ -8,14 +8,18 @@
 // box is the row block Gam with bounds shifted by the free response), and the
 // BASELINE config-4 polytope (40 random rows over N*nu = 200 inputs).
 //
-// Shared phase (once per call, H and G shared by the batch):
+// Shared phase (mpcqp_poly_setup, once per (H, G, F); H and G shared by the
+// batch, F = the condensed x0 -> gradient map, optional):
 //   Hinv = H^{-1}   (single-workgroup Gauss-Jordan on device)
 //   Ut   = C Hinv   (mt x n),  M = C Hinv C'  (mt x mt, packed lower)
-// Per instance:
-//   s0 = -Ut f,  z0 = -Hinv f                     (gemv)
+//   Kt   = (-Hinv F)'  (nx x n),  L = -Ut F  (mt x nx)
+// Per instance, one wavefront (mpcqp_poly_solve), gradient f = F x0 + f1:
+//   prologue  s0 = L x0 - Ut f1                     (unconstrained row values)
 //   dual range active set on M  -> y (y_r > 0: row r at its upper bound,
 //                                     y_r < 0: at its lower bound)
-//   z  = z0 - Ut' y                               (gemv, transposed)
+//   epilogue  z  = Kt' x0 - Hinv f1 - Ut' y
+// With x0 given, the per-instance work is O(mt*(nx + n) + n*nx) instead of
+// the O(n^2) of forming f and -Hinv f (BASELINE config 4: n = 200, mt = 40).
 //
 // Dual range active set (Goldfarb-Idnani written in the row space): the
 // wavefront keeps W = SWEEP_A(M), M swept on the active rows, as an 8x8
@@ -32,9 +36,18 @@ template <typename T>
 struct DualArgs {
   int batch, mt, m1;           // rows; the first m1 use (l1,u1) with stride s1
   const T* M; int64_t sM;      // packed lower mt x mt
-  const T* s0; int64_t sS0;
   const T* l1; const T* u1; int64_t s1;
   const T* l2; const T* u2;    // rows m1..mt-1, shared
+  // prologue / epilogue operands (shared factors from the setup phase)
+  int n, nx;
+  const T* Ut;                 // mt x n
+  const T* Hinv;               // n x n   (used when f1 is given)
+  const T* Kt;                 // nx x n  (used when x0 is given)
+  const T* L;                  // mt x nx (used when x0 is given)
+  const T* x0; int64_t sX0;
+  const T* f1; int64_t sF1;
+  const int32_t* flag;         // set by the shared inverse when H is not PD
+  T* z;
   T* y;
   int32_t* status;
   int max_iter;
@@ -52,12 +65,29 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
   T* uis = lis + NMAX;
   T* mds = uis + NMAX;
   T* ss = mds + NMAX;
-  T* Ps = ss + NMAX;
+  T* s0s = ss + NMAX;          // NMAX: unconstrained row values
+  T* xs = s0s + NMAX;          // 16: x0
+  T* Ps = xs + 16;
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = a.mt;
   const int P = n * (n + 1) / 2;
+  const int nz = a.n, nx = a.nx;
+  const T* x0 = a.x0 ? a.x0 + (int64_t)b * a.sX0 : nullptr;
+  const T* f1 = a.f1 ? a.f1 + (int64_t)b * a.sF1 : nullptr;
   stage_packed<T, NMAX*(NMAX + 1) / 2>(a.M + (int64_t)b * a.sM, Ps, P, lane);
+  if (x0 && lane < nx) xs[lane] = x0[lane];
+  __syncthreads();
+  // prologue: s0 = L x0 - Ut f1 (one row per lane)
+  if (lane < n) {
+    T acc = T(0);
+    if (x0)
+      for (int k = 0; k < nx; ++k) acc = fma(a.L[lane * nx + k], xs[k], acc);
+    if (f1)
+      for (int j = 0; j < nz; ++j) acc = fma(-a.Ut[(int64_t)lane * nz + j], f1[j], acc);
+    s0s[lane] = acc;
+  }
+  __syncthreads();
 
   Sym2D<T, BS> W;
   W.init(lane);
@@ -68,7 +98,7 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
   for (int r = 0; r < BS; ++r) {
     const int i = W.bi * BS + r;
     const bool v = i < n;
-    s0[r] = v ? a.s0[(int64_t)b * a.sS0 + i] : T(0);
+    s0[r] = v ? s0s[i] : T(0);
     li[r] = -Lim<T>::inf();
     ui[r] = Lim<T>::inf();
     if (v) {
@@ -98,6 +128,10 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
   const T tol = a.tol;
   const T dep_tol = sizeof(T) == 8 ? T(1e-10) : T(1e-5);
   const int max_iter = a.max_iter;
+  if (*a.flag) {
+    code = MPCQP_STATUS_NOT_CONVEX;
+    goto done;
+  }
   if (__any(nonfinite)) {
     code = MPCQP_STATUS_NONFINITE;
     goto done;
@@ -212,7 +246,8 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
     }
   }
 done:
-  if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
+  const bool okc = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
+  if (!okc) {
 #pragma unroll
     for (int r = 0; r < BS; ++r) yi[r] = __builtin_nan("");
   }
@@ -222,6 +257,18 @@ done:
       const int i = W.bi * BS + r;
       if (i < n) a.y[(int64_t)b * n + i] = yi[r];
     }
+  }
+  // epilogue: z = Kt' x0 - Hinv f1 - Ut' y   (lanes over z, coalesced rows)
+  publish<T, BS>(yi, ss, W.bi, W.bj);
+  __syncthreads();
+  for (int j = lane; j < nz; j += kWave) {
+    T acc = T(0);
+    if (x0)
+      for (int k = 0; k < nx; ++k) acc = fma(a.Kt[(int64_t)k * nz + j], xs[k], acc);
+    if (f1)
+      for (int i = 0; i < nz; ++i) acc = fma(-a.Hinv[(int64_t)i * nz + j], f1[i], acc);
+    for (int r = 0; r < n; ++r) acc = fma(-a.Ut[(int64_t)r * nz + j], ss[r], acc);
+    a.z[(int64_t)b * nz + j] = okc ? acc : __builtin_nan("");
   }
   if (lane == 0) a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
 }
@@ -324,39 +371,66 @@ __global__ __launch_bounds__(64) void gemv_t_kernel(int rows, int cols, T alpha,
   }
 }
 
+// Kt[k][j] = -(Hinv F)[j][k]   (nx x n)
+template <typename T>
+__global__ void form_kt_kernel(const T* F, int n, int nx, const T* Hinv, T* Kt) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nx * n) return;
+  const int k = e / n, j = e % n;
+  T acc = T(0);
+  for (int i = 0; i < n; ++i) acc = fma(Hinv[(int64_t)j * n + i], F[(int64_t)i * nx + k], acc);
+  Kt[e] = -acc;
+}
+
+// L[r][k] = sum_j C[r][j] Kt[k][j]  (= -C Hinv F = -Ut F, mt x nx)
+template <typename T>
+__global__ void form_l_kernel(const T* G, int m, int n, int mt, int nx, const T* Kt, T* L) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= mt * nx) return;
+  const int r = e / nx, k = e % nx;
+  T acc = T(0);
+  if (r < m) {
+    for (int j = 0; j < n; ++j) acc = fma(G[(int64_t)r * n + j], Kt[(int64_t)k * n + j], acc);
+  } else {
+    acc = Kt[(int64_t)k * n + (r - m)];
+  }
+  L[e] = acc;
+}
+
 static inline int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
+// Shared factors; independent of the batch size.
 struct PolyWs {
-  int64_t oW, oHinv, oUt, oM, oS0, oFlag, total;
+  int64_t oW, oHinv, oUt, oM, oKt, oL, oFlag, total;
 };
 
-static PolyWs poly_ws(size_t es, int batch, int n, int mt) {
+static PolyWs poly_ws(size_t es, int n, int mt, int nx) {
   PolyWs w;
   w.oW = 0;
   w.oHinv = align256(w.oW + (int64_t)n * n * es);
   w.oUt = align256(w.oHinv + (int64_t)n * n * es);
   w.oM = align256(w.oUt + (int64_t)mt * n * es);
-  w.oS0 = align256(w.oM + (int64_t)mt * (mt + 1) / 2 * es);
-  w.oFlag = align256(w.oS0 + (int64_t)batch * mt * es);
+  w.oKt = align256(w.oM + (int64_t)mt * (mt + 1) / 2 * es);
+  w.oL = align256(w.oKt + (int64_t)nx * n * es);
+  w.oFlag = align256(w.oL + (int64_t)mt * nx * es);
   w.total = align256(w.oFlag + 16);
   return w;
 }
 
 template <typename T, int BS>
 static void launch_dual(const DualArgs<T>& a, hipStream_t st) {
-  const size_t bytes = (size_t)(Sym2D<T, BS>::BUF + 4 * 8 * BS + a.mt * (a.mt + 1) / 2) * sizeof(T);
+  const size_t bytes =
+      (size_t)(Sym2D<T, BS>::BUF + 6 * 8 * BS + 16 + a.mt * (a.mt + 1) / 2) * sizeof(T);
   hipLaunchKernelGGL((dual_range_kernel<T, BS>), dim3(a.batch), dim3(kWave), bytes, st, a);
 }
 
 template <typename T>
-static int solve_poly_t(int batch, int n, int m, const void* H, const void* f, int64_t sf,
-                        const void* G, const void* hl, const void* hu, int64_t sh,
-                        const void* lbz, const void* ubz, void* z, void* y, int32_t* status,
-                        int max_iter, double tol, void* ws, int64_t wsb, hipStream_t st) {
-  const int mt = m + ((lbz || ubz) ? n : 0);
-  const PolyWs L = poly_ws(sizeof(T), batch, n, mt);
+static int poly_setup_t(int n, int m, int nbox, int nx, const void* H, const void* G,
+                        const void* F, void* ws, int64_t wsb, hipStream_t st) {
+  const int mt = m + (nbox ? n : 0);
+  const PolyWs L = poly_ws(sizeof(T), n, mt, nx);
   if (wsb < L.total) {
-    set_error("mpcqp_solve_poly: workspace %lld B < required %lld B", (long long)wsb,
+    set_error("mpcqp_poly_setup: workspace %lld B < required %lld B", (long long)wsb,
               (long long)L.total);
     return MPCQP_EINVAL;
   }
@@ -365,13 +439,12 @@ static int solve_poly_t(int batch, int n, int m, const void* H, const void* f, i
   T* Hinv = (T*)(base + L.oHinv);
   T* Ut = (T*)(base + L.oUt);
   T* Mp = (T*)(base + L.oM);
-  T* S0 = (T*)(base + L.oS0);
   int32_t* flag = (int32_t*)(base + L.oFlag);
   hipError_t e = hipMemsetAsync(flag, 0, 16, st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(poly flag)");
   const size_t gj_lds = (size_t)3 * n * sizeof(T);
   if (gj_lds > 64 * 1024) {
-    set_error("mpcqp_solve_poly: n=%d too large for the shared inverse", n);
+    set_error("mpcqp_poly_setup: n=%d too large for the shared inverse", n);
     return MPCQP_ENOTSUP;
   }
   hipLaunchKernelGGL(gj_inverse_kernel<T>, dim3(1), dim3(1024), gj_lds, st, (const T*)H, n, W,
@@ -384,19 +457,41 @@ static int solve_poly_t(int batch, int n, int m, const void* H, const void* f, i
   hipLaunchKernelGGL(form_m_kernel<T>, dim3((mt * mt + thr - 1) / thr), dim3(thr), 0, st,
                      (const T*)G, m, n, mt, (const T*)Ut, Mp);
   MPCQP_CHECK_LAUNCH("form_m_kernel");
-  // s0 = -Ut f ; z0 = -Hinv f
-  hipLaunchKernelGGL(gemv_t_kernel<T>, dim3(batch), dim3(kWave), (size_t)n * sizeof(T), st, mt,
-                     n, T(-1), (const T*)Ut, (const T*)f, sf, T(0), S0, (int64_t)mt, 0);
-  MPCQP_CHECK_LAUNCH("gemv_t_kernel(s0)");
-  hipLaunchKernelGGL(gemv_t_kernel<T>, dim3(batch), dim3(kWave), (size_t)n * sizeof(T), st, n, n,
-                     T(-1), (const T*)Hinv, (const T*)f, sf, T(0), (T*)z, (int64_t)n, 0);
-  MPCQP_CHECK_LAUNCH("gemv_t_kernel(z0)");
+  if (nx > 0 && F) {
+    T* Kt = (T*)(base + L.oKt);
+    T* Lm = (T*)(base + L.oL);
+    hipLaunchKernelGGL(form_kt_kernel<T>, dim3((nx * n + thr - 1) / thr), dim3(thr), 0, st,
+                       (const T*)F, n, nx, (const T*)Hinv, Kt);
+    MPCQP_CHECK_LAUNCH("form_kt_kernel");
+    hipLaunchKernelGGL(form_l_kernel<T>, dim3((mt * nx + thr - 1) / thr), dim3(thr), 0, st,
+                       (const T*)G, m, n, mt, nx, (const T*)Kt, Lm);
+    MPCQP_CHECK_LAUNCH("form_l_kernel");
+  }
+  return MPCQP_OK;
+}
+
+template <typename T>
+static int poly_solve_t(int batch, int n, int m, int nbox, int nx, const void* ws,
+                        const void* x0, int64_t sX0, const void* f1, int64_t sF1, const void* hl,
+                        const void* hu, int64_t sh, const void* lbz, const void* ubz, void* z,
+                        void* y, int32_t* status, int max_iter, double tol, hipStream_t st) {
+  const int mt = m + (nbox ? n : 0);
+  const PolyWs L = poly_ws(sizeof(T), n, mt, nx);
+  const char* base = (const char*)ws;
   DualArgs<T> a;
   a.batch = batch; a.mt = mt; a.m1 = m;
-  a.M = Mp; a.sM = 0; a.s0 = S0; a.sS0 = mt;
+  a.M = (const T*)(base + L.oM); a.sM = 0;
   a.l1 = (const T*)hl; a.u1 = (const T*)hu; a.s1 = sh;
   a.l2 = (const T*)lbz; a.u2 = (const T*)ubz;
-  a.y = (T*)y; a.status = status;
+  a.n = n; a.nx = x0 ? nx : 0;
+  a.Ut = (const T*)(base + L.oUt);
+  a.Hinv = (const T*)(base + L.oHinv);
+  a.Kt = (const T*)(base + L.oKt);
+  a.L = (const T*)(base + L.oL);
+  a.x0 = x0 ? (const T*)x0 : nullptr; a.sX0 = sX0;
+  a.f1 = (const T*)f1; a.sF1 = sF1;
+  a.flag = (const int32_t*)(base + L.oFlag);
+  a.z = (T*)z; a.y = (T*)y; a.status = status;
   a.max_iter = max_iter > 0 ? max_iter : 4 * mt + 40;
   a.tol = tol > 0 ? (T)tol : (sizeof(T) == 8 ? (T)1e-12 : (T)1e-6);
   switch ((mt + 7) / 8) {
@@ -410,18 +505,62 @@ static int solve_poly_t(int batch, int n, int m, const void* H, const void* f, i
     default: launch_dual<T, 8>(a, st); break;
   }
   MPCQP_CHECK_LAUNCH("dual_range_kernel");
-  // z = z0 - Ut' y
-  hipLaunchKernelGGL(gemv_t_kernel<T>, dim3(batch), dim3(kWave), (size_t)mt * sizeof(T), st, mt,
-                     n, T(-1), (const T*)Ut, (const T*)y, (int64_t)mt, T(1), (T*)z, (int64_t)n, 1);
-  MPCQP_CHECK_LAUNCH("gemv_t_kernel(z)");
   return MPCQP_OK;
 }
 
 }  // namespace mpcqp
 
 extern "C" int64_t mpcqp_solve_poly_workspace(int dtype, int batch, int n, int m, int nbox) {
+  (void)batch;
   const int mt = m + (nbox ? n : 0);
-  return mpcqp::poly_ws(mpcqp::dtype_size(dtype), batch, n, mt).total;
+  return mpcqp::poly_ws(mpcqp::dtype_size(dtype), n, mt, 0).total;
+}
+
+extern "C" int64_t mpcqp_poly_workspace(int dtype, int n, int m, int nbox, int nx) {
+  const int mt = m + (nbox ? n : 0);
+  return mpcqp::poly_ws(mpcqp::dtype_size(dtype), n, mt, nx).total;
+}
+
+#define MPCQP_POLY_SIZES(fn)                                                                  \
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64 || dtype == MPCQP_F32, fn ": bad dtype %d", dtype);       \
+  MPCQP_CHECK_ARG(n >= 1 && m >= 0 && nx >= 0 && nx <= 16, fn ": bad sizes");                  \
+  MPCQP_CHECK_ARG(m + (nbox ? n : 0) >= 1 && m + (nbox ? n : 0) <= 64,                         \
+                  fn ": rows m_total=%d outside [1,64]", m + (nbox ? n : 0));
+
+extern "C" int mpcqp_poly_setup(int dtype, int n, int m, int nbox, int nx, const void* H,
+                                const void* G, const void* F, void* workspace,
+                                int64_t workspace_bytes, void* stream) {
+  using namespace mpcqp;
+  MPCQP_POLY_SIZES("mpcqp_poly_setup")
+  MPCQP_CHECK_ARG(H && workspace, "mpcqp_poly_setup: H and workspace are required");
+  MPCQP_CHECK_ARG(m == 0 || G, "mpcqp_poly_setup: G required when m > 0");
+  MPCQP_CHECK_ARG(nx == 0 || F, "mpcqp_poly_setup: F required when nx > 0");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MPCQP_F64)
+    return poly_setup_t<double>(n, m, nbox, nx, H, G, F, workspace, workspace_bytes, st);
+  return poly_setup_t<float>(n, m, nbox, nx, H, G, F, workspace, workspace_bytes, st);
+}
+
+extern "C" int mpcqp_poly_solve(int dtype, int batch, int n, int m, int nbox, int nx,
+                                const void* workspace, const void* x0, int64_t strideX0,
+                                const void* f, int64_t stridef, const void* hl, const void* hu,
+                                int64_t strideh, const void* lbz, const void* ubz, void* z,
+                                void* y, int32_t* status, int max_iter, double tol,
+                                void* stream) {
+  using namespace mpcqp;
+  MPCQP_POLY_SIZES("mpcqp_poly_solve")
+  MPCQP_CHECK_ARG(batch >= 0, "mpcqp_poly_solve: batch < 0");
+  MPCQP_CHECK_ARG(workspace && z && status, "mpcqp_poly_solve: workspace, z, status are required");
+  MPCQP_CHECK_ARG(x0 == nullptr || nx > 0, "mpcqp_poly_solve: x0 given but nx = 0");
+  MPCQP_CHECK_ARG(strideX0 >= 0 && stridef >= 0 && strideh >= 0, "mpcqp_poly_solve: negative stride");
+  MPCQP_CHECK_ARG(!nbox || lbz || ubz, "mpcqp_poly_solve: nbox set without lbz/ubz");
+  if (batch == 0) return MPCQP_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == MPCQP_F64)
+    return poly_solve_t<double>(batch, n, m, nbox, nx, workspace, x0, strideX0, f, stridef, hl,
+                                hu, strideh, lbz, ubz, z, y, status, max_iter, tol, st);
+  return poly_solve_t<float>(batch, n, m, nbox, nx, workspace, x0, strideX0, f, stridef, hl, hu,
+                             strideh, lbz, ubz, z, y, status, max_iter, tol, st);
 }
 
 extern "C" int mpcqp_solve_poly(int dtype, int batch, int n, int m, const void* H, const void* f,
@@ -430,18 +569,16 @@ extern "C" int mpcqp_solve_poly(int dtype, int batch, int n, int m, const void* 
                                 void* y, int32_t* status, int max_iter, double tol,
                                 void* workspace, int64_t workspace_bytes, void* stream) {
   using namespace mpcqp;
-  MPCQP_CHECK_ARG(dtype == MPCQP_F64 || dtype == MPCQP_F32, "mpcqp_solve_poly: bad dtype %d", dtype);
-  MPCQP_CHECK_ARG(batch >= 0 && n >= 1 && m >= 0, "mpcqp_solve_poly: bad sizes");
-  const int mt = m + ((lbz || ubz) ? n : 0);
-  MPCQP_CHECK_ARG(mt >= 1 && mt <= 64, "mpcqp_solve_poly: rows m_total=%d outside [1,64]", mt);
+  const int nbox = (lbz || ubz) ? 1 : 0, nx = 0;
+  MPCQP_POLY_SIZES("mpcqp_solve_poly")
+  MPCQP_CHECK_ARG(batch >= 0, "mpcqp_solve_poly: batch < 0");
   MPCQP_CHECK_ARG(H && f && z && y && status && workspace, "mpcqp_solve_poly: null pointer");
   MPCQP_CHECK_ARG(m == 0 || G, "mpcqp_solve_poly: G required when m > 0");
   MPCQP_CHECK_ARG(stridef >= 0 && strideh >= 0, "mpcqp_solve_poly: negative stride");
   if (batch == 0) return MPCQP_OK;
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == MPCQP_F64)
-    return solve_poly_t<double>(batch, n, m, H, f, stridef, G, hl, hu, strideh, lbz, ubz, z, y,
-                                status, max_iter, tol, workspace, workspace_bytes, st);
-  return solve_poly_t<float>(batch, n, m, H, f, stridef, G, hl, hu, strideh, lbz, ubz, z, y,
-                             status, max_iter, tol, workspace, workspace_bytes, st);
+  int rc = mpcqp_poly_setup(dtype, n, m, nbox, nx, H, G, nullptr, workspace, workspace_bytes,
+                            stream);
+  if (rc != MPCQP_OK) return rc;
+  return mpcqp_poly_solve(dtype, batch, n, m, nbox, nx, workspace, nullptr, 0, f, stridef, hl,
+                          hu, strideh, lbz, ubz, z, y, status, max_iter, tol, stream);
 }

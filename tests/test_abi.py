@@ -72,8 +72,12 @@ def test_zero_batch_is_noop(lib):
 
 
 def test_workspace_query(lib):
+    # shared factors only: independent of the batch size
     w = lib.mpcqp_solve_poly_workspace(nat.F64, 1024, 200, 40, 0)
-    assert w >= (200 * 200 * 2 + 40 * 200 + 40 * 41 // 2 + 1024 * 40) * 8
+    assert w >= (200 * 200 * 2 + 40 * 200 + 40 * 41 // 2) * 8
+    assert w == lib.mpcqp_solve_poly_workspace(nat.F64, 1, 200, 40, 0)
+    w2 = lib.mpcqp_poly_workspace(nat.F64, 200, 40, 0, 12)
+    assert w2 >= w + (12 * 200 + 40 * 12) * 8
 
 
 def test_missing_library_fails_loudly(tmp_path):

@@ -74,3 +74,36 @@ def test_poly_two_sided_with_box(dev):
         hs = np.concatenate([hu[b], -hl[b]])
         zr, _, _ = oq.poly_qp(H, f[b], Gs, hs, lb=np.full(n, -0.7), ub=np.full(n, 0.7))
         assert np.abs(z[b] - zr).max() < 1e-8
+
+
+@pytest.mark.parametrize("nx,nu,N,m,box", [(12, 4, 50, 40, False), (4, 2, 10, 12, True), (2, 1, 20, 6, True)])
+def test_poly_parametric_x0(dev, nx, nu, N, m, box):
+    """PolyQP: shared factors once (poly_setup), per-instance x0 -> z with the
+    fused s0 / z epilogue; BASELINE config-4 shape first.  Checked against the
+    Goldfarb-Idnani oracle on the explicitly condensed QP."""
+    rng = np.random.default_rng(nx * 100 + N)
+    U, _ = np.linalg.qr(rng.normal(size=(nx, nx)))
+    A = (U * rng.uniform(0.5, 0.98, nx)) @ U.T
+    B = rng.normal(size=(nx, nu)) / np.sqrt(nx)
+    Q, R = np.eye(nx), 0.1 * np.eye(nu)
+    n = N * nu
+    d = oc.condense(A, B, Q, R, Q, N)
+    G = rng.normal(size=(m, n))
+    h = rng.uniform(0.5, 1.5, size=m)
+    b = 24
+    X0 = rng.normal(size=(b, nx)) * 3
+    f1 = rng.normal(size=(b, n)) * 0.1
+    lbz, ubz = (-0.4, 0.4) if box else (None, None)
+    qp = batched.PolyQP(_t(oc.pack_lower(d["H"]), dev), _t(G, dev), _t(d["F"], dev), lbz, ubz)
+    z, y, st = qp.solve(_t(X0, dev), _t(f1, dev), hu=_t(h, dev))
+    assert (batched.status_code(st) == 0).all(), batched.status_code(st)
+    z = z.cpu().numpy()
+    for i in range(b):
+        fi = d["F"] @ X0[i] + f1[i]
+        zr = oq.poly_qp(d["H"], fi, G, h, None if lbz is None else np.full(n, lbz),
+                        None if ubz is None else np.full(n, ubz))[0]
+        assert np.abs(z[i] - zr).max() < 1e-8 * max(1.0, np.abs(zr).max()), np.abs(z[i] - zr).max()
+    # same factors, gradient-only form (x0 = None) gives the same answer
+    z2, _, st2 = qp.solve(None, _t(X0 @ d["F"].T + f1, dev), hu=_t(h, dev))
+    assert (batched.status_code(st2) == 0).all()
+    assert np.abs(z2.cpu().numpy() - z).max() < 1e-9
