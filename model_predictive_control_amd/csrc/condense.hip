@@ -17,12 +17,19 @@
 // instance; Gamma and Phi fall out of the forward sweep for free.
 //
 // Mapping: one instance per 64-lane workgroup (= one wavefront).  The
-// per-instance matrices (A_k, B_k, Q, R, Qf, W_k, xbar, y) live in LDS; lane c
-// owns column c of [H | F] (z-columns then Phi-columns), so each H row is
-// written by consecutive lanes to consecutive packed addresses.  For nx <= 4
-// the three recursions run redundantly in every lane's registers (no LDS round
-// trips on the serial chain); wider states use an LDS-parallel recursion.
+// per-instance matrices (A_k, B_k, Q, R, Qf, W_k, xbar, y_k) live in
+// LDS; lane c owns column c of [H | F] (z-columns then Phi-columns), so each H
+// row is written by consecutive lanes to consecutive packed addresses.  For
+// nx <= 2 the recursions run redundantly in every lane's registers (no LDS
+// round trips on the serial chain); wider states use an LDS-parallel W
+// recursion with the xbar recursion on other lanes of the same phases.
 #include "common.hpp"
+
+// Recursions redundantly in every lane's registers up to this nx; wider
+// states (already nx = 4) use the LDS-parallel recursion, one entry per lane.
+#ifndef MPCQP_CONDENSE_REG_NX
+#define MPCQP_CONDENSE_REG_NX 2
+#endif
 
 namespace mpcqp {
 
@@ -119,7 +126,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   __syncthreads();
 
   // ------------------------------------------------------------ recursions
-  if constexpr (NX <= 4) {
+  if constexpr (NX <= MPCQP_CONDENSE_REG_NX) {
     // Serial chains, computed redundantly by every lane in registers (the
     // wave issues one instruction stream either way); lane 0 publishes.
     T W[NX][NX], Qr[NX][NX], Ar[NX][NX];
@@ -197,105 +204,80 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
 #pragma unroll
           for (int q = 0; q < NX; ++q) Xs[(k + 1) * NX + q] = xk[q];
       }
-      // y_N = Qf xbar_N ; y_k = Q xbar_k + A_k' y_{k+1}
-      T yk[NX];
-#pragma unroll
-      for (int r = 0; r < NX; ++r) {
-        T acc = T(0);
-#pragma unroll
-        for (int q = 0; q < NX; ++q) acc = fma(Qfs[r * NX + q], xk[q], acc);
-        yk[r] = acc;
-      }
-      if (lane == 0)
-#pragma unroll
-        for (int q = 0; q < NX; ++q) Ys[N * NX + q] = yk[q];
-      __syncthreads();  // Xs visible (read back below by every lane)
-      for (int k = N - 1; k >= 1; --k) {
-        if (tv) {
-#pragma unroll
-          for (int r = 0; r < NX; ++r)
-#pragma unroll
-            for (int q = 0; q < NX; ++q) Ar[r][q] = As[k * NX * NX + r * NX + q];
-        }
-        T yn[NX];
-#pragma unroll
-        for (int r = 0; r < NX; ++r) {
-          T acc = T(0);
-#pragma unroll
-          for (int q = 0; q < NX; ++q) acc = fma(Qr[r][q], Xs[k * NX + q], acc);
-#pragma unroll
-          for (int p = 0; p < NX; ++p) acc = fma(Ar[p][r], yk[p], acc);
-          yn[r] = acc;
-        }
-#pragma unroll
-        for (int q = 0; q < NX; ++q) yk[q] = yn[q];
-        if (lane == 0)
-#pragma unroll
-          for (int q = 0; q < NX; ++q) Ys[k * NX + q] = yk[q];
-      }
     }
   } else {
-    // LDS-parallel recursions: entry (p,q) of each NX x NX product per lane.
+    // LDS-parallel recursions: entry (p,q) of each NX x NX product per lane;
+    // the free-response recursion x_{k+1} = A_k x_k + c_k runs in the same
+    // barrier phases on other lanes (it is independent of W).
+    const int xoff = (NX * NX <= 32) ? 32 : 0;
+    const int xl = lane - xoff;
+    const bool xlane = need_aff && xl >= 0 && xl < NX;
     for (int e = lane; e < NX * NX; e += kWave) Ws[N * NX * NX + e] = Qfs[e];
+    if (xlane) Xs[xl] = X0s[xl];
     __syncthreads();
-    for (int k = N - 1; k >= 1; --k) {
+    for (int t = 0; t < N; ++t) {
+      const int k = N - 1 - t;  // W step (k >= 1)
       const T* Ak = As + (tv ? k : 0) * NX * NX;
       const T* W1 = Ws + (k + 1) * NX * NX;
-      for (int e = lane; e < NX * NX; e += kWave) {
-        const int p = e / NX, q = e % NX;
-        T acc = T(0);
-#pragma unroll
-        for (int s = 0; s < NX; ++s) acc = fma(W1[p * NX + s], Ak[s * NX + q], acc);
-        Ts[e] = acc;
-      }
-      __syncthreads();
-      for (int e = lane; e < NX * NX; e += kWave) {
-        const int r = e / NX, q = e % NX;
-        T acc = Qs[e];
-#pragma unroll
-        for (int p = 0; p < NX; ++p) acc = fma(Ak[p * NX + r], Ts[p * NX + q], acc);
-        Ws[k * NX * NX + e] = acc;
-      }
-      __syncthreads();
-    }
-    if (need_aff) {
-      if (lane < NX) Xs[lane] = X0s[lane];
-      __syncthreads();
-      for (int k = 0; k < N; ++k) {
-        const T* Ak = As + (tv ? k : 0) * NX * NX;
-        if (lane < NX) {
-          T acc = Cs[k * NX + lane];
-#pragma unroll
-          for (int q = 0; q < NX; ++q) acc = fma(Ak[lane * NX + q], Xs[k * NX + q], acc);
-          Xs[(k + 1) * NX + lane] = acc;
-        }
-        __syncthreads();
-      }
-      if (lane < NX) {
-        T acc = T(0);
-#pragma unroll
-        for (int q = 0; q < NX; ++q) acc = fma(Qfs[lane * NX + q], Xs[N * NX + q], acc);
-        Ys[N * NX + lane] = acc;
-      }
-      __syncthreads();
-      for (int k = N - 1; k >= 1; --k) {
-        const T* Ak = As + (tv ? k : 0) * NX * NX;
-        if (lane < NX) {
+      if (k >= 1) {
+        for (int e = lane; e < NX * NX; e += kWave) {
+          const int p = e / NX, q = e % NX;
           T acc = T(0);
 #pragma unroll
-          for (int q = 0; q < NX; ++q) acc = fma(Qs[lane * NX + q], Xs[k * NX + q], acc);
+          for (int s = 0; s < NX; ++s) acc = fma(W1[p * NX + s], Ak[s * NX + q], acc);
+          Ts[e] = acc;
+        }
+      }
+      if (xlane) {
+        const T* At = As + (tv ? t : 0) * NX * NX;
+        T acc = Cs[t * NX + xl];
 #pragma unroll
-          for (int p = 0; p < NX; ++p) acc = fma(Ak[p * NX + lane], Ys[(k + 1) * NX + p], acc);
-          Ys[k * NX + lane] = acc;
+        for (int q = 0; q < NX; ++q) acc = fma(At[xl * NX + q], Xs[t * NX + q], acc);
+        Xs[(t + 1) * NX + xl] = acc;
+      }
+      __syncthreads();
+      if (k >= 1) {
+        for (int e = lane; e < NX * NX; e += kWave) {
+          const int r = e / NX, q = e % NX;
+          T acc = Qs[e];
+#pragma unroll
+          for (int p = 0; p < NX; ++p) acc = fma(Ak[p * NX + r], Ts[p * NX + q], acc);
+          Ws[k * NX * NX + e] = acc;
         }
         __syncthreads();
       }
     }
   }
   __syncthreads();
+  // adjoint y_N = Qf xbar_N, y_k = Q xbar_k + A_k' y_{k+1}  (f = B_k' y_{k+1}).
+  // Summing f along the columns instead (f_col = sum_k s_k' Q xbar_k) removes
+  // this chain but loses ~10x accuracy in fp32 (cancellation), so it stays.
+  if (need_aff) {
+    if (lane < NX) {
+      T acc = T(0);
+#pragma unroll
+      for (int q = 0; q < NX; ++q) acc = fma(Qfs[lane * NX + q], Xs[N * NX + q], acc);
+      Ys[N * NX + lane] = acc;
+    }
+    __syncthreads();
+    for (int k = N - 1; k >= 1; --k) {
+      const T* Ak = As + (tv ? k : 0) * NX * NX;
+      if (lane < NX) {
+        T acc = T(0);
+#pragma unroll
+        for (int q = 0; q < NX; ++q) acc = fma(Qs[lane * NX + q], Xs[k * NX + q], acc);
+#pragma unroll
+        for (int p = 0; p < NX; ++p) acc = fma(Ak[p * NX + lane], Ys[(k + 1) * NX + p], acc);
+        Ys[k * NX + lane] = acc;
+      }
+      __syncthreads();
+    }
+  }
 
   // ------------------------------------------------------- column sweep
-  const int ncol = n + nx;
+  // z columns (H, Gam), then -- only when F or Phi is requested -- the x0
+  // columns
+  const int ncol = n + ((a.F || a.Phi) ? nx : 0);
   T* Hb = a.H + (int64_t)b * ((int64_t)n * (n + 1) / 2);
   T* Fb = a.F ? a.F + (int64_t)b * n * nx : nullptr;
   T* Gb = a.Gam ? a.Gam + (int64_t)b * ((int64_t)N * nx * n) : nullptr;
@@ -333,7 +315,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
         if (isz && Gb) {
 #pragma unroll
           for (int q = 0; q < NX; ++q)
-            if (q < nx) Gb[((int64_t)(i * nx + q)) * n + col] = s[q];
+            if (q < nx) __builtin_nontemporal_store(s[q], &Gb[((int64_t)(i * nx + q)) * n + col]);
         }
         if (!isz && Pb) {
 #pragma unroll
@@ -357,7 +339,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
         const int r = i * nu + aa;
         if (act) {
           if (isz) {
-            if (r >= col) Hb[(int64_t)r * (r + 1) / 2 + col] = o;
+            if (r >= col) __builtin_nontemporal_store(o, &Hb[(int64_t)r * (r + 1) / 2 + col]);
           } else if (Fb) {
             Fb[r * nx + bc] = o;
           }

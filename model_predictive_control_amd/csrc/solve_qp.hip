@@ -104,14 +104,15 @@ void qp_wg_kernel(QpArgs<T> a) {
     // sweep every z in: M = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']]
     for (int k = 0; k < n; ++k) {
       T* cbuf = sm + ((k & 1) ? L::oCol1 : L::oCol0);
-      M.put_col(k, cbuf);
+      T* rbuf = sm + ((k & 1) ? L::oRow1 : L::oRow0);
+      M.put_col(k, cbuf, rbuf);
       __syncthreads();
       const T d = cbuf[k];
       if (!(d > T(0))) {
         code = MPCQP_STATUS_NOT_CONVEX;
         break;
       }
-      M.sweep_buf(k, T(1), d, cbuf);
+      M.sweep_buf(k, T(1), d, cbuf, rbuf);
     }
     if (code == MPCQP_STATUS_OPTIMAL) {
       M.diag_abs(sm + L::oScale);
@@ -155,6 +156,7 @@ static int launch_qp_bs(const QpArgs<T>& a, hipStream_t st) {
 // 512 threads (32 x 16 grid of BR x 2BR blocks).
 using Shape64 = WShape<16, 4, 16, 4>;
 using Shape128 = WShape<32, 4, 16, 8>;
+using Shape160 = WShape<32, 5, 16, 10>;
 using Shape192 = WShape<32, 6, 16, 12>;
 
 template <typename T>
@@ -167,6 +169,7 @@ int launch_qp(const QpArgs<T>& a, hipStream_t st) {
   const int nt = a.n + a.m;
   if (nt <= 64) return launch_qp_bs<T, Shape64>(a, st);
   if (nt <= 128) return launch_qp_bs<T, Shape128>(a, st);
+  if (nt <= 160) return launch_qp_bs<T, Shape160>(a, st);
   if (nt <= 192) return launch_qp_bs<T, Shape192>(a, st);
   set_error("qp_wg: n + m = %d exceeds %d", nt, max_qp_size<T>());
   return MPCQP_ENOTSUP;

@@ -112,9 +112,10 @@ struct WSym {
     bj = tid / GR;
   }
 
-  // Column kc (uniform) of this thread's block into buf[row].  A uniform
-  // compile-time switch; the asm marker keeps the cases from being merged
-  // back into one dynamically indexed access (which would live in scratch).
+  // Column kc / row kr (uniform) of this thread's block into an LDS vector.
+  // Uniform compile-time switches that only READ registers; the asm marker
+  // keeps the cases from being merged back into one dynamically indexed
+  // access (which would live in scratch).
   template <int C>
   __device__ __forceinline__ void put_col_sel(int kc, T* buf) {
     if constexpr (C < BC) {
@@ -127,72 +128,83 @@ struct WSym {
       }
     }
   }
-  // Publish column k into buf (caller barriers before reading).
-  __device__ __forceinline__ void put_col(int k, T* buf) {
-    const int kb = k / BC;
-    if (bj == kb) put_col_sel<0>(k - kb * BC, buf);
-  }
-  __device__ __forceinline__ void get_col(const T* buf, T (&colr)[BR], T (&colc)[BC]) const {
-#pragma unroll
-    for (int r = 0; r < BR; ++r) colr[r] = buf[bi * BR + r];
-#pragma unroll
-    for (int c = 0; c < BC; ++c) colc[c] = buf[bj * BC + c];
-  }
-
-  // Column kc := sigma*a (owners of column k), row kr := sigma*colc/d with
-  // -1/d on the diagonal (owners of row k).  Uniform compile-time switches
-  // with per-lane selects: no divergent branch writes matrix registers.
-  template <int C>
-  __device__ __forceinline__ void fix_col(int kc, bool own, T sigma, const T (&a)[BR]) {
-    if constexpr (C < BC) {
-      if (kc == C) {
-#pragma unroll
-        for (int r = 0; r < BR; ++r) m[r][C] = own ? sigma * a[r] : m[r][C];
-      } else {
-        fix_col<C + 1>(kc, own, sigma, a);
-      }
-    }
-  }
   template <int R>
-  __device__ __forceinline__ void fix_row(int kr, int k, bool own, T sigma, T rd,
-                                          const T (&colc)[BC]) {
+  __device__ __forceinline__ void put_row_sel(int kr, T* buf) {
     if constexpr (R < BR) {
       if (kr == R) {
 #pragma unroll
-        for (int c = 0; c < BC; ++c) {
-          const T v = (bj * BC + c == k) ? -rd : sigma * colc[c] * rd;
-          m[R][c] = own ? v : m[R][c];
-        }
+        for (int c = 0; c < BC; ++c) buf[bj * BC + c] = m[R][c];
+        asm volatile("; row %0" ::"n"(R));
       } else {
-        fix_row<R + 1>(kr, k, own, sigma, rd, colc);
+        put_row_sel<R + 1>(kr, buf);
+      }
+    }
+  }
+  // Publish column k into cbuf and row k into rbuf (the matrix is symmetric
+  // up to rounding; the sweep needs both bit-exactly, see sweep_col).  k is
+  // workgroup-uniform; readfirstlane keeps k and its block coordinates in
+  // SGPRs so the case switches are scalar branches (otherwise the compiler
+  // rewrites them through the lane-varying bi/bj into divergent searches).
+  // The caller barriers before reading.
+  __device__ __forceinline__ void put_col(int k, T* cbuf, T* rbuf) {
+    k = uniform(k);
+    const int kbc = k / BC, kbr = k / BR;
+    const int kc = uniform(k - kbc * BC);  // convergent: not re-derived in the branch
+    const int kr = uniform(k - kbr * BR);
+    if (bj == kbc) put_col_sel<0>(kc, cbuf);
+    if (bi == kbr) put_row_sel<0>(kr, rbuf);
+  }
+  // colr: column k at this thread's rows, colc: row k at its columns.
+  __device__ __forceinline__ void get_col(const T* cbuf, const T* rbuf, T (&colr)[BR],
+                                          T (&colc)[BC]) const {
+#pragma unroll
+    for (int r = 0; r < BR; ++r) colr[r] = cbuf[bi * BR + r];
+#pragma unroll
+    for (int c = 0; c < BC; ++c) colc[c] = rbuf[bj * BC + c];
+  }
+
+  // Goodnight sweep on pivot k (d = M_kk; colr = column k at this thread's
+  // rows, colc = row k at its columns, both bit-exact register copies):
+  //   M_ij -= M_ik M_kj / d;  row/col k := sigma M_.k / d;  M_kk := -1/d.
+  // No branch writes matrix registers:
+  //  * row k: with a_k = 1 exactly, the generic update leaves exactly
+  //    m_kj - 1*m_kj = 0, and fma(ik, srow_j, .) installs the new row
+  //    (ik in {0, 1}; elsewhere it adds an exact 0);
+  //  * column k: selects, executed only by the wave that owns it.
+  __device__ __forceinline__ void sweep_col(int k, T sigma, T d, const T (&colr)[BR],
+                                            const T (&colc)[BC]) {
+    k = uniform(k);
+    const T rd = fast_rcp(d);
+    const int kbc = k / BC, kbr = k / BR;
+    const int kc = uniform(k - kbc * BC), kr = uniform(k - kbr * BR);
+    T a[BR], ik[BR], srow[BC];
+#pragma unroll
+    for (int r = 0; r < BR; ++r) {
+      const bool isk = (bi == kbr) && (r == kr);
+      a[r] = isk ? T(1) : colr[r] * rd;
+      ik[r] = isk ? T(1) : T(0);
+    }
+#pragma unroll
+    for (int c = 0; c < BC; ++c) srow[c] = (bj * BC + c == k) ? -rd : sigma * colc[c] * rd;
+#pragma unroll
+    for (int r = 0; r < BR; ++r)
+#pragma unroll
+      for (int c = 0; c < BC; ++c) m[r][c] = fma(ik[r], srow[c], fma(-a[r], colc[c], m[r][c]));
+    if (__any(bj == kbc)) {
+      const bool own = bj == kbc;
+#pragma unroll
+      for (int r = 0; r < BR; ++r) {
+        const T sc = (bi * BR + r == k) ? -rd : sigma * colr[r] * rd;
+#pragma unroll
+        for (int c = 0; c < BC; ++c) m[r][c] = (own && c == kc) ? sc : m[r][c];
       }
     }
   }
 
-  // Goodnight sweep on pivot k with column k fetched (colr: rows bi*BR+r,
-  // colc: rows bj*BC+c of column k; d = M_kk):
-  //   M_ij -= M_ik M_kj / d;  row/col k := sigma M_.k / d;  M_kk := -1/d.
-  // The generic update runs everywhere; row and column k are then
-  // overwritten by the threads that own them (no cancellation).
-  __device__ __forceinline__ void sweep_col(int k, T sigma, T d, const T (&colr)[BR],
-                                            const T (&colc)[BC]) {
-    const T rd = fast_rcp(d);
-    T a[BR];
-#pragma unroll
-    for (int r = 0; r < BR; ++r) a[r] = colr[r] * rd;
-#pragma unroll
-    for (int r = 0; r < BR; ++r)
-#pragma unroll
-      for (int c = 0; c < BC; ++c) m[r][c] = fma(-a[r], colc[c], m[r][c]);
-    const int kbc = k / BC, kbr = k / BR;
-    fix_col<0>(k - kbc * BC, bj == kbc, sigma, a);
-    fix_row<0>(k - kbr * BR, k, bi == kbr, sigma, rd, colc);
-  }
-
-  // Same, reading column k from its LDS buffer (short live ranges).
-  __device__ __forceinline__ void sweep_buf(int k, T sigma, T d, const T* buf) {
+  // Same, reading column/row k from their LDS buffers (short live ranges).
+  __device__ __forceinline__ void sweep_buf(int k, T sigma, T d, const T* cbuf, const T* rbuf) {
     T colr[BR], colc[BC];
-    get_col(buf, colr, colc);
+    get_col(cbuf, rbuf, colr, colc);
     sweep_col(k, sigma, d, colr, colc);
   }
 
@@ -274,7 +286,9 @@ struct WLds {
   static constexpr int NMAX = S::NMAX;
   static constexpr int oCol0 = 0;
   static constexpr int oCol1 = oCol0 + NMAX;
-  static constexpr int oW = oCol1 + NMAX;
+  static constexpr int oRow0 = oCol1 + NMAX;
+  static constexpr int oRow1 = oRow0 + NMAX;
+  static constexpr int oW = oRow1 + NMAX;
   static constexpr int oLo = oW + NMAX;
   static constexpr int oHi = oLo + NMAX;
   static constexpr int oF = oHi + NMAX;
@@ -370,6 +384,9 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
       T viol, valp;
       int p;
       scan(viol, p, valp);
+      p = uniform(p);
+      viol = readlane(viol, 0);
+      valp = readlane(valp, 0);
       if (!(viol > tol)) break;
       const T lop = lo[p], hip = hi[p];
       const int side = (valp < lop) ? 1 : 2;
@@ -387,8 +404,9 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
           goto out;
         }
         T* cbuf = sm + (cb ? L::oCol1 : L::oCol0);
+        T* rbuf = sm + (cb ? L::oRow1 : L::oRow0);
         cb ^= 1;
-        M.put_col(p, cbuf);
+        M.put_col(p, cbuf, rbuf);
         __syncthreads();
         const T* crb = cbuf + M.bi * BS;  // column p at this thread's rows
         const T mpp = cbuf[p];
@@ -410,6 +428,8 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
           k = take ? i : k;
         }
         rowg_argmin<S::GR>(ti, k);
+        k = uniform(k);
+        ti = readlane(ti, 0);
         if (!(ti < Lim<T>::inf()) && !(t2 < Lim<T>::inf())) {
           code = MPCQP_STATUS_INFEASIBLE;
           goto out;
@@ -433,22 +453,25 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
         T sigma = pz ? T(-1) : T(1);  // p inactive: swept if z, unswept if row
         T d = mpp;
         const T* sbuf = cbuf;
+        const T* srbuf = rbuf;
         if (partial) {
           if (!dep) valp = fma(sgn, s_eff, valp);
           T* kbuf = sm + (cb ? L::oCol1 : L::oCol0);
+          T* krbuf = sm + (cb ? L::oRow1 : L::oRow0);
           cb ^= 1;
-          M.put_col(k, kbuf);
+          M.put_col(k, kbuf, krbuf);
           __syncthreads();
           idx = k;
           sigma = (k < nz) ? T(1) : T(-1);  // k active: unswept if z, swept if row
           d = kbuf[k];
           sbuf = kbuf;
+          srbuf = krbuf;
         }
         if (partial ? !(d > T(0)) : !(d < T(0))) {
           code = MPCQP_STATUS_NOT_CONVEX;
           goto out;
         }
-        M.sweep_buf(idx, sigma, d, sbuf);
+        M.sweep_buf(idx, sigma, d, sbuf, srbuf);
 #pragma unroll
         for (int r = 0; r < BS; ++r) {
           const bool me = M.bi * BS + r == idx;
@@ -464,7 +487,7 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
       T viol, valp;
       int p;
       scan(viol, p, valp);
-      active = viol > tol;
+      active = readlane(viol, 0) > tol;
     }
   }
   if (active) code = MPCQP_STATUS_MAXITER;
