@@ -82,8 +82,8 @@ __device__ __forceinline__ int gi_box_core(Sym2D<T, BS>& M, T* buf, const T* fs,
       if (st[r] == 0) {
         const int i = M.bi * BS + r;
         const T li = lbs[i], ui = ubs[i];
-        const T vl = finite(li) ? (li - zr[r]) / (T(1) + fabs(li)) : -Lim<T>::inf();
-        const T vu = finite(ui) ? (zr[r] - ui) / (T(1) + fabs(ui)) : -Lim<T>::inf();
+        const T vl = finite(li) ? (li - zr[r]) * fast_rcp(T(1) + fabs(li)) : -Lim<T>::inf();
+        const T vu = finite(ui) ? (zr[r] - ui) * fast_rcp(T(1) + fabs(ui)) : -Lim<T>::inf();
         const T v = fmax(vl, vu);
         if (v > viol) {
           viol = v;

@@ -127,17 +127,6 @@ struct QSym {
     return d;
   }
 
-  // Column k read back from the group's tile left by the last column(k)
-  // call (no publish, no barrier); valid while nothing rewrote the tile.
-  __device__ __forceinline__ T cached_column(int k, const T* gb, T (&colr)[BS], T (&colc)[BS]) const {
-    const int kb = k / BS, kc = k - kb * BS;
-#pragma unroll
-    for (int r = 0; r < BS; ++r) colr[r] = gb[(bi * BS + r) * BS + kc];
-#pragma unroll
-    for (int c = 0; c < BS; ++c) colc[c] = gb[(bj * BS + c) * BS + kc];
-    return gb[k * BS + kc];
-  }
-
   // Goodnight sweep (sigma = +1) / reverse sweep (sigma = -1) on pivot k with
   // its column already fetched:  M_ij - M_ik M_kj / d  off row/column k,
   // sigma M_kj / d on row k, sigma M_ik / d on column k, -1/d at (k, k).
@@ -205,8 +194,18 @@ struct QBoxLds {
   static constexpr int oF = QSym<T, BS>::BUF;
   static constexpr int oLb = oF + NMAX;
   static constexpr int oUb = oLb + NMAX;
-  static constexpr int size = oUb + NMAX;
+  static constexpr int oSl = oUb + NMAX;  // 1/(1+|lb|), NaN where lb = -inf
+  static constexpr int oSu = oSl + NMAX;  // 1/(1+|ub|), NaN where ub = +inf
+  static constexpr int size = oSu + NMAX;
 };
+
+// Relative-violation scale of a bound: 1/(1+|b|) for a finite bound, NaN for
+// an infinite one (a NaN violation never wins the arg-max and fmax skips it),
+// so the per-iteration scan multiplies instead of dividing.
+template <typename T>
+__device__ __forceinline__ T bound_scale(T bnd) {
+  return finite(bnd) ? T(1) / (T(1) + fabs(bnd)) : __builtin_nan("");
+}
 
 // Goldfarb-Idnani dual active set for the group's box QP (see gi_box_core.hpp
 // for the method); entry: M = -H^{-1}.  Primal and dual quantities are tracked
@@ -218,15 +217,17 @@ struct QBoxLds {
 template <typename T, int BS>
 __device__ __forceinline__ void qscan(const QSym<T, BS>& M, const int (&st)[BS], const T (&zr)[BS],
                                       const T* lbs, const T* ubs, T& viol, int& pi, T& zv) {
+  using L = QBoxLds<T, BS>;
+  const T* sls = lbs + (L::oSl - L::oLb);
+  const T* sus = lbs + (L::oSu - L::oLb);
   viol = -Lim<T>::inf();
   pi = 0;
   zv = T(0);
 #pragma unroll
   for (int r = 0; r < BS; ++r) {
     const int i = M.bi * BS + r;
-    const T li = lbs[i], ui = ubs[i];
-    const T vl = finite(li) ? (li - zr[r]) / (T(1) + fabs(li)) : -Lim<T>::inf();
-    const T vu = finite(ui) ? (zr[r] - ui) / (T(1) + fabs(ui)) : -Lim<T>::inf();
+    const T vl = (lbs[i] - zr[r]) * sls[i];  // NaN for an infinite bound
+    const T vu = (zr[r] - ubs[i]) * sus[i];
     const T v = (st[r] == 0) ? fmax(vl, vu) : -Lim<T>::inf();
     const bool take = v > viol;
     viol = take ? v : viol;
@@ -309,8 +310,8 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
       int k = 0;
 #pragma unroll
       for (int r = 0; r < BS; ++r) {
-        c[r] *= rm;  // dz per unit move of z_p
-        const T dmu = ((st[r] == 1) ? -c[r] : ((st[r] == 2) ? c[r] : T(0))) * sgn;
+        const T cs = c[r] * rm;  // dz per unit move of z_p (c stays raw for the sweep)
+        const T dmu = ((st[r] == 1) ? -cs : ((st[r] == 2) ? cs : T(0))) * sgn;
         const bool cand = (st[r] == 1 || st[r] == 2) && dmu < T(0);
         const T t = cand ? -mu[r] * fast_rcp(dmu) : Lim<T>::inf();
         const bool take = t < ti;
@@ -322,8 +323,9 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
       const T s_eff = stepping ? (partial ? ti : t2) : T(0);
 #pragma unroll
       for (int r = 0; r < BS; ++r) {
-        const T dmu = ((st[r] == 1) ? -c[r] : ((st[r] == 2) ? c[r] : T(0))) * sgn;
-        zr[r] = (st[r] == 0) ? fma(sgn * s_eff, c[r], zr[r]) : zr[r];
+        const T cs = c[r] * rm;
+        const T dmu = ((st[r] == 1) ? -cs : ((st[r] == 2) ? cs : T(0))) * sgn;
+        zr[r] = (st[r] == 0) ? fma(sgn * s_eff, cs, zr[r]) : zr[r];
         mu[r] = fma(s_eff, dmu, mu[r]);
       }
       gp = fma(-sgn * s_eff, rm, gp);  // d g_p / d z_p = -1 / M_pp
@@ -331,11 +333,19 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
       // the index whose state changes: k joins F (partial) or p leaves it (full)
       const int idx = partial ? k : p;
       const T sigma = partial ? T(1) : T(-1);
-      // full steps sweep on p, whose column is still in the tile: publish
+      // full steps sweep on p, whose column is still in registers: publish
       // again only when some group of the wave drops a bound
       T kr[BS], kcol[BS];
-      const T d = __any(stepping && partial) ? M.column(idx, gb, kr, kcol)
-                                             : M.cached_column(idx, gb, kr, kcol);
+      T d = mpp;
+      if (__any(stepping && partial)) {
+        d = M.column(idx, gb, kr, kcol);
+      } else {
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+          kr[r] = c[r];
+          kcol[r] = cc[r];
+        }
+      }
       const bool bad = stepping && (partial ? !(d > T(0)) : !(d < T(0)));
       if (stepping && !bad) {
         M.sweep_col(idx, sigma, d, kr, kcol);

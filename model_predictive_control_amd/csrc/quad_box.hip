@@ -60,6 +60,8 @@ __global__ __launch_bounds__(64, (QuadOcc<T, BS>::w)) void box_quad_kernel(BoxAr
     fs[i] = fi;
     lbs[i] = li;
     ubs[i] = ui;
+    lbs[i + (L::oSl - L::oLb)] = bound_scale(li);
+    lbs[i + (L::oSu - L::oLb)] = bound_scale(ui);
     nonfinite |= v && !finite(fi);
     badbox |= v && (!(li <= ui) || li == Lim<T>::inf() || ui == -Lim<T>::inf());
   }
@@ -208,6 +210,8 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
       const T ui = (v && a.ub) ? a.ub[(int64_t)b * a.sub + i] : Lim<T>::inf();
       lbs[i] = li;
       ubs[i] = ui;
+      lbs[i + (BL::oSl - BL::oLb)] = bound_scale(li);
+      lbs[i + (BL::oSu - BL::oLb)] = bound_scale(ui);
       fs[i] = T(0);
       badbox |= v && (!(li <= ui) || li == Lim<T>::inf() || ui == -Lim<T>::inf());
     }

@@ -166,8 +166,8 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
 #pragma unroll
       for (int r = 0; r < BS; ++r) {
         if (st[r] == 0) {
-          const T vl = finite(li[r]) ? (li[r] - si[r]) / (T(1) + fabs(li[r])) : -Lim<T>::inf();
-          const T vu = finite(ui[r]) ? (si[r] - ui[r]) / (T(1) + fabs(ui[r])) : -Lim<T>::inf();
+          const T vl = finite(li[r]) ? (li[r] - si[r]) * fast_rcp(T(1) + fabs(li[r])) : -Lim<T>::inf();
+          const T vu = finite(ui[r]) ? (si[r] - ui[r]) * fast_rcp(T(1) + fabs(ui[r])) : -Lim<T>::inf();
           const T vv = fmax(vl, vu);
           if (vv > viol) {
             viol = vv;

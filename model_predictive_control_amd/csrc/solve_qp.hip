@@ -65,6 +65,8 @@ void qp_wg_kernel(QpArgs<T> a) {
     lo[i] = l;
     hi[i] = u;
     fs[i] = fi;
+    sm[L::oSl + i] = finite(l) ? T(1) / (T(1) + fabs(l)) : __builtin_nan("");
+    sm[L::oSu + i] = finite(u) ? T(1) / (T(1) + fabs(u)) : __builtin_nan("");
   }
   WSym<T, S> M;
   M.init(tid);

@@ -292,7 +292,9 @@ struct WLds {
   static constexpr int oLo = oW + NMAX;
   static constexpr int oHi = oLo + NMAX;
   static constexpr int oF = oHi + NMAX;
-  static constexpr int oScale = oF + NMAX;
+  static constexpr int oSl = oF + NMAX;     // 1/(1+|lo|), NaN for an infinite bound
+  static constexpr int oSu = oSl + NMAX;    // 1/(1+|hi|)
+  static constexpr int oScale = oSu + NMAX;
   static constexpr int oRed = oScale + NMAX;  // GC*NMAX doubles (8-byte aligned)
   static constexpr int total = oRed + S::GC * NMAX * (int)(sizeof(double) / sizeof(T));
 };
@@ -316,6 +318,8 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
   T* hi = sm + L::oHi;
   T* fs = sm + L::oF;
   T* scale = sm + L::oScale;
+  const T* sls = sm + L::oSl;
+  const T* sus = sm + L::oSu;
   int st[BS];
   T mu[BS];
 #pragma unroll
@@ -364,9 +368,8 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
 #pragma unroll
     for (int r = 0; r < BS; ++r) {
       const int i = M.bi * BS + r;
-      const T li = lo[i], ui = hi[i];
-      const T vl = finite(li) ? (li - val[r]) / (T(1) + fabs(li)) : -Lim<T>::inf();
-      const T vu = finite(ui) ? (val[r] - ui) / (T(1) + fabs(ui)) : -Lim<T>::inf();
+      const T vl = (lo[i] - val[r]) * sls[i];  // NaN (never wins) for infinite bounds
+      const T vu = (val[r] - hi[i]) * sus[i];
       T v = (st[r] == 0) ? fmax(vl, vu) : -Lim<T>::inf();
       v = (v == v) ? v : -Lim<T>::inf();
       const bool take = v > viol;
