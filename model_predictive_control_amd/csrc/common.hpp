@@ -10,6 +10,35 @@
 
 namespace mpcqp {
 
+// Optional phase timing (tools/phase_timing.py builds a separate library
+// with -DMPCQP_PHASE_TIMING): every wave accumulates the s_memtime cycles of
+// each phase in registers (mpcqp_ph_acc[i]) and lane 0 adds them to
+// mpcqp_phase_cycles[] once, at the end of the kernel.
+#ifdef MPCQP_PHASE_TIMING
+extern __device__ unsigned long long mpcqp_phase_cycles[8];
+struct PhaseClock {
+  unsigned long long t, acc[8];
+  __device__ PhaseClock() : t(__builtin_readcyclecounter()) {
+    for (int i = 0; i < 8; ++i) acc[i] = 0;
+  }
+  __device__ __forceinline__ void mark(int i) {
+    const unsigned long long n = __builtin_readcyclecounter();
+    acc[i] += n - t;
+    t = n;
+  }
+  __device__ __forceinline__ void flush() {
+    if (threadIdx.x % 64 == 0)
+      for (int i = 0; i < 8; ++i) atomicAdd(&mpcqp_phase_cycles[i], acc[i]);
+  }
+};
+#define MPCQP_PHASE(i) mpcqp_clk.mark(i)
+#else
+#define MPCQP_PHASE(i) \
+  do {                 \
+  } while (0)
+#endif
+
+
 constexpr int kWave = 64;  // CDNA wavefront width (hard-coded, never warpSize)
 
 // ---------------------------------------------------------------- errors

@@ -214,20 +214,35 @@ __device__ __forceinline__ T bound_scale(T bnd) {
 // exact mat-vec refresh recomputes z and the multipliers and the bounds are
 // re-checked, so accumulated drift can never hide a violated bound.
 // live = this group holds a real instance.  Returns the status code.
+// Bounds of this lane's rows and their violation scales, held in registers
+// for the whole solve (loop-invariant; the scan runs every iteration).
+template <typename T, int BS>
+struct QBounds {
+  T lo[BS], hi[BS], sl[BS], su[BS];
+  __device__ __forceinline__ void load(const QSym<T, BS>& M, const T* lbs, const T* ubs) {
+    using L = QBoxLds<T, BS>;
+#pragma unroll
+    for (int r = 0; r < BS; ++r) {
+      const int i = M.bi * BS + r;
+      lo[r] = lbs[i];
+      hi[r] = ubs[i];
+      sl[r] = lbs[i + (L::oSl - L::oLb)];
+      su[r] = lbs[i + (L::oSu - L::oLb)];
+    }
+  }
+};
+
 template <typename T, int BS>
 __device__ __forceinline__ void qscan(const QSym<T, BS>& M, const int (&st)[BS], const T (&zr)[BS],
-                                      const T* lbs, const T* ubs, T& viol, int& pi, T& zv) {
-  using L = QBoxLds<T, BS>;
-  const T* sls = lbs + (L::oSl - L::oLb);
-  const T* sus = lbs + (L::oSu - L::oLb);
+                                      const QBounds<T, BS>& B, T& viol, int& pi, T& zv) {
   viol = -Lim<T>::inf();
   pi = 0;
   zv = T(0);
 #pragma unroll
   for (int r = 0; r < BS; ++r) {
     const int i = M.bi * BS + r;
-    const T vl = (lbs[i] - zr[r]) * sls[i];  // NaN for an infinite bound
-    const T vu = (zr[r] - ubs[i]) * sus[i];
+    const T vl = (B.lo[r] - zr[r]) * B.sl[r];  // NaN for an infinite bound
+    const T vu = (zr[r] - B.hi[r]) * B.su[r];
     const T v = (st[r] == 0) ? fmax(vl, vu) : -Lim<T>::inf();
     const bool take = v > viol;
     viol = take ? v : viol;
@@ -237,10 +252,20 @@ __device__ __forceinline__ void qscan(const QSym<T, BS>& M, const int (&st)[BS],
   group_argmax(viol, pi, zv);
 }
 
+#ifdef MPCQP_PHASE_TIMING
+#define MPCQP_CLK_PARAM , PhaseClock& mpcqp_clk
+#define MPCQP_CLK_ARG , mpcqp_clk
+#else
+#define MPCQP_CLK_PARAM
+#define MPCQP_CLK_ARG
+#endif
+
 template <typename T, int BS>
 __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, const T* lbs,
                                            const T* ubs, int n, int max_iter, T tol, bool live,
-                                           T (&zr)[BS], int& iters) {
+                                           T (&zr)[BS], int& iters MPCQP_CLK_PARAM) {
+  QBounds<T, BS> B;
+  B.load(M, lbs, ubs);
   int st[BS];
   T mu[BS];
 #pragma unroll
@@ -256,7 +281,7 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
 #pragma unroll
     for (int r = 0; r < BS; ++r) {
       const int i = M.bi * BS + r;
-      const T zA = (st[r] == 1) ? lbs[i] : ((st[r] == 2) ? ubs[i] : T(0));
+      const T zA = (st[r] == 1) ? B.lo[r] : ((st[r] == 2) ? B.hi[r] : T(0));
       w[r] = (st[r] == 0) ? fs[i] : -zA;
       zr[r] = zA;
     }
@@ -279,7 +304,7 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
       if (__any(active && need_p)) {
         T viol, zv;
         int pi;
-        qscan<T, BS>(M, st, zr, lbs, ubs, viol, pi, zv);
+        qscan<T, BS>(M, st, zr, B, viol, pi, zv);
         if (active && need_p) {
           if (!(viol > tol)) {
             active = false;  // settled (pending the exact re-check)
@@ -294,6 +319,7 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
           }
         }
       }
+      MPCQP_PHASE(5);
       if (!__any(active)) break;
       bool stepping = active;
       if (stepping && ++iters > max_iter) {
@@ -330,6 +356,7 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
       }
       gp = fma(-sgn * s_eff, rm, gp);  // d g_p / d z_p = -1 / M_pp
       zp = fma(sgn, s_eff, zp);
+      MPCQP_PHASE(6);
       // the index whose state changes: k joins F (partial) or p leaves it (full)
       const int idx = partial ? k : p;
       const T sigma = partial ? T(1) : T(-1);
@@ -364,6 +391,7 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
         }
         need_p = !partial;
       }
+      MPCQP_PHASE(7);
       if (bad) {
         code = MPCQP_STATUS_NOT_CONVEX;
         active = false;
@@ -373,14 +401,13 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
     refresh();
     T viol, zv;
     int pi;
-    qscan<T, BS>(M, st, zr, lbs, ubs, viol, pi, zv);
+    qscan<T, BS>(M, st, zr, B, viol, pi, zv);
     active = live && code == MPCQP_STATUS_OPTIMAL && viol > tol;
     if (!__any(active)) break;
   }
 #pragma unroll
   for (int r = 0; r < BS; ++r) {
-    const int i = M.bi * BS + r;
-    zr[r] = fmin(fmax(zr[r], lbs[i]), ubs[i]);
+    zr[r] = fmin(fmax(zr[r], B.lo[r]), B.hi[r]);
   }
   return code;
 }

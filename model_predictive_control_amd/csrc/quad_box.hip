@@ -20,6 +20,9 @@ struct QuadOcc {
 
 template <typename T, int BS>
 __global__ __launch_bounds__(64, (QuadOcc<T, BS>::w)) void box_quad_kernel(BoxArgsQ<T> a) {
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
   using L = QBoxLds<T, BS>;
   constexpr int NMAX = L::NMAX;
   constexpr int PMAX = NMAX * (NMAX + 1) / 2;
@@ -85,7 +88,7 @@ __global__ __launch_bounds__(64, (QuadOcc<T, BS>::w)) void box_quad_kernel(BoxAr
   T zr[BS];
   int iters = 0;
   const int c2 = gi_box_quad<T, BS>(M, gb, fs, lbs, ubs, n, a.max_iter, a.tol,
-                                    live && code == MPCQP_STATUS_OPTIMAL, zr, iters);
+                                    live && code == MPCQP_STATUS_OPTIMAL, zr, iters MPCQP_CLK_ARG);
   if (code == MPCQP_STATUS_OPTIMAL) code = c2;
   if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
 #pragma unroll
@@ -170,6 +173,9 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
   T* Mv = sm + L.oMinv;
   const int ld = L.ld;
 
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
   // ------------------------------------------------------------- stage in
   bool nonfinite = false, badbox = false;
   {
@@ -219,6 +225,7 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
   __syncthreads();
 
   int code = MPCQP_STATUS_OPTIMAL;
+  MPCQP_PHASE(0);
   // ------------------------------------- Riccati backward (all lanes, regs)
   {
     T P[NX][NX], Qr[NX][NX], Rr[NU][NU], Ar[NX][NX], Br[NX][NU];
@@ -345,6 +352,7 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
     }
     if (!ok) code = MPCQP_STATUS_NOT_CONVEX;
 
+    MPCQP_PHASE(1);
     // ---- free response xbar (forward) and adjoint y -> f (backward)
     if (tv == 0) load_sq<T, NX, NX>(As, Ar, NX);
     T xk[NX];
@@ -404,6 +412,7 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
   }
   __syncthreads();
 
+  MPCQP_PHASE(2);
   // ------------------------------ columns of -H^{-1}, one lane per column
   for (int c = q; c < n; c += 16) {
     const int jj = c / nu, bb = c - jj * nu;
@@ -476,6 +485,7 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
   }
   __syncthreads();
 
+  MPCQP_PHASE(3);
   // ------------------------------------------------ box QP on M = -H^{-1}
   QSym<T, BS> M;
   M.init(lane);
@@ -487,8 +497,12 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
   T zr[BS];
   int iters = 0;
   const int c2 = gi_box_quad<T, BS>(M, gb, fs, lbs, ubs, n, a.max_iter, a.tol,
-                                    live && code == MPCQP_STATUS_OPTIMAL, zr, iters);
+                                    live && code == MPCQP_STATUS_OPTIMAL, zr, iters MPCQP_CLK_ARG);
   if (code == MPCQP_STATUS_OPTIMAL) code = c2;
+  MPCQP_PHASE(4);
+#ifdef MPCQP_PHASE_TIMING
+  mpcqp_clk.flush();
+#endif
   if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
 #pragma unroll
     for (int r = 0; r < BS; ++r) zr[r] = __builtin_nan("");
@@ -576,3 +590,19 @@ template int mpc_box_quad<double>(const MpcArgsQ<double>&, hipStream_t);
 template int mpc_box_quad<float>(const MpcArgsQ<float>&, hipStream_t);
 
 }  // namespace mpcqp
+
+#ifdef MPCQP_PHASE_TIMING
+namespace mpcqp {
+__device__ unsigned long long mpcqp_phase_cycles[8];
+}
+// Debug library only: read (and optionally reset) the phase counters.
+extern "C" int mpcqp_debug_phase_cycles(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcqp::mpcqp_phase_cycles), 8 * sizeof(unsigned long long)) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mpcqp::mpcqp_phase_cycles), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif

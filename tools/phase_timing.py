@@ -1,0 +1,56 @@
+"""Per-phase cycle counts of the fused config-2 kernel (mpc_quad_kernel).
+
+Build (in the container):  python tools/phase_timing.py --build
+Run (GPU box):             python tools/phase_timing.py
+The debug library (-DMPCQP_PHASE_TIMING) is separate from the product one;
+lane 0 of each wave adds s_memtime deltas per phase into a device array.
+"""
+import ctypes, os, subprocess, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CS = os.path.join(ROOT, "model_predictive_control_amd", "csrc")
+LIB = os.path.join(ROOT, "model_predictive_control_amd", "lib", "libmpcqp_timing.so")
+SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.hip", "quad_box.hip",
+        "solve_qp.hip", "misc.hip"]
+PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/recheck", "GI: scan+argmax", "GI: pivot col+ratio", "GI: sweep"]
+
+if "--build" in sys.argv:
+    objs = []
+    for s in SRCS:
+        o = f"/tmp/timing_{s}.o"
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
+                        "-DMPCQP_PHASE_TIMING", "-I", os.path.join(ROOT, "include"), "-c",
+                        os.path.join(CS, s), "-o", o], check=True)
+        objs.append(o)
+    subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "--offload-arch=gfx950", "-o", LIB] + objs, check=True)
+    print("built", LIB)
+    sys.exit(0)
+
+os.environ["MPCQP_LIB"] = LIB
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+import bench  # noqa: E402
+from model_predictive_control_amd import _native, batched  # noqa: E402
+
+lib = _native.load()
+lib.mpcqp_debug_phase_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = (ctypes.c_ulonglong * 8)()
+
+
+class A:
+    pass
+
+
+a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1; a.mode = "fused"
+w = bench.Config2(a, torch.device("cuda"), 0)
+w._fused(0)
+torch.cuda.synchronize()
+lib.mpcqp_debug_phase_cycles(buf, 1)
+R = 10
+for _ in range(R):
+    w._fused(0)
+torch.cuda.synchronize()
+lib.mpcqp_debug_phase_cycles(buf, 1)
+waves = (a.batch + 3) // 4 * R
+tot = sum(buf[i] for i in range(8))
+for i, name in enumerate(PHASES):
+    print(f"{name:16s} {buf[i] / waves:10.0f} cycles/wave  {100 * buf[i] / tot:5.1f} %")
