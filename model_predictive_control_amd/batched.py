@@ -439,6 +439,11 @@ def rollout(A, B, K, x0, steps: int):
     return xs
 
 
+def max_qp_size(dtype=torch.float64) -> int:
+    """Largest n + m accepted by solve_qp (and n by solve_box) for dtype."""
+    return int(_lib().mpcqp_max_qp_size(_code(dtype)))
+
+
 def n_packed(n: int) -> int:
     return n * (n + 1) // 2
 

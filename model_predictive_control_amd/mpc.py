@@ -16,9 +16,11 @@ device:
 repeated ``sqp_iters`` times.  Any number of initial states is solved in one
 batch (``solve`` accepts x of shape (nx,) or (batch, nx)).
 
-Scope notes: the collision rows of main.py:95-104 are non-convex and out of
-scope; the state box (main.py:58-61) needs per-instance constraint rows and
-is not enforced by this controller yet ("next").
+With ``state_box=True`` (default) the state box of main.py:58-61 on x_1..x_N
+is enforced as well: step 3 also returns Gam and the free response xbar, and
+step 4 becomes ``mpcqp_solve_qp`` with rows  x_min - xbar <= Gam z <= x_max -
+xbar  (one QP per workgroup; needs N*(nx+nu) <= 192, i.e. N <= 32).  The
+collision rows of main.py:95-104 are non-convex and out of scope.
 """
 from __future__ import annotations
 
@@ -35,7 +37,7 @@ from .parameters import VehicleParameters
 class MPCController:
     def __init__(self, N: int, ts: float, params: VehicleParameters | None = None, model=None,
                  x_obs=None, *, Q=None, QN=None, R=None, sqp_iters: int = 3,
-                 dtype=torch.float64, device=None) -> None:
+                 state_box: bool = True, dtype=torch.float64, device=None) -> None:
         self.N = N
         self.ts = ts
         self.params = params or VehicleParameters()
@@ -58,7 +60,16 @@ class MPCController:
         self.ub_inputs = np.array([p.max_drive, p.max_steer])
         self.lbz = t(np.tile(self.lb_inputs, N))
         self.ubz = t(np.tile(self.ub_inputs, N))
-        self.bounds = dict(lbx=np.tile(self.lb_inputs, N), ubx=np.tile(self.ub_inputs, N))
+        # state box of main.py:58-61 on x_1..x_N (the g rows of main.py:99-100)
+        self.lb_states = np.array([p.min_pos_x, p.min_pos_y, p.min_heading, p.min_vel])
+        self.ub_states = np.array([p.max_pos_x, p.max_pos_y, p.max_heading, p.max_vel])
+        self.state_box = state_box
+        if state_box and N * (self.nx + self.nu) > batched.max_qp_size(dtype):
+            raise ValueError(f"state box needs N*(nx+nu) <= {batched.max_qp_size(dtype)} (N={N})")
+        self.xmin = t(np.tile(self.lb_states, N))
+        self.xmax = t(np.tile(self.ub_states, N))
+        self.bounds = dict(lbx=np.tile(self.lb_inputs, N), ubx=np.tile(self.ub_inputs, N),
+                           lbg=np.tile(self.lb_states, N), ubg=np.tile(self.ub_states, N))
         self.sqp_iters = sqp_iters
         self._warm = None
         self.last_status = None
@@ -80,10 +91,21 @@ class MPCController:
                 xs.append(fe_step_batched(xs[-1], U[:, k], self.params, self.ts))
             Xn = torch.stack(xs, 1)
             A, B, c = fe_linearize_batched(Xn, U, self.params, self.ts)
-            d = batched.condense(A.contiguous(), B.contiguous(), self.Q, self.R, self.QN, N,
-                                 x0=X0, c=c.contiguous(), tv=True, outputs=("H", "f"))
-            z, status = batched.solve_box(d["H"], d["f"], self.lbz, self.ubz)
+            if self.state_box:
+                d = batched.condense(A.contiguous(), B.contiguous(), self.Q, self.R, self.QN, N,
+                                     x0=X0, c=c.contiguous(), tv=True,
+                                     outputs=("H", "f", "Gam", "xbar"))
+                z, lam, status = batched.solve_qp(d["H"], d["f"], d["Gam"], self.xmin - d["xbar"],
+                                                  self.xmax - d["xbar"], self.lbz, self.ubz)
+                self.last_lam_g = lam
+            else:
+                d = batched.condense(A.contiguous(), B.contiguous(), self.Q, self.R, self.QN, N,
+                                     x0=X0, c=c.contiguous(), tv=True, outputs=("H", "f", "Gam", "xbar"))
+                z, status = batched.solve_box(d["H"], d["f"], self.lbz, self.ubz)
             U = z.view(b, N, nu)
+        # predicted states x_1..x_N of the last linearisation (IPOPT's "g" rows)
+        self.last_prediction = (d["xbar"] + torch.bmm(d["Gam"], z.unsqueeze(-1)).squeeze(-1)
+                                ).view(b, N, self.nx)
         self._warm = torch.cat([U[:, 1:], U[:, -1:]], 1).contiguous()
         self.last_status = status
         return z, status
@@ -96,9 +118,19 @@ class MPCController:
         z, status = self.solve_batch(X0)
         zn = z.cpu().numpy()
         st = batched.status_code(status).cpu().numpy()
+        g = self.last_prediction.reshape(X0.shape[0], -1).cpu().numpy()
         return {"x": zn.reshape(-1, 1) if single else zn,
+                "g": g.reshape(-1, 1) if single else g,
                 "status": st[0] if single else st,
                 "success": bool(st[0] == 0) if single else st == 0}
+
+    def log_step(self, log, sol, x0) -> None:
+        """Append one step to a session_2/log.py:8-12 ControllerLog:
+        solver_success, state_prediction (N+1, nx) = [x0; g], input_prediction (N, nu)."""
+        log.solver_success.append(bool(sol["success"]))
+        log.state_prediction.append(np.vstack([np.asarray(x0, float).reshape(1, -1),
+                                               np.asarray(sol["g"]).reshape(-1, self.nx)]))
+        log.input_prediction.append(self.reshape_input(sol))
 
     def reshape_input(self, sol):
         """main.py:118-119."""

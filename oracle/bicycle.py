@@ -37,8 +37,10 @@ def fe_jac_fd(x, u, ts, eps=1e-7):
     return A, B
 
 
-def rti_step(x0, U, ts, Q, QN, R, lbu, ubu, N, jac=fe_jac_fd):
-    """One SQP-RTI iteration: rollout, linearise, condense, exact box QP."""
+def rti_step(x0, U, ts, Q, QN, R, lbu, ubu, N, jac=fe_jac_fd, xmin=None, xmax=None):
+    """One SQP-RTI iteration: rollout, linearise, condense, exact QP with the
+    input box (main.py:68-69) and, when xmin/xmax are given, the state box on
+    x_1..x_N (main.py:58-61) as rows Gam z within [xmin, xmax] - xbar."""
     xs = [np.asarray(x0, float)]
     for k in range(N - 1):
         xs.append(fe(xs[-1], U[k], ts))
@@ -47,5 +49,10 @@ def rti_step(x0, U, ts, Q, QN, R, lbu, ubu, N, jac=fe_jac_fd):
         A[k], B[k] = jac(xs[k], U[k], ts)
         c[k] = fe(xs[k], U[k], ts) - A[k] @ xs[k] - B[k] @ U[k]
     d = oc.condense(A, B, Q, R, QN, N, x0=x0, c=c)
-    z, _, _ = oq.box_qp(d["H"], d["f"], np.tile(lbu, N), np.tile(ubu, N))
+    if xmin is None:
+        z, _, _ = oq.box_qp(d["H"], d["f"], np.tile(lbu, N), np.tile(ubu, N))
+    else:
+        G = np.vstack([d["Gam"], -d["Gam"]])
+        h = np.concatenate([np.tile(xmax, N) - d["xbar"], d["xbar"] - np.tile(xmin, N)])
+        z, _, _ = oq.poly_qp(d["H"], d["f"], G, h, np.tile(lbu, N), np.tile(ubu, N))
     return z.reshape(N, 2), d

@@ -95,7 +95,7 @@ def test_rollout_many(dev):
 def test_mpc_controller_rti_matches_oracle(dev):
     p = VehicleParameters()
     N, ts = 30, 0.08
-    ctrl = mpc.MPCController(N, ts, p, sqp_iters=1)
+    ctrl = mpc.MPCController(N, ts, p, sqp_iters=1, state_box=False)
     x0 = np.array([0.3, -0.1, 0.0, 0.0])
     sol = ctrl.solve(x0)
     assert sol["x"].shape == (N * 2, 1) and sol["success"]
@@ -106,7 +106,7 @@ def test_mpc_controller_rti_matches_oracle(dev):
                           np.array([-1, -0.384]), np.array([1, 0.384]), N)
     assert np.abs(U - Uref).max() < 1e-6
     # batched solve of many initial states == per-instance solves
-    ctrl2 = mpc.MPCController(N, ts, p, sqp_iters=1)
+    ctrl2 = mpc.MPCController(N, ts, p, sqp_iters=1, state_box=False)
     X0 = np.array([[0.3, -0.1, 0.0, 0.0], [0.5, 0.2, 0.3, 0.1], [-0.4, 0.1, -0.2, -0.2]])
     zb = ctrl2.solve(X0)["x"]
     for i in range(3):
@@ -115,6 +115,38 @@ def test_mpc_controller_rti_matches_oracle(dev):
         assert np.abs(zb[i].reshape(N, 2) - Ur).max() < 1e-6
     u0 = mpc.MPCController(N, ts, p)(x0)
     assert u0.shape == (2,) and np.all(np.abs(u0) <= [1, 0.384 + 1e-12])
+
+
+def test_mpc_controller_state_box_matches_oracle(dev):
+    """RTI step with the state box of main.py:58-61 (rows on x_1..x_N) against
+    the oracle (explicit condensing + Goldfarb-Idnani); initial velocities
+    near the |v| <= 0.5 bound make those rows active."""
+    p = VehicleParameters()
+    N, ts = 30, 0.08
+    Q = np.diag([1., 6., 0.2, 0.05])
+    xmin = np.array([p.min_pos_x, p.min_pos_y, p.min_heading, p.min_vel])
+    xmax = np.array([p.max_pos_x, p.max_pos_y, p.max_heading, p.max_vel])
+    X0 = np.array([[2.5, 1.5, 0.3, 0.45], [0.3, -0.1, 0.0, 0.0], [-2.0, -1.0, -0.5, -0.4]])
+    ctrl = mpc.MPCController(N, ts, p, sqp_iters=1, state_box=True)
+    sol = ctrl.solve(X0)
+    assert sol["success"].all(), sol["status"]
+    active_rows = 0
+    for i in range(3):
+        Ur, d = ob.rti_step(X0[i], np.zeros((N, 2)), ts, Q, 100 * Q, np.diag([1, 0.01]),
+                            np.array([-1, -0.384]), np.array([1, 0.384]), N, xmin=xmin, xmax=xmax)
+        assert np.abs(sol["x"][i].reshape(N, 2) - Ur).max() < 1e-6
+        g = d["xbar"] + d["Gam"] @ Ur.reshape(-1)
+        assert np.abs(sol["g"][i] - g).max() < 1e-6
+        assert (g <= np.tile(xmax, N) + 1e-8).all() and (g >= np.tile(xmin, N) - 1e-8).all()
+        active_rows += int((np.abs(g - np.tile(xmax, N)) < 1e-7).sum() + (np.abs(g - np.tile(xmin, N)) < 1e-7).sum())
+    assert active_rows > 0  # the state box binds for these starts
+    # ControllerLog output (session_2/log.py:8-12)
+    from model_predictive_control_amd.problems import ControllerLog
+    log = ControllerLog()
+    x0 = X0[1]
+    ctrl.log_step(log, ctrl.solve(x0), x0)
+    assert log.solver_success == [True]
+    assert log.state_prediction[0].shape == (N + 1, 4) and log.input_prediction[0].shape == (N, 2)
 
 
 def test_mpc_closed_loop_reaches_origin(dev):
