@@ -225,6 +225,21 @@ int mpcqp_riccati(int dtype, int batch, int nx, int nu, int N,
                   const void* Q, int64_t strideQ, const void* R, int64_t strideR,
                   const void* Pf, int64_t stridePf, void* P, void* K, void* stream);
 
+/*
+ * Batched re-linearisation of the kinematic bicycle for the RTI step of
+ * MPCController (session_4/main.py:41-113 on fwd_euler(KinematicBicycle),
+ * main.py:132-135, 250-251): per instance, roll the forward-Euler model out
+ * from x0 (4) under U (N x 2, the warm start) and write, for k = 0..N-1,
+ *   A_k = I + ts df/dx (N x 4 x 4), B_k = ts df/du (N x 4 x 2),
+ *   c_k = fd(x_k,u_k) - A_k x_k - B_k u_k (N x 4),
+ * and optionally the rolled-out states X (N+1 x 4).  Layouts match
+ * mpcqp_condense with MPCQP_TV.  params = {l_f, l_r, acceleration, friction}
+ * (parameters.py:7-8,47-48).  x = [p_x, p_y, psi, v], u = [a, delta].
+ */
+int mpcqp_bicycle_rti(int dtype, int batch, int N, double ts, const double* params,
+                      const void* x0, int64_t strideX0, const void* U, int64_t strideU,
+                      void* X, void* A, void* B, void* c, void* stream);
+
 /* Batched  y_b = alpha * M_b x_b + beta * y_b,  M_b (rows x cols) row-major. */
 int mpcqp_gemv(int dtype, int batch, int rows, int cols, double alpha,
                const void* M, int64_t strideM, const void* x, int64_t strideX,

@@ -55,6 +55,8 @@ SIGNATURES = {
                             _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i, _d, _vp]),
     "mpcqp_riccati": (_i, [_i, _i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                            _vp, _i64, _vp, _vp, _vp]),
+    "mpcqp_bicycle_rti": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _i64, _vp, _i64,
+                               _vp, _vp, _vp, _vp, _vp]),
     "mpcqp_gemv": (_i, [_i, _i, _i, _i, _d, _vp, _i64, _vp, _i64, _d, _vp, _i64, _vp]),
     "mpcqp_rollout": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
 }

@@ -15,6 +15,8 @@ Shape conventions (batch-outermost, row-major):
 """
 from __future__ import annotations
 
+import ctypes
+
 import math
 
 import torch
@@ -419,6 +421,28 @@ def gemv(M, x, alpha: float = 1.0, beta: float = 0.0, y=None):
                            float(beta), _ptr(y), rows, _stream())
     nat.check(rc, "mpcqp_gemv")
     return y
+
+
+# ------------------------------------------------- bicycle re-linearisation
+def bicycle_rti(x0, U, params, ts: float, *, states: bool = False):
+    """Batched FE rollout + per-stage linearisation of the kinematic bicycle
+    (include/mpcqp.h ``mpcqp_bicycle_rti``).  x0 (b, 4), U (b, N, 2) device
+    tensors; params a VehicleParameters.  Returns A (b,N,4,4), B (b,N,4,2),
+    c (b,N,4) [, X (b,N+1,4) when states]."""
+    dt, dev = x0.dtype, x0.device
+    x0 = x0.contiguous()
+    U = U.contiguous()
+    b, N = int(U.shape[0]), int(U.shape[1])
+    A = torch.empty((b, N, 4, 4), dtype=dt, device=dev)
+    B = torch.empty((b, N, 4, 2), dtype=dt, device=dev)
+    c = torch.empty((b, N, 4), dtype=dt, device=dev)
+    X = torch.empty((b, N + 1, 4), dtype=dt, device=dev) if states else None
+    prm = (ctypes.c_double * 4)(params.axis_front, params.axis_rear, params.acceleration,
+                                params.friction)
+    rc = _lib().mpcqp_bicycle_rti(_code(dt), b, N, float(ts), prm, _ptr(x0), 4, _ptr(U), 2 * N,
+                                  _ptr(X), _ptr(A), _ptr(B), _ptr(c), _stream())
+    nat.check(rc, "mpcqp_bicycle_rti")
+    return (A, B, c, X) if states else (A, B, c)
 
 
 # --------------------------------------------------------------- rollout

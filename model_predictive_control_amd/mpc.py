@@ -7,9 +7,9 @@ IPOPT every closed-loop step (``solve`` main.py:115-116, ``__call__``
 main.py:121-129).  Here each ``solve`` is a real-time-iteration SQP step on
 device:
 
-  1. nominal rollout of the forward-Euler model from x0 with the warm-started
-     input sequence (previous solution shifted one stage),
-  2. per-stage linearisation (A_k, B_k, c_k)  (bicycle.fe_linearize_batched),
+  1.+2. nominal rollout of the forward-Euler model from x0 with the warm-
+     started input sequence (previous solution shifted one stage) and the
+     per-stage linearisation (A_k, B_k, c_k)    (libmpcqp ``mpcqp_bicycle_rti``),
   3. time-varying condensing  -> H, f        (libmpcqp ``mpcqp_condense``, TV),
   4. input-box QP                            (libmpcqp ``mpcqp_solve_box``),
 
@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 from . import batched
-from .bicycle import KinematicBicycle, fe_linearize_batched, fe_step_batched
+from .bicycle import KinematicBicycle
 from .parameters import VehicleParameters
 
 
@@ -86,11 +86,8 @@ class MPCController:
             U = torch.zeros((b, N, nu), dtype=self.dtype, device=self.device)
         z = status = None
         for _ in range(self.sqp_iters):
-            xs = [X0]
-            for k in range(N - 1):
-                xs.append(fe_step_batched(xs[-1], U[:, k], self.params, self.ts))
-            Xn = torch.stack(xs, 1)
-            A, B, c = fe_linearize_batched(Xn, U, self.params, self.ts)
+            # FE rollout from x0 under U + per-stage (A_k, B_k, c_k): one launch
+            A, B, c = batched.bicycle_rti(X0, U, self.params, self.ts)
             if self.state_box:
                 d = batched.condense(A.contiguous(), B.contiguous(), self.Q, self.R, self.QN, N,
                                      x0=X0, c=c.contiguous(), tv=True,
