@@ -558,7 +558,7 @@ class Config5:
                                              "hbm_GBs": round(cb / (t_c * 1e-3) / 1e9, 1)})
         sb = solve_bytes_per_instance(n, 4) * bsz
         r_s = roof("qp_wg_kernel<float,160>", "hbm", sb, t_s, HBM_PEAK_GBS, "GB/s",
-                   traffic.get("solve_box"), {"bytes_per_launch": sb})
+                   traffic.get("solve_qp"), {"bytes_per_launch": sb})
         extra = {"kernel_us": {"condense": round(t_c * 1e3, 2), "solve_box": round(t_s * 1e3, 2)}}
         dom, other = (r_s, r_c) if t_s >= t_c else (r_c, r_s)
         return dom, {"roofline_other": other}, extra
@@ -680,10 +680,13 @@ def main():
 
     out = None
     if rank == 0:
+        # PMC-measured HBM bytes per launch (tools/traffic.sh), committed under
+        # profiles/ per config; --traffic overrides
         traffic = {}
-        if args.traffic:
-            with open(args.traffic) as fh:
-                traffic = json.load(fh)
+        tpath = args.traffic or os.path.join(ROOT, "profiles", f"traffic_cfg{args.config}.json")
+        if os.path.exists(tpath) and (args.traffic or args.batch == C.default_batch):
+            with open(tpath) as fh:
+                traffic = json.load(fh)  # measured at the config's default batch
         err = wl.check()
         dom, others, extra = wl.kernels(traffic)
         cpu = None
