@@ -96,7 +96,6 @@ __global__ __launch_bounds__(64, (MpcOcc<NX, BS>::w)) void mpc_box_kernel(MpcBox
   T* fs = sm + BL::oF;
   T* lbs = sm + BL::oLb;
   T* ubs = sm + BL::oUb;
-  T* zs = sm + BL::oZ;
   T* As = sm + L.oA;
   T* Bs = sm + L.oB;
   T* Qs = sm + L.oQ;
@@ -433,7 +432,7 @@ __global__ __launch_bounds__(64, (MpcOcc<NX, BS>::w)) void mpc_box_kernel(MpcBox
   if (__any(nonfinite)) code = MPCQP_STATUS_NONFINITE;
   else if (__any(badbox)) code = MPCQP_STATUS_INFEASIBLE;
   if (code == MPCQP_STATUS_OPTIMAL)
-    code = gi_box_core<T, BS>(M, buf, fs, lbs, ubs, zs, n, a.max_iter, a.tol, zr, iters);
+    code = gi_box_core<T, BS>(M, buf, fs, lbs, ubs, n, a.max_iter, a.tol, zr, iters);
   if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
 #pragma unroll
     for (int r = 0; r < BS; ++r) zr[r] = __builtin_nan("");

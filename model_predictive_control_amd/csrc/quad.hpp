@@ -194,9 +194,7 @@ struct QBoxLds {
   static constexpr int oF = QSym<T, BS>::BUF;
   static constexpr int oLb = oF + NMAX;
   static constexpr int oUb = oLb + NMAX;
-  static constexpr int oSl = oUb + NMAX;  // 1/(1+|lb|), NaN where lb = -inf
-  static constexpr int oSu = oSl + NMAX;  // 1/(1+|ub|), NaN where ub = +inf
-  static constexpr int size = oSu + NMAX;
+  static constexpr int size = oUb + NMAX;
 };
 
 // Relative-violation scale of a bound: 1/(1+|b|) for a finite bound, NaN for
@@ -207,7 +205,7 @@ __device__ __forceinline__ T bound_scale(T bnd) {
   return finite(bnd) ? T(1) / (T(1) + fabs(bnd)) : __builtin_nan("");
 }
 
-// Goldfarb-Idnani dual active set for the group's box QP (see gi_box_core.hpp
+// Goldfarb-Idnani dual active set for one box QP per group / wave (see gi_box_core.hpp
 // for the method); entry: M = -H^{-1}.  Primal and dual quantities are tracked
 // incrementally along the steps (z_F, the active multipliers, and the
 // multiplier of the bound being added); when every group has settled, one
@@ -219,21 +217,40 @@ __device__ __forceinline__ T bound_scale(T bnd) {
 template <typename T, int BS>
 struct QBounds {
   T lo[BS], hi[BS], sl[BS], su[BS];
-  __device__ __forceinline__ void load(const QSym<T, BS>& M, const T* lbs, const T* ubs) {
-    using L = QBoxLds<T, BS>;
+  template <class Mat>
+  __device__ __forceinline__ void load(const Mat& M, const T* lbs, const T* ubs) {
 #pragma unroll
     for (int r = 0; r < BS; ++r) {
       const int i = M.bi * BS + r;
       lo[r] = lbs[i];
       hi[r] = ubs[i];
-      sl[r] = lbs[i + (L::oSl - L::oLb)];
-      su[r] = lbs[i + (L::oSu - L::oLb)];
+      sl[r] = bound_scale(lo[r]);
+      su[r] = bound_scale(hi[r]);
     }
   }
 };
 
+// Reductions over the rows of one QP, per layout: four QPs per wave (DPP
+// rows of 16 lanes) or one QP per wave (8 row blocks).
 template <typename T, int BS>
-__device__ __forceinline__ void qscan(const QSym<T, BS>& M, const int (&st)[BS], const T (&zr)[BS],
+__device__ __forceinline__ void rows_argmax(const QSym<T, BS>&, T& v, int& idx, T& pay) {
+  group_argmax(v, idx, pay);
+}
+template <typename T, int BS>
+__device__ __forceinline__ void rows_argmin(const QSym<T, BS>&, T& v, int& idx) {
+  group_argmin(v, idx);
+}
+template <typename T, int BS>
+__device__ __forceinline__ void rows_argmax(const Sym2D<T, BS>&, T& v, int& idx, T& pay) {
+  blocks_argmax(v, idx, pay);
+}
+template <typename T, int BS>
+__device__ __forceinline__ void rows_argmin(const Sym2D<T, BS>&, T& v, int& idx) {
+  blocks_argmin(v, idx);
+}
+
+template <typename T, int BS, class Mat>
+__device__ __forceinline__ void qscan(const Mat& M, const int (&st)[BS], const T (&zr)[BS],
                                       const QBounds<T, BS>& B, T& viol, int& pi, T& zv) {
   viol = -Lim<T>::inf();
   pi = 0;
@@ -249,7 +266,7 @@ __device__ __forceinline__ void qscan(const QSym<T, BS>& M, const int (&st)[BS],
     pi = take ? i : pi;
     zv = take ? zr[r] : zv;
   }
-  group_argmax(viol, pi, zv);
+  rows_argmax(M, viol, pi, zv);
 }
 
 #ifdef MPCQP_PHASE_TIMING
@@ -260,8 +277,8 @@ __device__ __forceinline__ void qscan(const QSym<T, BS>& M, const int (&st)[BS],
 #define MPCQP_CLK_ARG
 #endif
 
-template <typename T, int BS>
-__device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, const T* lbs,
+template <typename T, int BS, class Mat>
+__device__ __forceinline__ int gi_box(Mat& M, T* gb, const T* fs, const T* lbs,
                                            const T* ubs, int n, int max_iter, T tol, bool live,
                                            T (&zr)[BS], int& iters MPCQP_CLK_PARAM) {
   QBounds<T, BS> B;
@@ -344,7 +361,7 @@ __device__ __forceinline__ int gi_box_quad(QSym<T, BS>& M, T* gb, const T* fs, c
         ti = take ? t : ti;
         k = take ? (M.bi * BS + r) : k;
       }
-      group_argmin(ti, k);
+      rows_argmin(M, ti, k);
       const bool partial = ti < t2;
       const T s_eff = stepping ? (partial ? ti : t2) : T(0);
 #pragma unroll

@@ -63,8 +63,6 @@ __global__ __launch_bounds__(64, (QuadOcc<T, BS>::w)) void box_quad_kernel(BoxAr
     fs[i] = fi;
     lbs[i] = li;
     ubs[i] = ui;
-    lbs[i + (L::oSl - L::oLb)] = bound_scale(li);
-    lbs[i + (L::oSu - L::oLb)] = bound_scale(ui);
     nonfinite |= v && !finite(fi);
     badbox |= v && (!(li <= ui) || li == Lim<T>::inf() || ui == -Lim<T>::inf());
   }
@@ -87,7 +85,7 @@ __global__ __launch_bounds__(64, (QuadOcc<T, BS>::w)) void box_quad_kernel(BoxAr
   if (code == MPCQP_STATUS_OPTIMAL && !ok) code = MPCQP_STATUS_NOT_CONVEX;
   T zr[BS];
   int iters = 0;
-  const int c2 = gi_box_quad<T, BS>(M, gb, fs, lbs, ubs, n, a.max_iter, a.tol,
+  const int c2 = gi_box<T, BS>(M, gb, fs, lbs, ubs, n, a.max_iter, a.tol,
                                     live && code == MPCQP_STATUS_OPTIMAL, zr, iters MPCQP_CLK_ARG);
   if (code == MPCQP_STATUS_OPTIMAL) code = c2;
   if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
@@ -216,8 +214,6 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
       const T ui = (v && a.ub) ? a.ub[(int64_t)b * a.sub + i] : Lim<T>::inf();
       lbs[i] = li;
       ubs[i] = ui;
-      lbs[i + (BL::oSl - BL::oLb)] = bound_scale(li);
-      lbs[i + (BL::oSu - BL::oLb)] = bound_scale(ui);
       fs[i] = T(0);
       badbox |= v && (!(li <= ui) || li == Lim<T>::inf() || ui == -Lim<T>::inf());
     }
@@ -496,7 +492,7 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
   else if ((__ballot(badbox) & gmask) != 0) code = MPCQP_STATUS_INFEASIBLE;
   T zr[BS];
   int iters = 0;
-  const int c2 = gi_box_quad<T, BS>(M, gb, fs, lbs, ubs, n, a.max_iter, a.tol,
+  const int c2 = gi_box<T, BS>(M, gb, fs, lbs, ubs, n, a.max_iter, a.tol,
                                     live && code == MPCQP_STATUS_OPTIMAL, zr, iters MPCQP_CLK_ARG);
   if (code == MPCQP_STATUS_OPTIMAL) code = c2;
   MPCQP_PHASE(4);

@@ -47,7 +47,6 @@ __global__ __launch_bounds__(64, BoxOcc<BS>::w) void box_gi_kernel(BoxArgs<T> a)
   T* fs = sm + L::oF;
   T* lbs = sm + L::oLb;
   T* ubs = sm + L::oUb;
-  T* zs = sm + L::oZ;
   T* Ps = sm + L::oEnd;  // packed H
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
@@ -91,7 +90,7 @@ __global__ __launch_bounds__(64, BoxOcc<BS>::w) void box_gi_kernel(BoxArgs<T> a)
       }
     }
     if (code == MPCQP_STATUS_OPTIMAL)
-      code = gi_box_core<T, BS>(M, buf, fs, lbs, ubs, zs, n, a.max_iter, a.tol, zr, iters);
+      code = gi_box_core<T, BS>(M, buf, fs, lbs, ubs, n, a.max_iter, a.tol, zr, iters);
   }
   if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
 #pragma unroll

@@ -65,6 +65,30 @@ __device__ __forceinline__ void blocks_argmax(T& v, int& idx) {
   }
 }
 
+// Same with a payload value carried along with the winner.
+template <typename T>
+__device__ __forceinline__ void blocks_argmax(T& v, int& idx, T& pay) {
+  {
+    const T ov = dpp<0x128>(v);
+    const int oi = dpp<0x128>(idx);
+    const T op = dpp<0x128>(pay);
+    const bool take = (ov > v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+    pay = take ? op : pay;
+  }
+#pragma unroll
+  for (int off = 16; off <= 32; off <<= 1) {
+    const T ov = __shfl_xor(v, off, kWave);
+    const int oi = __shfl_xor(idx, off, kWave);
+    const T op = __shfl_xor(pay, off, kWave);
+    const bool take = (ov > v) || (ov == v && oi < idx);
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+    pay = take ? op : pay;
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void blocks_argmin(T& v, int& idx) {
   {
@@ -141,11 +165,11 @@ struct Sym2D {
     return d;
   }
 
-  // Goodnight sweep on pivot k: sigma = +1 moves k into the swept set,
-  // sigma = -1 (reverse sweep) moves it out.  Returns the pivot M_kk.
-  __device__ __forceinline__ T sweep(int k, T sigma, T* buf) {
-    T colr[BS], colc[BS];
-    const T d = column(k, buf, colr, colc);
+  // Goodnight sweep on pivot k with its column fetched (d = M_kk): sigma =
+  // +1 moves k into the swept set, sigma = -1 (reverse sweep) moves it out.
+  // Row/column k are selected, not produced by cancellation.
+  __device__ __forceinline__ void sweep_col(int k, T sigma, T d, const T (&colr)[BS],
+                                            const T (&colc)[BS]) {
     const T rd = fast_rcp(d);
     T ar[BS];
 #pragma unroll
@@ -161,6 +185,13 @@ struct Sym2D {
         m[r][c] = (ik || jk) ? spec : gen;
       }
     }
+  }
+
+  // Fetch column k and sweep on it.  Returns the pivot M_kk.
+  __device__ __forceinline__ T sweep(int k, T sigma, T* buf) {
+    T colr[BS], colc[BS];
+    const T d = column(k, buf, colr, colc);
+    sweep_col(k, sigma, d, colr, colc);
     return d;
   }
 
