@@ -12,10 +12,11 @@ namespace mpcqp {
 
 // Optional phase timing (tools/phase_timing.py builds a separate library
 // with -DMPCQP_PHASE_TIMING): every wave accumulates the s_memtime cycles of
-// each phase in registers (mpcqp_ph_acc[i]) and lane 0 adds them to
-// mpcqp_phase_cycles[] once, at the end of the kernel.
+// each phase in registers and lane 0 adds them to this translation unit's
+// mpcqp_phase_cycles[] once, at the end of the kernel; each instrumented
+// unit exports its own mpcqp_debug_phase_cycles_* reader.
 #ifdef MPCQP_PHASE_TIMING
-extern __device__ unsigned long long mpcqp_phase_cycles[8];
+static __device__ unsigned long long mpcqp_phase_cycles[8];  // one copy per translation unit
 struct PhaseClock {
   unsigned long long t, acc[8];
   __device__ PhaseClock() : t(__builtin_readcyclecounter()) {
@@ -32,7 +33,23 @@ struct PhaseClock {
   }
 };
 #define MPCQP_PHASE(i) mpcqp_clk.mark(i)
+#define MPCQP_DEBUG_PHASE_READER(NAME)                                                        \
+  extern "C" int NAME(unsigned long long* out, int reset) {                                   \
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcqp::mpcqp_phase_cycles),                       \
+                            8 * sizeof(unsigned long long)) != hipSuccess)                    \
+      return -2;                                                                              \
+    if (reset) {                                                                              \
+      unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};                                     \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(mpcqp::mpcqp_phase_cycles), z, sizeof(z)) != hipSuccess) \
+        return -2;                                                                            \
+    }                                                                                         \
+    return 0;                                                                                 \
+  }
+#define MPCQP_CLK_PARAM , PhaseClock& mpcqp_clk
+#define MPCQP_CLK_ARG , mpcqp_clk
 #else
+#define MPCQP_CLK_PARAM
+#define MPCQP_CLK_ARG
 #define MPCQP_PHASE(i) \
   do {                 \
   } while (0)

@@ -269,13 +269,6 @@ __device__ __forceinline__ void qscan(const Mat& M, const int (&st)[BS], const T
   rows_argmax(M, viol, pi, zv);
 }
 
-#ifdef MPCQP_PHASE_TIMING
-#define MPCQP_CLK_PARAM , PhaseClock& mpcqp_clk
-#define MPCQP_CLK_ARG , mpcqp_clk
-#else
-#define MPCQP_CLK_PARAM
-#define MPCQP_CLK_ARG
-#endif
 
 template <typename T, int BS, class Mat>
 __device__ __forceinline__ int gi_box(Mat& M, T* gb, const T* fs, const T* lbs,

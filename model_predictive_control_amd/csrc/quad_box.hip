@@ -588,17 +588,6 @@ template int mpc_box_quad<float>(const MpcArgsQ<float>&, hipStream_t);
 }  // namespace mpcqp
 
 #ifdef MPCQP_PHASE_TIMING
-namespace mpcqp {
-__device__ unsigned long long mpcqp_phase_cycles[8];
-}
 // Debug library only: read (and optionally reset) the phase counters.
-extern "C" int mpcqp_debug_phase_cycles(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcqp::mpcqp_phase_cycles), 8 * sizeof(unsigned long long)) != hipSuccess)
-    return -2;
-  if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(mpcqp::mpcqp_phase_cycles), z, sizeof(z)) != hipSuccess) return -2;
-  }
-  return 0;
-}
+MPCQP_DEBUG_PHASE_READER(mpcqp_debug_phase_cycles)
 #endif

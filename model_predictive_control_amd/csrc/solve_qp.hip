@@ -31,6 +31,14 @@ struct QpArgs {
   T tol;
 };
 
+// Pivots per barrier in the initial sweep-in: the replicas cost BK*(BR+BC)
+// registers, so large blocks (and fp64) use pairs.
+template <typename T, class S>
+struct QpBlock {
+  static constexpr int e = S::BR * S::BC * (int)(sizeof(T) / 4);  // block VGPRs
+  static constexpr int bk = e <= 32 ? 4 : (e <= 64 ? 2 : 1);
+};
+
 // Two waves per SIMD: a 512-thread workgroup fits once per CU, a 256-thread
 // one twice (VGPR budget 256).
 template <typename T, class S>
@@ -49,6 +57,9 @@ void qp_wg_kernel(QpArgs<T> a) {
   const int n = a.n, m = a.m, nt = n + m;
   const T inf = Lim<T>::inf();
 
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
   int bad = 0, nonfin = 0;
   for (int i = tid; i < NMAX; i += S::threads) {
     T l = -inf, u = inf, fi = T(0);
@@ -90,6 +101,7 @@ void qp_wg_kernel(QpArgs<T> a) {
       if (c == BC - 1) asm volatile("" ::: "memory");  // one row of loads in flight
     }
   const int flags = __syncthreads_or((bad ? 1 : 0) | (nonfin ? 2 : 0));
+  MPCQP_PHASE(0);
   int code = MPCQP_STATUS_OPTIMAL;
   int iters = 0;
   T val[BR], lam[BR];
@@ -103,8 +115,22 @@ void qp_wg_kernel(QpArgs<T> a) {
   } else if (flags & 1) {
     code = MPCQP_STATUS_INFEASIBLE;
   } else {
-    // sweep every z in: M = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']]
-    for (int k = 0; k < n; ++k) {
+    // sweep every z in: M = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']] --
+    // BK pivots per publish/barrier (sweep_blk), the remainder one by one
+    constexpr int BK = QpBlock<T, S>::bk;
+    int k = 0;
+    for (int blk = 0; BK > 1 && k + BK <= n; k += BK, ++blk) {
+      T* cb = sm + L::oBlk + (blk & 1) * 8 * NMAX;
+      T* rb = cb + 4 * NMAX;
+#pragma unroll
+      for (int t = 0; t < BK; ++t) M.put_col(k + t, cb + t * NMAX, rb + t * NMAX);
+      __syncthreads();
+      if (!M.template sweep_blk<BK>(k, T(1), true, cb, rb)) {
+        code = MPCQP_STATUS_NOT_CONVEX;
+        break;
+      }
+    }
+    for (; code == MPCQP_STATUS_OPTIMAL && k < n; ++k) {
       T* cbuf = sm + ((k & 1) ? L::oCol1 : L::oCol0);
       T* rbuf = sm + ((k & 1) ? L::oRow1 : L::oRow0);
       M.put_col(k, cbuf, rbuf);
@@ -116,6 +142,7 @@ void qp_wg_kernel(QpArgs<T> a) {
       }
       M.sweep_buf(k, T(1), d, cbuf, rbuf);
     }
+    MPCQP_PHASE(1);
     if (code == MPCQP_STATUS_OPTIMAL) {
       M.diag_abs(sm + L::oScale);
       __syncthreads();
@@ -131,7 +158,7 @@ void qp_wg_kernel(QpArgs<T> a) {
         return T(0);
       };
       code = gi_mixed<T, S>(M, sm, n, nt, a.max_iter, a.tol, dep_tol, val, lam, iters, kel,
-                            a.refine);
+                            a.refine MPCQP_CLK_ARG);
     }
   }
   const bool ok = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
@@ -144,6 +171,9 @@ void qp_wg_kernel(QpArgs<T> a) {
     }
   }
   if (tid == 0) a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
+#ifdef MPCQP_PHASE_TIMING
+  mpcqp_clk.flush();
+#endif
 }
 
 template <typename T, class S>
@@ -241,3 +271,7 @@ extern "C" int mpcqp_solve_qp(int dtype, int batch, int n, int m, const void* H,
   return solve_qp_t<float>(batch, n, m, H, strideH, f, stridef, G, strideG, hl, hu, strideh, lb,
                            strideLb, ub, strideUb, z, y, status, max_iter, tol, st);
 }
+
+#ifdef MPCQP_PHASE_TIMING
+MPCQP_DEBUG_PHASE_READER(mpcqp_debug_phase_cycles_qp)
+#endif

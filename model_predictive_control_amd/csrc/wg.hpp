@@ -201,6 +201,84 @@ struct WSym {
     }
   }
 
+  // BK consecutive sweeps (pivots k0..k0+BK-1, sigma) from ONE publish of
+  // their columns (cb[t*NMAX + i] = M[i][k0+t]) and rows (rb[t*NMAX + j] =
+  // M[k0+t][j]).  Every thread replays the four sweeps on its block and on
+  // local replicas of the fetched columns/rows and of the BK x BK pivot
+  // block, with exactly the formulas of sweep_col, so every replica stays
+  // bitwise equal to the register it mirrors; one barrier instead of BK.  Returns
+  // false (uniformly) if a pivot fails the sign test (want > 0 when
+  // positive, < 0 otherwise); the matrix is then left mid-block.
+  template <int BK>
+  __device__ __forceinline__ bool sweep_blk(int k0, T sigma, bool positive, const T* cb,
+                                            const T* rb) {
+    k0 = uniform(k0);
+    T cr[BK][BR], cc[BK][BC], P[BK][BK];
+#pragma unroll
+    for (int t = 0; t < BK; ++t) {
+#pragma unroll
+      for (int r = 0; r < BR; ++r) cr[t][r] = cb[t * NMAX + bi * BR + r];
+#pragma unroll
+      for (int c = 0; c < BC; ++c) cc[t][c] = rb[t * NMAX + bj * BC + c];
+#pragma unroll
+      for (int q = 0; q < BK; ++q) P[q][t] = cb[t * NMAX + k0 + q];
+    }
+#pragma unroll
+    for (int t = 0; t < BK; ++t) {
+      const int k = k0 + t;
+      const T d = P[t][t];
+      if (positive ? !(d > T(0)) : !(d < T(0))) return false;
+      const T rd = fast_rcp(d);
+      const int kbc = k / BC, kbr = k / BR;
+      const int kc = uniform(k - kbc * BC), kr = uniform(k - kbr * BR);
+      // the register block (sweep_col)
+      T a[BR], ik[BR], srow[BC];
+#pragma unroll
+      for (int r = 0; r < BR; ++r) {
+        const bool isk = (bi == kbr) && (r == kr);
+        a[r] = isk ? T(1) : cr[t][r] * rd;
+        ik[r] = isk ? T(1) : T(0);
+      }
+#pragma unroll
+      for (int c = 0; c < BC; ++c) srow[c] = (bj * BC + c == k) ? -rd : sigma * cc[t][c] * rd;
+#pragma unroll
+      for (int r = 0; r < BR; ++r)
+#pragma unroll
+        for (int c = 0; c < BC; ++c) m[r][c] = fma(ik[r], srow[c], fma(-a[r], cc[t][c], m[r][c]));
+      if (__any(bj == kbc)) {
+        const bool own = bj == kbc;
+#pragma unroll
+        for (int r = 0; r < BR; ++r) {
+          const T sc = (bi * BR + r == k) ? -rd : sigma * cr[t][r] * rd;
+#pragma unroll
+          for (int c = 0; c < BC; ++c) m[r][c] = (own && c == kc) ? sc : m[r][c];
+        }
+      }
+      // replicas of the later columns (my rows) and rows (my columns)
+#pragma unroll
+      for (int u = t + 1; u < BK; ++u) {
+        const T pku = P[t][u], puk = P[u][t];  // M[k][k_u], M[k_u][k] before this sweep
+#pragma unroll
+        for (int r = 0; r < BR; ++r) {
+          const bool isk = (bi == kbr) && (r == kr);
+          cr[u][r] = isk ? sigma * pku * rd : fma(-(cr[t][r] * rd), pku, cr[u][r]);
+        }
+#pragma unroll
+        for (int c = 0; c < BC; ++c) {
+          const bool jk = bj * BC + c == k;
+          cc[u][c] = jk ? sigma * puk * rd : fma(-(puk * rd), cc[t][c], cc[u][c]);
+        }
+      }
+      // the pivot block, in place: entries off row/column t first (they read
+      // row/column t), then row/column t; only the part later steps use
+#pragma unroll
+      for (int x = t + 1; x < BK; ++x)
+#pragma unroll
+        for (int y = t + 1; y < BK; ++y) P[x][y] = fma(-(P[x][t] * rd), P[t][y], P[x][y]);
+    }
+    return true;
+  }
+
   // Same, reading column/row k from their LDS buffers (short live ranges).
   __device__ __forceinline__ void sweep_buf(int k, T sigma, T d, const T* cbuf, const T* rbuf) {
     T colr[BR], colc[BC];
@@ -288,7 +366,8 @@ struct WLds {
   static constexpr int oCol1 = oCol0 + NMAX;
   static constexpr int oRow0 = oCol1 + NMAX;
   static constexpr int oRow1 = oRow0 + NMAX;
-  static constexpr int oW = oRow1 + NMAX;
+  static constexpr int oBlk = oRow1 + NMAX;  // 2 x (4 columns + 4 rows) for sweep4
+  static constexpr int oW = oBlk + 16 * NMAX;
   static constexpr int oLo = oW + NMAX;
   static constexpr int oHi = oLo + NMAX;
   static constexpr int oF = oHi + NMAX;
@@ -311,7 +390,7 @@ struct WLds {
 template <typename T, class S, class KEl>
 __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, int max_iter,
                                         T tol, T dep_tol, T (&val)[S::BR], T (&lam)[S::BR],
-                                        int& iters, KEl&& kel, int refine) {
+                                        int& iters, KEl&& kel, int refine MPCQP_CLK_PARAM) {
   constexpr int BS = S::BR;  // row-block length
   using L = WLds<T, S>;
   T* lo = sm + L::oLo;
@@ -494,6 +573,7 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
     }
   }
   if (active) code = MPCQP_STATUS_MAXITER;
+  MPCQP_PHASE(2);
   for (int it = 0; it < refine; ++it) {
     T x[BS];
 #pragma unroll
@@ -531,6 +611,7 @@ __device__ __forceinline__ int gi_mixed(WSym<T, S>& M, T* sm, int nz, int nt, in
     }
   }
 out:
+  MPCQP_PHASE(3);
 #pragma unroll
   for (int r = 0; r < BS; ++r) {
     const int i = M.bi * BS + r;

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CS = os.path.join(ROOT, "model_predictive_control_amd", "csrc")
 LIB = os.path.join(ROOT, "model_predictive_control_amd", "lib", "libmpcqp_timing.so")
 SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.hip", "quad_box.hip",
-        "solve_qp.hip", "misc.hip"]
+        "solve_qp.hip", "bicycle.hip", "misc.hip"]
 PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/recheck", "GI: scan+argmax", "GI: pivot col+ratio", "GI: sweep"]
 
 if "--build" in sys.argv:
@@ -32,7 +32,9 @@ import bench  # noqa: E402
 from model_predictive_control_amd import _native, batched  # noqa: E402
 
 lib = _native.load()
-lib.mpcqp_debug_phase_cycles.argtypes = [ctypes.c_void_p, ctypes.c_int]
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+reader = lib.mpcqp_debug_phase_cycles if cfg == 2 else lib.mpcqp_debug_phase_cycles_qp
+reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = (ctypes.c_ulonglong * 8)()
 
 
@@ -40,17 +42,29 @@ class A:
     pass
 
 
-a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1; a.mode = "fused"
-w = bench.Config2(a, torch.device("cuda"), 0)
-w._fused(0)
-torch.cuda.synchronize()
-lib.mpcqp_debug_phase_cycles(buf, 1)
 R = 10
-for _ in range(R):
-    w._fused(0)
+if cfg == 2:
+    a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1; a.mode = "fused"
+    w = bench.Config2(a, torch.device("cuda"), 0)
+    run = lambda: w._fused(0)  # noqa: E731
+    waves = (a.batch + 3) // 4 * R
+else:
+    # qp_wg_kernel of config 3 / 5 (phases 0..3: K load, z sweep-in, GI, refinement)
+    PHASES = ["load K", "sweep-in z", "active set", "refinement", "", "", "", ""]
+    a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1
+    w = bench.CONFIGS[cfg](a, torch.device("cuda"), 0)
+    w._condense(0)
+    run = lambda: w._solve(0)  # noqa: E731
+    waves = a.batch * 8 * R  # 512-thread workgroups
+run()
 torch.cuda.synchronize()
-lib.mpcqp_debug_phase_cycles(buf, 1)
-waves = (a.batch + 3) // 4 * R
+reader(buf, 1)
+for _ in range(R):
+    run()
+torch.cuda.synchronize()
+reader(buf, 1)
 tot = sum(buf[i] for i in range(8))
 for i, name in enumerate(PHASES):
+    if not name:
+        continue
     print(f"{name:16s} {buf[i] / waves:10.0f} cycles/wave  {100 * buf[i] / tot:5.1f} %")
