@@ -25,6 +25,8 @@
 // recursion with the xbar recursion on other lanes of the same phases.
 #include "common.hpp"
 
+#include <cstdlib>
+
 // Recursions redundantly in every lane's registers up to this nx; wider
 // states (already nx = 4) use the LDS-parallel recursion, one entry per lane.
 #ifndef MPCQP_CONDENSE_REG_NX
@@ -387,6 +389,393 @@ static int launch_condense(const CondenseArgs<T>& a, hipStream_t st) {
   return MPCQP_OK;
 }
 
+// ===================================================================== MFMA path
+// condense_mfma_kernel (fp32, 5 <= nx <= 15): the same recursions as
+// condense_kernel, on v_mfma_f32_16x16x4_f32 with the state padded to 16 and
+// slot 15 carrying the affine part (augmented state x~ = [x; 1]):
+//     A~_k = [[A_k, c_k], [0, 1]],  Q~ = diag(Q, 0),  B~_k = [B_k; 0]
+//     W~_N = Qf~,  W~_k = Q~ + A~_k' W~_{k+1} A~_k = [[W_k, eta_k], [eta_k', *]]
+//     What_k = B~_k' W~_{k+1}                      (nu x 16, kept in LDS)
+// so that the forward sweep over Gamma~_{k+1} = A~_k Gamma~_k (+ B_k in block
+// k) and E_{k+1} = A~_k E_k, E_0 = [[I, x0], [0, 1]] (E = [Phi, xbar]) yields
+//     H row block k   = What_k Gamma~_{k+1}   (+ R on the diagonal block)
+//     [F | f] block k = What_k E_{k+1}        (column 15: f = B_k'(W x + eta) = B_k' y)
+// i.e. f, F, Phi and xbar come out of one extra 16-column tile, drift
+// included, with no separate adjoint chain.
+//
+// Layout: one instance per wavefront.  Every 16 x 16 operand is an MFMA tile;
+// C/D tiles (lane (g, c): rows 4g..4g+3 of column c) are turned into B
+// operands (lane (g, c): rows g, 4+g, 8+g, 12+g of column c) by a 4 x 4
+// (lane group x register) transpose of two permlane32 + two permlane16
+// swaps -- no LDS round trip on the recursion.  The Gamma block row lives in
+// registers as NT B-operand tiles.  The What_k Gamma~ product (nu <= 16
+// rows) runs on the VALU from the C tile: 16 FMAs per 4 output rows plus the
+// same transpose as a cross-group reduction, which leaves output row g of
+// column c in lane (g, c), so each H row segment is one 64-lane store.
+typedef float mf4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void xpose4(float (&v)[4]) {
+  // lane group g, register r  ->  lane group r, register g
+  auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0]), __float_as_uint(v[2]), false, false);
+  auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[1]), __float_as_uint(v[3]), false, false);
+  auto t0 = __builtin_amdgcn_permlane16_swap(s0[0], s1[0], false, false);
+  auto t1 = __builtin_amdgcn_permlane16_swap(s0[1], s1[1], false, false);
+  v[0] = __uint_as_float(t0[0]);
+  v[1] = __uint_as_float(t0[1]);
+  v[2] = __uint_as_float(t1[0]);
+  v[3] = __uint_as_float(t1[1]);
+}
+
+__device__ __forceinline__ mf4 mfma4(const float (&a)[4], const float (&b)[4], mf4 acc) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+  return acc;
+}
+
+// Buffer descriptors (raw, stride 0, range-checked): every per-lane memory
+// access is base (SGPR) + 32-bit byte offset, and a masked-out lane uses an
+// offset past num_records -- its load returns 0 and its store is dropped, so
+// the loads and stores carry no exec-mask branches and no selects.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr int kOOB = 0x7ffffff0;
+__device__ __forceinline__ rsrc_t mk_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bld(rsrc_t r, int off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void bst(float v, rsrc_t r, int off) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+
+// NT: Gamma tiles (n <= 16 NT); NU4: What rows held per lane (nu <= NU4);
+// DRIFT: per-stage c_k present (its loads get their own queue)
+template <int NT, int NU4, bool DRIFT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+void condense_mfma_kernel(CondenseArgs<float> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  float* wh = reinterpret_cast<float*>(smem_raw);  // What_k: N x NU4 x 16
+  float* Rs = wh + a.N * NU4 * 16;                 // R: nu x nu
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
+  const int b = blockIdx.x;
+  const int l = threadIdx.x, g = l >> 4, cl = l & 15;
+  const int nx = a.nx, nu = a.nu, N = a.N, n = N * nu;
+  const int64_t sa = a.tv ? (int64_t)nx * nx : 0, sbk = a.tv ? (int64_t)nx * nu : 0;
+  const float* Ab = a.A + (int64_t)b * a.sA;
+  const float* Bb = a.B + (int64_t)b * a.sB;
+  const float* Cb = DRIFT ? a.c + (int64_t)b * a.sC : nullptr;
+  {
+    const float* Rb = a.R + (int64_t)b * a.sR;
+    for (int e = l; e < nu * nu; e += kWave) Rs[e] = Rb[e];
+  }
+  // Operand loads run PF stages ahead through a register queue (shifted by
+  // one slot per stage): one stage of the serial chain is a few hundred
+  // cycles, an HBM miss several thousand.
+  constexpr int PF = 4;
+  // A~[p][q] = A[p][q] (p,q < nx) | c[p] (q = 15) | 1 (p = q = 15) | 0: the A and
+  // c loads return 0 outside their masks, so A~ = rawA + rawC + one.
+  int oAb[4], oCb[4], oBb[4], oAf[4], oCf[4];
+  float one_b[4], one_f[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int p = 4 * s + g;  // backward: row p, column cl (B operand of A~, A operand of B~')
+    oAb[s] = (p < nx && cl < nx) ? 4 * (p * nx + cl) : kOOB;
+    oCb[s] = (p < nx && cl == 15) ? 4 * p : kOOB;
+    oBb[s] = (p < nx && cl < nu) ? 4 * (p * nu + cl) : kOOB;
+    one_b[s] = (p == 15 && cl == 15) ? 1.f : 0.f;
+    oAf[s] = (cl < nx && p < nx) ? 4 * (cl * nx + p) : kOOB;  // forward: row cl, column p
+    oCf[s] = (cl < nx && p == 15) ? 4 * cl : kOOB;
+    one_f[s] = (cl == 15 && p == 15) ? 1.f : 0.f;
+  }
+  auto stage_rsrc = [&](int k, rsrc_t& ra, rsrc_t& rb, rsrc_t& rc) {
+    ra = mk_rsrc(Ab + k * sa, (int64_t)nx * nx * 4);
+    rb = mk_rsrc(Bb + k * sbk, (int64_t)nx * nu * 4);
+    rc = mk_rsrc(Cb ? Cb + (int64_t)k * nx : Ab, Cb ? (int64_t)nx * 4 : 0);
+  };
+
+  // ------------------------------------------------ backward: W~, What
+  float wB[4], qC[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int p = 4 * s + g;
+    wB[s] = (p < nx && cl < nx) ? a.Qf[(int64_t)b * a.sQf + p * nx + cl] : 0.f;  // symmetric
+    const int pc = 4 * g + s;
+    qC[s] = (pc < nx && cl < nx) ? a.Q[(int64_t)b * a.sQ + pc * nx + cl] : 0.f;
+  }
+  auto load_bw = [&](int k, float (&ao)[4], float (&co)[4], float (&bo)[4]) {
+    (void)co;
+    rsrc_t ra, rb, rc;
+    stage_rsrc(k, ra, rb, rc);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ao[s] = bld(ra, oAb[s]);
+      if constexpr (DRIFT) co[s] = bld(rc, oCb[s]);
+      bo[s] = bld(rb, oBb[s]);
+    }
+  };
+  // stage body: consume slot (loaded PF stages earlier), refill it with
+  // stage k - PF, run the stage.  The loop is unrolled by PF so every slot
+  // is a fixed register set (moving a slot would wait on its load).
+  auto bw_stage = [&](int k, float (&sa_)[4], float (&sc_)[4], float (&sb_)[4]) {
+    float aT[4], bT[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      aT[s] = sa_[s] + one_b[s];
+      if constexpr (DRIFT) aT[s] += sc_[s];
+      bT[s] = sb_[s];
+    }
+    // unconditional refill (clamped stage): no phi ever touches a slot
+    load_bw(k - PF >= 0 ? (k - PF < N ? k - PF : N - 1) : 0, sa_, sc_, sb_);
+    if (k >= N) return;  // alignment padding
+    // What_k = B~_k' W~_{k+1}: rows 4g+j < nu of lane (g, cl)
+    const mf4 w = mfma4(bT, wB, mf4{0.f, 0.f, 0.f, 0.f});
+    if (k >= 1) {
+      const mf4 x = mfma4(wB, aT, mf4{0.f, 0.f, 0.f, 0.f});  // X = W~ A~
+      float xv[4] = {x[0], x[1], x[2], x[3]};
+      xpose4(xv);
+      const mf4 w2 = mfma4(aT, xv, mf4{qC[0], qC[1], qC[2], qC[3]});  // Q~ + A~' X
+#pragma unroll
+      for (int s = 0; s < 4; ++s) wB[s] = w2[s];
+      xpose4(wB);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * g + j;
+      if (i < NU4) wh[(k * NU4 + i) * 16 + cl] = (i < nu) ? w[j] : 0.f;
+    }
+  };
+  float qa[PF][4], qb[PF][4], qc[PF][4];
+  // stages kt = N-1+pad .. 0 with pad so that the count is a multiple of PF
+  const int ktop = N - 1 + (PF - N % PF) % PF;
+#pragma unroll
+  for (int d = 0; d < PF; ++d) {
+    const int k = ktop - d;
+    load_bw(k < N ? (k >= 0 ? k : 0) : N - 1, qa[d], qc[d], qb[d]);
+  }
+  for (int k0 = ktop; k0 >= 0; k0 -= PF) {
+#pragma unroll
+    for (int d = 0; d < PF; ++d) bw_stage(k0 - d, qa[d], qc[d], qb[d]);
+  }
+  __syncthreads();
+  MPCQP_PHASE(0);
+
+  // ------------------------------------------------ forward: Gamma~, E
+  const bool wantE = a.f || a.F || a.Phi || a.xbar;
+  const bool wantFf = a.f || a.F;
+  const rsrc_t rH = mk_rsrc(a.H + (int64_t)b * ((int64_t)n * (n + 1) / 2), (int64_t)n * (n + 1) / 2 * 4);
+  const rsrc_t rG = mk_rsrc(a.Gam ? a.Gam + (int64_t)b * ((int64_t)N * nx * n) : a.H,
+                            a.Gam ? (int64_t)N * nx * n * 4 : 0);
+  const rsrc_t rF = mk_rsrc(a.F ? a.F + (int64_t)b * n * nx : a.H, a.F ? (int64_t)n * nx * 4 : 0);
+  const rsrc_t rf = mk_rsrc(a.f ? a.f + (int64_t)b * n : a.H, a.f ? (int64_t)n * 4 : 0);
+  const rsrc_t rP = mk_rsrc(a.Phi ? a.Phi + (int64_t)b * N * nx * nx : a.H, a.Phi ? (int64_t)N * nx * nx * 4 : 0);
+  const rsrc_t rX = mk_rsrc(a.xbar ? a.xbar + (int64_t)b * N * nx : a.H, a.xbar ? (int64_t)N * nx * 4 : 0);
+  float gB[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) gB[t][s] = 0.f;
+  float eB[4];
+  {
+    const float* X0b = a.x0 ? a.x0 + (int64_t)b * a.sX0 : nullptr;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int p = 4 * s + g;
+      float v = 0.f;
+      if (p < nx && cl < nx) v = (p == cl) ? 1.f : 0.f;
+      else if (cl == 15) v = (p < nx) ? (X0b ? X0b[p] : 0.f) : (p == 15 ? 1.f : 0.f);
+      eB[s] = v;
+    }
+  }
+  // A~_r as A operand (lane: row cl, column 4s+g); B_r rows 4g+j at this
+  // lane's column of block r
+  auto load_fw = [&](int r, float (&ao)[4], float (&co)[4], float (&bo)[4]) {
+    (void)co;
+    rsrc_t ra, rb, rc;
+    stage_rsrc(r, ra, rb, rc);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ao[s] = bld(ra, oAf[s]);
+      if constexpr (DRIFT) co[s] = bld(rc, oCf[s]);
+    }
+    const int q = (cl - r * nu) & 15;  // this lane's column offset in block r (mod 16)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = 4 * g + j;
+      bo[j] = bld(rb, (p < nx && q < nu) ? 4 * (p * nu + q) : kOOB);
+    }
+  };
+  constexpr int PFF = 2;  // forward prefetch depth (the stage body is large)
+  auto fw_stage = [&](int r, float (&sa_)[4], float (&sc_)[4], float (&sb_)[4]) {
+    float aA[4], bI[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      aA[s] = sa_[s] + one_f[s];
+      if constexpr (DRIFT) aA[s] += sc_[s];
+      bI[s] = sb_[s];
+    }
+    load_fw(r + PFF < N ? r + PFF : N - 1, sa_, sc_, sb_);
+    if (r >= N) return;  // alignment padding
+    float wv[NU4][4];
+#pragma unroll
+    for (int i = 0; i < NU4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wv[i][j] = wh[(r * NU4 + i) * 16 + 4 * g + j];
+    const int blk0 = r * nu;
+    const int ntact = ((r + 1) * nu + 15) >> 4;
+    MPCQP_PHASE(1);
+    // all MFMA chains first (independent tiles overlap in the matrix pipe),
+    // then the VALU epilogue per tile
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (t < ntact) {
+        const mf4 dd = mfma4(aA, gB[t], mf4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int s = 0; s < 4; ++s) gB[t][s] = dd[s];
+      }
+    }
+    float eC[4];
+    if (wantE) {
+      const mf4 dd = mfma4(aA, eB, mf4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int s = 0; s < 4; ++s) eC[s] = dd[s];
+    }
+#ifdef MPCQP_PHASE_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7\n v_mov_b32 %0, %0" : "+v"(gB[0][0]));
+#endif
+    MPCQP_PHASE(2);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = 16 * t + cl;
+      if (t < ntact) {
+        float(&d)[4] = gB[t];  // Gamma~_{r+1} tile, C layout
+        const bool inblk = col >= blk0 && col < blk0 + nu;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = inblk ? bI[j] : d[j];
+        if (a.Gam) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int p = 4 * g + j;
+            bst(d[j], rG, (p < nx && col < n) ? 4 * ((r * nx + p) * n + col) : kOOB);
+          }
+        }
+#pragma unroll
+        for (int ic = 0; ic < NU4 / 4; ++ic) {
+          float P[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float acc = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc = fmaf(wv[4 * ic + i][j], d[j], acc);
+            P[i] = acc;
+          }
+          xpose4(P);
+          float h = (P[0] + P[1]) + (P[2] + P[3]);
+          const int i = 4 * ic + g;
+          const int R = blk0 + i;
+          const bool st = i < nu && col <= R;
+          if (inblk && i < nu) h += Rs[i * nu + (col - blk0)];
+          bst(h, rH, st ? 4 * (R * (R + 1) / 2 + col) : kOOB);
+        }
+        xpose4(d);  // B layout for the next stage
+      } else if (a.Gam && 16 * t < n) {  // structural zeros of the block row
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int p = 4 * g + j;
+          bst(0.f, rG, (p < nx && col < n) ? 4 * ((r * nx + p) * n + col) : kOOB);
+        }
+      }
+    }
+    MPCQP_PHASE(3);
+    if (wantE) {
+      float(&d)[4] = eC;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = 4 * g + j;
+        if (a.xbar) bst(d[j], rX, (p < nx && cl == 15) ? 4 * (r * nx + p) : kOOB);
+        if (a.Phi) bst(d[j], rP, (p < nx && cl < nx) ? 4 * ((r * nx + p) * nx + cl) : kOOB);
+      }
+      if (wantFf) {
+#pragma unroll
+        for (int ic = 0; ic < NU4 / 4; ++ic) {
+          float P[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float acc = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc = fmaf(wv[4 * ic + i][j], d[j], acc);
+            P[i] = acc;
+          }
+          xpose4(P);
+          const float h = (P[0] + P[1]) + (P[2] + P[3]);
+          const int i = 4 * ic + g;
+          const int R = blk0 + i;
+          if (a.F) bst(h, rF, (i < nu && cl < nx) ? 4 * (R * nx + cl) : kOOB);
+          if (a.f) bst(h, rf, (i < nu && cl == 15) ? 4 * R : kOOB);
+        }
+      }
+      xpose4(d);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) eB[s] = d[s];
+    }
+    MPCQP_PHASE(4);
+  };
+#pragma unroll
+  for (int d = 0; d < PFF; ++d) load_fw(d < N ? d : N - 1, qa[d], qc[d], qb[d]);
+  for (int r0 = 0; r0 < N; r0 += PFF) {
+#pragma unroll
+    for (int d = 0; d < PFF; ++d) fw_stage(r0 + d, qa[d], qc[d], qb[d]);
+  }
+#ifdef MPCQP_PHASE_TIMING
+  mpcqp_clk.flush();
+#endif
+}
+
+template <int NT, int NU4, bool DRIFT>
+static int launch_condense_mfma3(const CondenseArgs<float>& a, hipStream_t st) {
+  const size_t bytes = ((size_t)a.N * NU4 * 16 + (size_t)a.nu * a.nu) * sizeof(float);
+  if (bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)condense_mfma_kernel<NT, NU4, DRIFT>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(condense_mfma)");
+  }
+  hipLaunchKernelGGL((condense_mfma_kernel<NT, NU4, DRIFT>), dim3(a.batch), dim3(kWave), bytes, st, a);
+  MPCQP_CHECK_LAUNCH("condense_mfma_kernel");
+  return MPCQP_OK;
+}
+template <int NT, int NU4>
+static int launch_condense_mfma(const CondenseArgs<float>& a, hipStream_t st) {
+  return a.c ? launch_condense_mfma3<NT, NU4, true>(a, st) : launch_condense_mfma3<NT, NU4, false>(a, st);
+}
+
+// fp32 with 5 <= nx <= 15 and N*nu <= 256 (MPCQP_CONDENSE_MFMA=0 forces the
+// wavefront kernel, for A/B checks).  Returns 1 if not applicable.
+static int condense_mfma(const CondenseArgs<float>& a, hipStream_t st) {
+  static const int enabled = [] {
+    const char* e = getenv("MPCQP_CONDENSE_MFMA");
+    return e ? atoi(e) : 1;
+  }();
+  const int n = a.N * a.nu;
+  if (!enabled || a.nx < 5 || a.nx > 15 || a.nu > 16 || n > 256 ||
+      (size_t)a.N * 16 * 16 * sizeof(float) > 160 * 1024)
+    return 1;
+  const int nt = (n + 15) / 16;
+  if (a.nu <= 4) {
+    if (nt <= 4) return launch_condense_mfma<4, 4>(a, st);
+    if (nt <= 8) return launch_condense_mfma<8, 4>(a, st);
+    if (nt <= 10) return launch_condense_mfma<10, 4>(a, st);
+    if (nt <= 12) return launch_condense_mfma<12, 4>(a, st);
+    return launch_condense_mfma<16, 4>(a, st);
+  }
+  if (a.nu <= 8) {
+    if (nt <= 8) return launch_condense_mfma<8, 8>(a, st);
+    return launch_condense_mfma<16, 8>(a, st);
+  }
+  return launch_condense_mfma<16, 16>(a, st);
+}
+
 template <typename T>
 static int condense_t(int batch, int nx, int nu, int N, int flags, const void* A, int64_t sA,
                       const void* Bm, int64_t sB, const void* Q, int64_t sQ, const void* R,
@@ -400,6 +789,10 @@ static int condense_t(int batch, int nx, int nu, int N, int flags, const void* A
   a.Qf = (const T*)Qf; a.sQf = sQf; a.c = (const T*)c; a.sC = sC;
   a.x0 = (const T*)x0; a.sX0 = sX0;
   a.H = (T*)H; a.F = (T*)F; a.f = (T*)f; a.Gam = (T*)Gam; a.Phi = (T*)Phi; a.xbar = (T*)xbar;
+  if constexpr (sizeof(T) == 4) {
+    const int rc = condense_mfma(a, st);
+    if (rc != 1) return rc;
+  }
   if (nx <= 2) return launch_condense<T, 2>(a, st);
   if (nx <= 4) return launch_condense<T, 4>(a, st);
   if (nx <= 8) return launch_condense<T, 8>(a, st);
@@ -435,3 +828,7 @@ extern "C" int mpcqp_condense(int dtype, int batch, int nx, int nu, int N, int f
                            strideR, Qf, strideQf, c, strideC, x0, strideX0, H, F, f, Gam, Phi,
                            xbar, st);
 }
+
+#ifdef MPCQP_PHASE_TIMING
+MPCQP_DEBUG_PHASE_READER(mpcqp_debug_phase_cycles_condense)
+#endif

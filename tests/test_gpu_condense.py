@@ -132,3 +132,28 @@ def test_condense_large_batch_pointwise(dev):
     for b in (0, 1, 777, 4095):
         ref = oc.condense(A, B, Q, R, Pf, N, x0=X0[b])
         assert np.abs(out["f"][b].cpu().numpy() - ref["f"]).max() < 1e-10 * max(1, np.abs(ref["f"]).max())
+
+
+@pytest.mark.parametrize("nx,nu,N,tv", [(5, 3, 6, True), (8, 2, 10, True), (12, 4, 40, True),
+                                        (15, 1, 9, True), (12, 6, 20, True), (6, 12, 10, True),
+                                        (12, 4, 40, False), (7, 16, 16, True)])
+def test_condense_fp32_mfma_all_outputs(dev, nx, nu, N, tv):
+    """fp32 with 5 <= nx <= 15 runs condense_mfma_kernel (augmented-state
+    MFMA recursion): every output, per-stage drift c_k, vs the fp64 oracle."""
+    rng = np.random.default_rng(31 + 7 * nx + nu + N)
+    batch = 3
+    A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, tv, batch)
+    A *= 0.8
+    x0 = rng.normal(size=(batch, nx))
+    c = rng.normal(size=(batch, N, nx)) * 0.3 if tv else None
+    f32 = torch.float32
+    out = batched.condense(_t(A, dev, f32), _t(B, dev, f32), _t(Q, dev, f32), _t(R, dev, f32),
+                           _t(Qf, dev, f32), N, x0=_t(x0, dev, f32),
+                           c=None if c is None else _t(c, dev, f32), tv=tv,
+                           outputs=("H", "F", "f", "Gam", "Phi", "xbar"))
+    torch.cuda.synchronize()
+    A32, B32 = A.astype(np.float32).astype(np.float64), B.astype(np.float32).astype(np.float64)
+    ref = [oc.condense(A32[b], B32[b], Q, R, Qf, N, x0=x0[b], c=None if c is None else c[b])
+           for b in range(batch)]
+    out = {k: v.double() for k, v in out.items()}
+    _check(out, ref, N * nu, 2e-5)

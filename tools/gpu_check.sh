@@ -6,7 +6,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out
 mkdir -p $OUT
 cd $ROOT
-timeout -k 10 600 python -m pytest tests -m gpu -q -rf > $OUT/${TAG}_pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf --timeout 120 --timeout-method thread > $OUT/${TAG}_pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 $OUT/${TAG}_pytest.log
 if [ $rc -gt 1 ]; then exit $rc; fi

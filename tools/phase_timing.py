@@ -48,6 +48,15 @@ if cfg == 2:
     w = bench.Config2(a, torch.device("cuda"), 0)
     run = lambda: w._fused(0)  # noqa: E731
     waves = (a.batch + 3) // 4 * R
+elif cfg == 55:
+    # condense_mfma_kernel of config 5 (phase 0 backward W~/What, 1 forward Gamma~/E)
+    reader = lib.mpcqp_debug_phase_cycles_condense
+    reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    PHASES = ["backward W/What", "fw: loads+What", "fw: MFMA tiles", "fw: Gam/H epilogue", "fw: E tile", "", "", ""]
+    a = A(); a.batch = 32768; a.slots = 1; a.horizon = 0; a.reps = 1
+    w = bench.CONFIGS[5](a, torch.device("cuda"), 0)
+    run = lambda: w._condense(0)  # noqa: E731
+    waves = a.batch * R
 else:
     # qp_wg_kernel of config 3 / 5 (phases 0..3: K load, z sweep-in, GI, refinement)
     PHASES = ["load K", "sweep-in z", "active set", "refinement", "", "", "", ""]
