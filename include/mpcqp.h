@@ -47,6 +47,7 @@
 #ifndef MPCQP_H
 #define MPCQP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -213,6 +214,38 @@ int mpcqp_solve_qp(int dtype, int batch, int n, int m,
                    const void* ub, int64_t strideUb,
                    void* z, void* y, int32_t* status, int max_iter, double tol,
                    void* stream);
+
+/*
+ * Two-kernel fp32 path for the large QPs of mpcqp_solve_qp / mpcqp_solve_box
+ * (configs 3 and 5; replaces the same per-step IPOPT call,
+ * session_4/main.py:115-116): the "sweep every z in" phase runs as its own
+ * MFMA kernel (mpcqp_sweep) into a caller workspace, then the active set runs
+ * on the pre-swept matrix.  Same arguments, results and status codes as
+ * mpcqp_solve_qp / mpcqp_solve_box.
+ *   mpcqp_solve_qp_workspace: bytes the _ws calls need for (dtype, batch, n,
+ *     m) -- batch * (n+m)(n+m+1)/2 floats -- or 0 where the path does not
+ *     apply (fp64, n + m <= 64, padded n + m > 192); with 0 or ws == NULL the
+ *     _ws calls are the plain ones.
+ *   mpcqp_sweep: M = SWEEP_z([[H, G'], [G, 0]]) = [[-H^-1, H^-1 G'],
+ *     [G H^-1, -G H^-1 G']] packed lower over n + m per instance (dense
+ *     stride), status[b] = 0 / MPCQP_STATUS_NOT_CONVEX / MPCQP_STATUS_NONFINITE.
+ *     MPCQP_F32 only; 64 < 16*ceil(n/16) + m <= 192.
+ */
+size_t mpcqp_solve_qp_workspace(int dtype, int batch, int n, int m);
+int mpcqp_sweep(int dtype, int batch, int n, int m, const void* H, int64_t strideH,
+                const void* G, int64_t strideG, void* M, int32_t* status, void* stream);
+int mpcqp_solve_qp_ws(int dtype, int batch, int n, int m,
+                      const void* H, int64_t strideH, const void* f, int64_t stridef,
+                      const void* G, int64_t strideG, const void* hl, const void* hu,
+                      int64_t strideh, const void* lb, int64_t strideLb,
+                      const void* ub, int64_t strideUb,
+                      void* z, void* y, int32_t* status, int max_iter, double tol,
+                      void* ws, size_t ws_bytes, void* stream);
+int mpcqp_solve_box_ws(int dtype, int batch, int n,
+                       const void* H, int64_t strideH, const void* f, int64_t stridef,
+                       const void* lb, int64_t strideLb, const void* ub, int64_t strideUb,
+                       void* z, int32_t* status, int max_iter, double tol,
+                       void* ws, size_t ws_bytes, void* stream);
 
 /*
  * Batched finite-horizon Riccati recursion, FHC.py:51-61:

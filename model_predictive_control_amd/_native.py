@@ -53,6 +53,13 @@ SIGNATURES = {
     "mpcqp_max_qp_size": (_i, [_i]),
     "mpcqp_solve_qp": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64,
                             _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i, _d, _vp]),
+    "mpcqp_solve_qp_workspace": (ctypes.c_size_t, [_i, _i, _i, _i]),
+    "mpcqp_sweep": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "mpcqp_solve_qp_ws": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64,
+                               _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i, _d, _vp, ctypes.c_size_t,
+                               _vp]),
+    "mpcqp_solve_box_ws": (_i, [_i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
+                                _vp, _vp, _i, _d, _vp, ctypes.c_size_t, _vp]),
     "mpcqp_riccati": (_i, [_i, _i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                            _vp, _i64, _vp, _vp, _vp]),
     "mpcqp_bicycle_rti": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _i64, _vp, _i64,

@@ -24,7 +24,8 @@ import torch
 from . import _native as nat
 
 __all__ = [
-    "condense", "solve_box", "mpc_box", "solve_poly", "riccati", "gemv", "rollout",
+    "condense", "solve_box", "mpc_box", "solve_poly", "solve_qp", "sweep", "riccati", "gemv",
+    "rollout",
     "pack_lower", "unpack_lower", "status_code", "status_iters",
 ]
 
@@ -47,6 +48,22 @@ def _stream() -> int:
 
 def _ptr(t):
     return None if t is None else t.data_ptr()
+
+
+_WS: dict = {}
+
+
+def _workspace(nbytes: int, dev) -> torch.Tensor | None:
+    """Device scratch for the two-kernel QP path, cached per (device, size):
+    a buffer is never freed or replaced, so HIP graphs captured over a call
+    keep a valid pointer."""
+    if nbytes <= 0:
+        return None
+    key = (str(dev), int(nbytes))
+    ws = _WS.get(key)
+    if ws is None:
+        ws = _WS[key] = torch.empty((int(nbytes),), dtype=torch.uint8, device=dev)
+    return ws
 
 
 def _dev(x, dtype, device):
@@ -205,8 +222,11 @@ def _bound(v, n, dt, dev):
 
 
 def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, tol: float = 0.0,
-              out: tuple | None = None):
-    """Batched  min 1/2 z'Hz + f'z  s.t.  lb <= z <= ub.  Returns (z, status)."""
+              out: tuple | None = None, presweep: bool = True):
+    """Batched  min 1/2 z'Hz + f'z  s.t.  lb <= z <= ub.  Returns (z, status).
+
+    fp32 with n > 64: the -H^-1 sweep runs first as its own MFMA kernel
+    (``mpcqp_solve_box_ws``) unless ``presweep=False``."""
     dt, dev = f.dtype, f.device
     f = _dev(f, dt, dev)
     H = _dev(H, dt, dev)
@@ -225,10 +245,13 @@ def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, tol: float = 0.0,
         status = torch.empty((batch,), dtype=torch.int32, device=dev)
     else:
         z, status = out
-    rc = _lib().mpcqp_solve_box(_code(dt), batch, n, _ptr(H), sH, _ptr(f), sf, _ptr(lbt), slb,
+    lib = _lib()
+    wsb = int(lib.mpcqp_solve_qp_workspace(_code(dt), batch, n, 0)) if presweep else 0
+    ws = _workspace(wsb, dev)
+    rc = lib.mpcqp_solve_box_ws(_code(dt), batch, n, _ptr(H), sH, _ptr(f), sf, _ptr(lbt), slb,
                                 _ptr(ubt), sub, _ptr(z), _ptr(status), int(max_iter), float(tol),
-                                _stream())
-    nat.check(rc, "mpcqp_solve_box")
+                                _ptr(ws), wsb, _stream())
+    nat.check(rc, "mpcqp_solve_box_ws")
     return z, status
 
 
@@ -337,12 +360,14 @@ class PolyQP:
 
 # ------------------------------------------ general QP, per-instance rows
 def solve_qp(H, f, G=None, hl=None, hu=None, lb=None, ub=None, *, max_iter: int = 0,
-             tol: float = 0.0, out: tuple | None = None):
+             tol: float = 0.0, out: tuple | None = None, presweep: bool = True):
     """Batched  min 1/2 z'Hz + f'z  s.t.  lb <= z <= ub,  hl <= G z <= hu.
 
     Every operand may be per instance (leading batch dim) or shared: H packed
     lower (n(n+1)/2), G (m, n), hl/hu (m), lb/ub (n).  n + m <= 192.
-    One instance per workgroup (libmpcqp ``mpcqp_solve_qp``).
+    One instance per workgroup (libmpcqp ``mpcqp_solve_qp``); fp32 with
+    64 < n + m runs the z sweep first as its own MFMA kernel
+    (``mpcqp_solve_qp_ws``) unless ``presweep=False``.
     Returns (z, y, status); y (batch, m) are the row multipliers
     (y > 0 at the upper bound, y < 0 at the lower bound).
     """
@@ -376,11 +401,37 @@ def solve_qp(H, f, G=None, hl=None, hu=None, lb=None, ub=None, *, max_iter: int 
         status = torch.empty((batch,), dtype=torch.int32, device=dev)
     else:
         z, y, status = out
-    rc = _lib().mpcqp_solve_qp(_code(dt), batch, n, m, _ptr(H), sH, _ptr(f), sf, _ptr(G), sG,
+    lib = _lib()
+    wsb = int(lib.mpcqp_solve_qp_workspace(_code(dt), batch, n, m)) if presweep else 0
+    ws = _workspace(wsb, dev)
+    rc = lib.mpcqp_solve_qp_ws(_code(dt), batch, n, m, _ptr(H), sH, _ptr(f), sf, _ptr(G), sG,
                                _ptr(hl), _ptr(hu), sh, _ptr(lbt), slb, _ptr(ubt), sub, _ptr(z),
-                               _ptr(y), _ptr(status), int(max_iter), float(tol), _stream())
-    nat.check(rc, "mpcqp_solve_qp")
+                               _ptr(y), _ptr(status), int(max_iter), float(tol), _ptr(ws), wsb,
+                               _stream())
+    nat.check(rc, "mpcqp_solve_qp_ws")
     return z, y, status
+
+
+def sweep(H, G=None):
+    """Batched M = SWEEP_z([[H, G'], [G, 0]]) (libmpcqp ``mpcqp_sweep``, fp32,
+    MFMA): returns (M packed lower over n + m per instance, status) with
+    M = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']]."""
+    dt, dev = H.dtype, H.device
+    H = _dev(H, dt, dev)
+    nH = int(H.shape[-1])
+    n = isqrt_packed(nH)
+    sH, bH = _inst(H, 1, "H")
+    m = 0 if G is None else int(G.shape[-2])
+    G = _dev(G, dt, dev)
+    sG, bG = (0, None) if G is None else _inst(G, 2, "G")
+    batch = _batch_of((sH, bH), (sG, bG))
+    nt = n + m
+    M = torch.empty((batch, nt * (nt + 1) // 2), dtype=dt, device=dev)
+    status = torch.empty((batch,), dtype=torch.int32, device=dev)
+    rc = _lib().mpcqp_sweep(_code(dt), batch, n, m, _ptr(H), sH, _ptr(G), sG, _ptr(M),
+                            _ptr(status), _stream())
+    nat.check(rc, "mpcqp_sweep")
+    return M, status
 
 
 # ---------------------------------------------------------------- Riccati

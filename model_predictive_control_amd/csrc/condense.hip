@@ -24,6 +24,7 @@
 // round trips on the serial chain); wider states use an LDS-parallel W
 // recursion with the xbar recursion on other lanes of the same phases.
 #include "common.hpp"
+#include "mfma.hpp"
 
 #include <cstdlib>
 
@@ -412,42 +413,6 @@ static int launch_condense(const CondenseArgs<T>& a, hipStream_t st) {
 // rows) runs on the VALU from the C tile: 16 FMAs per 4 output rows plus the
 // same transpose as a cross-group reduction, which leaves output row g of
 // column c in lane (g, c), so each H row segment is one 64-lane store.
-typedef float mf4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void xpose4(float (&v)[4]) {
-  // lane group g, register r  ->  lane group r, register g
-  auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0]), __float_as_uint(v[2]), false, false);
-  auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[1]), __float_as_uint(v[3]), false, false);
-  auto t0 = __builtin_amdgcn_permlane16_swap(s0[0], s1[0], false, false);
-  auto t1 = __builtin_amdgcn_permlane16_swap(s0[1], s1[1], false, false);
-  v[0] = __uint_as_float(t0[0]);
-  v[1] = __uint_as_float(t0[1]);
-  v[2] = __uint_as_float(t1[0]);
-  v[3] = __uint_as_float(t1[1]);
-}
-
-__device__ __forceinline__ mf4 mfma4(const float (&a)[4], const float (&b)[4], mf4 acc) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
-  return acc;
-}
-
-// Buffer descriptors (raw, stride 0, range-checked): every per-lane memory
-// access is base (SGPR) + 32-bit byte offset, and a masked-out lane uses an
-// offset past num_records -- its load returns 0 and its store is dropped, so
-// the loads and stores carry no exec-mask branches and no selects.
-using rsrc_t = __amdgpu_buffer_rsrc_t;
-constexpr int kOOB = 0x7ffffff0;
-__device__ __forceinline__ rsrc_t mk_rsrc(const void* p, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ float bld(rsrc_t r, int off) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-__device__ __forceinline__ void bst(float v, rsrc_t r, int off) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
-}
-
 // NT: Gamma tiles (n <= 16 NT); NU4: What rows held per lane (nu <= NU4);
 // DRIFT: per-stage c_k present (its loads get their own queue)
 template <int NT, int NU4, bool DRIFT>

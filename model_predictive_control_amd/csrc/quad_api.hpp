@@ -57,7 +57,12 @@ inline bool use_block_kernels() {
 // solve_qp.hip
 int solve_box_wg(int dtype, int batch, int n, const void* H, int64_t sH, const void* f,
                  int64_t sf, const void* lb, int64_t sLb, const void* ub, int64_t sUb, void* z,
-                 int32_t* status, int max_iter, double tol, hipStream_t st);
+                 int32_t* status, int max_iter, double tol, hipStream_t st,
+                 const void* Ms = nullptr);
 int max_qp_size_dtype(int dtype);
+size_t qp_ws_bytes(int dtype, int batch, int n, int m);
+// sweep.hip
+int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void* G, int64_t sG,
+                 void* M, int32_t* status, hipStream_t st);
 
 }  // namespace mpcqp

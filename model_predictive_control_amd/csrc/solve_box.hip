@@ -168,3 +168,26 @@ extern "C" int mpcqp_solve_box(int dtype, int batch, int n, const void* H, int64
   return solve_box_t<float>(batch, n, H, strideH, f, stridef, lb, strideLb, ub, strideUb, z,
                             status, max_iter, tol, st);
 }
+
+extern "C" int mpcqp_solve_box_ws(int dtype, int batch, int n, const void* H, int64_t strideH,
+                                  const void* f, int64_t stridef, const void* lb,
+                                  int64_t strideLb, const void* ub, int64_t strideUb, void* z,
+                                  int32_t* status, int max_iter, double tol, void* ws,
+                                  size_t ws_bytes, void* stream) {
+  using namespace mpcqp;
+  const size_t need = qp_ws_bytes(dtype, batch, n, 0);
+  if (need == 0 || ws == nullptr || n <= 64)
+    return mpcqp_solve_box(dtype, batch, n, H, strideH, f, stridef, lb, strideLb, ub, strideUb, z,
+                           status, max_iter, tol, stream);
+  MPCQP_CHECK_ARG(ws_bytes >= need, "mpcqp_solve_box_ws: workspace %zu bytes < %zu", ws_bytes, need);
+  MPCQP_CHECK_ARG(n <= max_qp_size_dtype(dtype), "mpcqp_solve_box_ws: n=%d outside [1,%d]", n,
+                  max_qp_size_dtype(dtype));
+  MPCQP_CHECK_ARG(H && f && z && status, "mpcqp_solve_box_ws: H, f, z, status are required");
+  MPCQP_CHECK_ARG(strideH >= 0 && stridef >= 0 && strideLb >= 0 && strideUb >= 0,
+                  "mpcqp_solve_box_ws: negative stride");
+  hipStream_t st = (hipStream_t)stream;
+  int rc = sweep_launch(batch, n, 0, H, strideH, nullptr, 0, ws, status, st);
+  if (rc != MPCQP_OK) return rc;
+  return solve_box_wg(dtype, batch, n, H, strideH, f, stridef, lb, strideLb, ub, strideUb, z,
+                      status, max_iter, tol, st, ws);
+}

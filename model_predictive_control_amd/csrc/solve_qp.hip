@@ -16,6 +16,10 @@
 
 namespace mpcqp {
 
+int sweep_tiles(int dtype, int n, int m);
+int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void* G, int64_t sG,
+                 void* M, int32_t* status, hipStream_t st);
+
 template <typename T>
 struct QpArgs {
   int batch, n, m;
@@ -29,6 +33,9 @@ struct QpArgs {
   int max_iter;
   int refine;
   T tol;
+  // pre-swept M (sweep.hip: packed lower over n + m, stride (n+m)(n+m+1)/2)
+  // and its per-instance status in status[]; nullptr: sweep in the kernel
+  const T* Ms;
 };
 
 // Pivots per barrier in the initial sweep-in: the replicas cost BK*(BR+BC)
@@ -60,6 +67,8 @@ void qp_wg_kernel(QpArgs<T> a) {
 #ifdef MPCQP_PHASE_TIMING
   PhaseClock mpcqp_clk;
 #endif
+  // status written by the pre-sweep (read before anyone writes it back)
+  const int pre = a.Ms ? a.status[b] : 0;
   int bad = 0, nonfin = 0;
   for (int i = tid; i < NMAX; i += S::threads) {
     T l = -inf, u = inf, fi = T(0);
@@ -83,13 +92,16 @@ void qp_wg_kernel(QpArgs<T> a) {
   M.init(tid);
   const T* Hb = a.H + (int64_t)b * a.sH;
   const T* Gb = a.G ? a.G + (int64_t)b * a.sG : nullptr;
+  const T* Mb = a.Ms ? a.Ms + (int64_t)b * ((int64_t)nt * (nt + 1) / 2) : nullptr;
 #pragma unroll
   for (int r = 0; r < BR; ++r)
 #pragma unroll
     for (int c = 0; c < BC; ++c) {
       const int i = M.bi * BR + r, j = M.bj * BC + c;
       T v = T(0);
-      if (i < n && j < n) {
+      if (Mb) {
+        if (i < nt && j < nt) v = (j <= i) ? Mb[i * (i + 1) / 2 + j] : Mb[j * (j + 1) / 2 + i];
+      } else if (i < n && j < n) {
         v = (j <= i) ? Hb[i * (i + 1) / 2 + j] : Hb[j * (j + 1) / 2 + i];
       } else if (i < nt && j < n) {
         v = Gb[(int64_t)(i - n) * n + j];
@@ -110,7 +122,9 @@ void qp_wg_kernel(QpArgs<T> a) {
     val[r] = __builtin_nan("");
     lam[r] = __builtin_nan("");
   }
-  if (flags & 2) {
+  if (pre) {
+    code = pre;
+  } else if (flags & 2) {
     code = MPCQP_STATUS_NONFINITE;
   } else if (flags & 1) {
     code = MPCQP_STATUS_INFEASIBLE;
@@ -118,7 +132,7 @@ void qp_wg_kernel(QpArgs<T> a) {
     // sweep every z in: M = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']] --
     // BK pivots per publish/barrier (sweep_blk), the remainder one by one
     constexpr int BK = QpBlock<T, S>::bk;
-    int k = 0;
+    int k = Mb ? n : 0;  // pre-swept: every z is in already
     for (int blk = 0; BK > 1 && k + BK <= n; k += BK, ++blk) {
       T* cb = sm + L::oBlk + (blk & 1) * 8 * NMAX;
       T* rb = cb + 4 * NMAX;
@@ -212,7 +226,7 @@ static int solve_qp_t(int batch, int n, int m, const void* H, int64_t sH, const 
                       int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
                       int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
                       void* z, void* y, int32_t* status, int max_iter, double tol,
-                      hipStream_t st) {
+                      hipStream_t st, const void* Ms = nullptr) {
   QpArgs<T> a;
   a.batch = batch; a.n = n; a.m = m;
   a.H = (const T*)H; a.sH = sH;
@@ -226,18 +240,30 @@ static int solve_qp_t(int batch, int n, int m, const void* H, int64_t sH, const 
   // fp32: two refinement steps against the original data; fp64: one
   a.refine = sizeof(T) == 4 ? 2 : 1;
   a.tol = tol > 0 ? (T)tol : (sizeof(T) == 8 ? (T)1e-12 : (T)1e-6);
+  a.Ms = (const T*)Ms;
   return launch_qp<T>(a, st);
 }
 
 // used by mpcqp_solve_box for n > 64
+// (with Ms: the pre-swept -H^-1 of mpcqp_sweep, fp32 only)
 int solve_box_wg(int dtype, int batch, int n, const void* H, int64_t sH, const void* f,
                  int64_t sf, const void* lb, int64_t sLb, const void* ub, int64_t sUb, void* z,
-                 int32_t* status, int max_iter, double tol, hipStream_t st) {
+                 int32_t* status, int max_iter, double tol, hipStream_t st, const void* Ms) {
   if (dtype == MPCQP_F64)
     return solve_qp_t<double>(batch, n, 0, H, sH, f, sf, nullptr, 0, nullptr, nullptr, 0, lb,
                               sLb, ub, sUb, z, nullptr, status, max_iter, tol, st);
   return solve_qp_t<float>(batch, n, 0, H, sH, f, sf, nullptr, 0, nullptr, nullptr, 0, lb, sLb,
-                           ub, sUb, z, nullptr, status, max_iter, tol, st);
+                           ub, sUb, z, nullptr, status, max_iter, tol, st, Ms);
+}
+
+// Workspace of the two-kernel path (MFMA pre-sweep + qp_wg_kernel): the
+// packed swept matrix per instance, or 0 where that path does not apply
+// (fp64, or n + m within the 256-thread kernel where the in-kernel sweep is
+// cheap).
+size_t qp_ws_bytes(int dtype, int batch, int n, int m) {
+  if (batch <= 0 || n + m <= 64 || sweep_tiles(dtype, n, m) == 0) return 0;
+  const size_t nt = (size_t)(n + m);
+  return (size_t)batch * (nt * (nt + 1) / 2) * sizeof(float);
 }
 
 int max_qp_size_dtype(int dtype) {
@@ -270,6 +296,37 @@ extern "C" int mpcqp_solve_qp(int dtype, int batch, int n, int m, const void* H,
                               lb, strideLb, ub, strideUb, z, y, status, max_iter, tol, st);
   return solve_qp_t<float>(batch, n, m, H, strideH, f, stridef, G, strideG, hl, hu, strideh, lb,
                            strideLb, ub, strideUb, z, y, status, max_iter, tol, st);
+}
+
+extern "C" size_t mpcqp_solve_qp_workspace(int dtype, int batch, int n, int m) {
+  return mpcqp::qp_ws_bytes(dtype, batch, n, m);
+}
+
+extern "C" int mpcqp_solve_qp_ws(int dtype, int batch, int n, int m, const void* H,
+                                 int64_t strideH, const void* f, int64_t stridef, const void* G,
+                                 int64_t strideG, const void* hl, const void* hu, int64_t strideh,
+                                 const void* lb, int64_t strideLb, const void* ub,
+                                 int64_t strideUb, void* z, void* y, int32_t* status,
+                                 int max_iter, double tol, void* ws, size_t ws_bytes,
+                                 void* stream) {
+  using namespace mpcqp;
+  const size_t need = qp_ws_bytes(dtype, batch, n, m);
+  if (need == 0 || ws == nullptr)
+    return mpcqp_solve_qp(dtype, batch, n, m, H, strideH, f, stridef, G, strideG, hl, hu, strideh,
+                          lb, strideLb, ub, strideUb, z, y, status, max_iter, tol, stream);
+  MPCQP_CHECK_ARG(ws_bytes >= need, "mpcqp_solve_qp_ws: workspace %zu bytes < %zu", ws_bytes, need);
+  MPCQP_CHECK_ARG(n + m <= max_qp_size_dtype(dtype), "mpcqp_solve_qp_ws: n + m = %d exceeds %d",
+                  n + m, max_qp_size_dtype(dtype));
+  MPCQP_CHECK_ARG(H && f && z && status, "mpcqp_solve_qp_ws: H, f, z, status are required");
+  MPCQP_CHECK_ARG(m == 0 || G, "mpcqp_solve_qp_ws: G required when m > 0");
+  MPCQP_CHECK_ARG(strideH >= 0 && stridef >= 0 && strideG >= 0 && strideh >= 0 &&
+                      strideLb >= 0 && strideUb >= 0,
+                  "mpcqp_solve_qp_ws: negative stride");
+  hipStream_t st = (hipStream_t)stream;
+  int rc = sweep_launch(batch, n, m, H, strideH, G, strideG, ws, status, st);
+  if (rc != MPCQP_OK) return rc;
+  return solve_qp_t<float>(batch, n, m, H, strideH, f, stridef, G, strideG, hl, hu, strideh, lb,
+                           strideLb, ub, strideUb, z, y, status, max_iter, tol, st, ws);
 }
 
 #ifdef MPCQP_PHASE_TIMING

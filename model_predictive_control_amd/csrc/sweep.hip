@@ -1,0 +1,292 @@
+// sweep.hip -- batched blocked Goodnight sweep on MFMA (fp32): the "sweep every
+// z in" phase of the workgroup QP kernel (solve_qp.hip) as its own kernel.
+//
+// For the condensed QP of session_4/main.py:115-116 the dual active set needs
+//     M = SWEEP_z(K),  K = [[H, G'], [G, 0]]
+//       = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']]
+// before its first iteration.  In qp_wg_kernel this is n rank-1 updates of
+// the (n+m)^2 matrix, each behind a barrier (65 % of config 5's solve time).
+// Here it is the same sweep in 16-pivot blocks: per block k, with
+// D = M_kk, R_i = M_ki (the block row) and Ds = SWEEP(D) = -D^-1,
+//     M_ij += R_i' (Ds R_j)        (i >= j, both != k)   -- MFMA
+//     M_ki  = D^-1 R_i  (i < k),   M_ik = R_i' D^-1 (i > k),   M_kk = Ds
+// which is Goodnight's a_ij - a_ik a_kj / a_kk with a_kk -> D.  Sweeping every
+// z block leaves M above (the 16 x 16 SWEEP(D) runs on the VALU with DPP
+// row_newbcast / ds_bpermute broadcasts).
+//
+// Layout: one instance per wavefront, the lower block triangle of the padded
+// matrix held as T(T+1)/2 MFMA C-layout tiles in registers (mfma.hpp: lane
+// (g, c) holds rows 4g..4g+3 of column c), so every product above is of the
+// form P' Y that v_mfma_f32_16x16x4f32 takes from C-layout operands directly;
+// the transposed block rows R_i = M_ik' (i > k) come from one MFMA against the
+// identity (exact).  Index space: z indices at 0..n-1, padded to np = 16 KP
+// with identity pivots (sweeping a decoupled unit pivot changes nothing
+// else), rows at np..np+m-1.  T = ceil((np + m) / 16) <= 12.
+//
+// Input H packed lower (n(n+1)/2), G (m x n) row-major; output M packed lower
+// over the original n + m indices.  status[b]: 0, MPCQP_STATUS_NOT_CONVEX (a
+// pivot <= 0: H not positive definite) or MPCQP_STATUS_NONFINITE;
+// mpcqp_solve_qp_ws / mpcqp_solve_box_ws consume M and that status.
+#include "common.hpp"
+#include "mfma.hpp"
+
+namespace mpcqp {
+
+struct SweepArgs {
+  int batch, n, m, np, kp;
+  const float* H; int64_t sH;
+  const float* G; int64_t sG;
+  float* M;
+  int32_t* status;
+};
+
+__device__ __forceinline__ constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
+
+__device__ __forceinline__ mf4 mm(const mf4& p, const mf4& y, mf4 acc) {
+  // acc + P' Y (both C layout)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(p[s], y[s], acc, 0, 0, 0);
+  return acc;
+}
+
+template <int P>
+__device__ __forceinline__ float row_bcast(float v) {
+  // lane P of each 16-lane row to the whole row
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + P, 0xf, 0xf, false));
+}
+
+// SWEEP of a symmetric 16 x 16 C-layout tile in place (-> -D^-1); bad |= a
+// pivot that is not > 0.
+__device__ __forceinline__ void sweep16(mf4& d, int g, int c, bool& bad) {
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    const int gp = p >> 2, ip = p & 3;
+    const float piv = readlane(d[ip], 16 * gp + p);
+    bad |= !(piv > 0.f);
+    const float inv = 1.f / piv;
+    float col[4];
+    switch (p) {  // row_newbcast needs an immediate lane
+#define MPCQP_RB(P_)                                               \
+  case P_:                                                         \
+    for (int i = 0; i < 4; ++i) col[i] = row_bcast<P_>(d[i]);      \
+    break;
+      MPCQP_RB(0) MPCQP_RB(1) MPCQP_RB(2) MPCQP_RB(3) MPCQP_RB(4) MPCQP_RB(5) MPCQP_RB(6)
+      MPCQP_RB(7) MPCQP_RB(8) MPCQP_RB(9) MPCQP_RB(10) MPCQP_RB(11) MPCQP_RB(12) MPCQP_RB(13)
+      MPCQP_RB(14) MPCQP_RB(15)
+#undef MPCQP_RB
+    }
+    // row p, column c: lane (gp, c), register ip
+    const float rowv = __int_as_float(
+        __builtin_amdgcn_ds_bpermute(4 * (16 * gp + c), __float_as_int(d[ip])));
+    const bool iscol = c == p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float t = col[i] * inv;
+      const float gen = fmaf(-t, rowv, d[i]);
+      const bool isrow = (i == ip) && (g == gp);
+      d[i] = iscol ? (isrow ? -inv : t) : (isrow ? rowv * inv : gen);
+    }
+  }
+}
+
+// offsets are 32-bit bytes from a range-checked descriptor: a masked lane
+// adds kOOB and reads 0 / drops its store (cols of tile column tj go in the
+// instruction's immediate offset)
+// (masked offsets are kOOB | x <= 0x7fffffff, so adding imm <= 4095 never wraps)
+__device__ __forceinline__ float bld_i(rsrc_t r, unsigned voff, int imm) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(voff + (unsigned)imm), 0, 0));
+}
+__device__ __forceinline__ void bst_i(float v, rsrc_t r, unsigned voff, int imm) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(voff + (unsigned)imm), 0, 0);
+}
+
+template <int T>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
+void sweep_mfma_kernel(SweepArgs a) {
+  constexpr int NT = T * (T + 1) / 2;
+  const int b = blockIdx.x;
+  const int l = threadIdx.x, g = l >> 4, c = l & 15;
+  const int n = a.n, m = a.m, np = a.np, kp = a.kp, nt = n + m;
+  const rsrc_t rH = mk_rsrc(a.H + (int64_t)b * a.sH, (int64_t)n * (n + 1) / 2 * 4);
+  const rsrc_t rG = mk_rsrc(m ? a.G + (int64_t)b * a.sG : a.H, (int64_t)m * n * 4);
+
+  // ---- load K into the lower block triangle (z at 0..n-1, pad, rows at np..)
+  mf4 t[NT];
+  bool nonfin = false;
+  // pad columns of the last z tile column read nothing
+  const unsigned cmask = (16 * (kp - 1) + c < n) ? 0u : (unsigned)kOOB;
+#pragma unroll
+  for (int ti = 0; ti < T; ++ti) {
+    unsigned base[4];
+    if (ti < kp) {  // H rows: packed row offset
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * ti + 4 * g + i;
+        base[i] = r < n ? 4 * (r * (r + 1) / 2 + c) : kOOB;
+      }
+    } else {  // G rows
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * ti + 4 * g + i - np;
+        base[i] = r < m ? 4 * (r * n + c) : kOOB;
+      }
+    }
+#pragma unroll
+    for (int tj = 0; tj < ti; ++tj) {
+      if (tj < kp) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = bld_i(ti < kp ? rH : rG, base[i] | (tj == kp - 1 ? cmask : 0u), 64 * tj);
+          nonfin |= !finite(v);
+          t[tri(ti, tj)][i] = v;
+        }
+      } else {
+        t[tri(ti, tj)] = mf4{0.f, 0.f, 0.f, 0.f};
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ti < kp) {  // diagonal z tile: mirror the upper half, unit pad pivots
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * ti + 4 * g + i, cc = 16 * ti + c;
+        const int hi = r > cc ? r : cc, lo = r > cc ? cc : r;
+        const float v = bld(rH, hi < n ? 4 * (hi * (hi + 1) / 2 + lo) : kOOB) +
+                        ((r == cc && r >= n) ? 1.f : 0.f);
+        nonfin |= !finite(v);
+        t[tri(ti, ti)][i] = v;
+      }
+    } else {
+      t[tri(ti, ti)] = mf4{0.f, 0.f, 0.f, 0.f};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  bool bad = false;
+  mf4 eye;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) eye[i] = (4 * g + i == c) ? 1.f : 0.f;
+  const mf4 zero = {0.f, 0.f, 0.f, 0.f};
+
+  // ---- blocked sweep over the z blocks
+#pragma unroll
+  for (int k = 0; k < T; ++k) {
+    if (k < kp) {  // uniform
+      mf4 ds = t[tri(k, k)];
+      sweep16(ds, g, c, bad);
+      __builtin_amdgcn_sched_barrier(0);
+      mf4 R[T];
+#pragma unroll
+      for (int i = 0; i < T; ++i) {
+        if (i < k) R[i] = t[tri(k, i)];
+        else if (i > k) R[i] = mm(t[tri(i, k)], eye, zero);  // M_ik' (exact)
+      }
+#pragma unroll
+      for (int j = 0; j < T; ++j) {
+        if (j == k) continue;
+        const mf4 v = mm(ds, R[j], zero);  // Ds R_j = -D^-1 R_j (Ds symmetric)
+#pragma unroll
+        for (int i = j; i < T; ++i)
+          if (i != k) t[tri(i, j)] = mm(R[i], v, t[tri(i, j)]);
+        if (j < k) t[tri(k, j)] = -v;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const mf4 dinv = -ds;
+#pragma unroll
+      for (int i = k + 1; i < T; ++i) t[tri(i, k)] = mm(R[i], dinv, zero);
+      t[tri(k, k)] = ds;
+    }
+  }
+
+  // ---- store M packed lower over the original n + m indices
+  const bool fin_bad = __builtin_amdgcn_ballot_w64(nonfin) != 0;
+  const bool piv_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+  const rsrc_t rM = mk_rsrc(a.M + (int64_t)b * ((int64_t)nt * (nt + 1) / 2),
+                            (int64_t)nt * (nt + 1) / 2 * 4);
+  // opaque lane id: keeps the load phase's index math from being CSE'd into
+  // (and kept live until) the stores
+  int ls = l;
+  asm volatile("" : "+v"(ls));
+  const int gs = ls >> 4, cs = ls & 15;
+  // tile-space column -> original column (pad: masked)
+  const unsigned czmask = (16 * (kp - 1) + cs < n) ? 0u : (unsigned)kOOB;     // last z tile column
+  const unsigned crmask = (16 * (T - 1) + cs - np < m) ? 0u : (unsigned)kOOB;  // last row tile column
+#pragma unroll
+  for (int ti = 0; ti < T; ++ti) {
+    unsigned base[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int R = 16 * ti + 4 * gs + i;
+      const int r = R < n ? R : (R < np ? -1 : (R - np < m ? n + R - np : -1));
+      base[i] = r >= 0 ? 4 * (r * (r + 1) / 2 + cs) : kOOB;
+    }
+#pragma unroll
+    for (int tj = 0; tj <= ti; ++tj) {
+      // column orig = C (z) or C - np + n (rows); diagonal tiles keep r >= c
+      const int shift = tj < kp ? 0 : 4 * (n - np);
+      const unsigned msk = (tj == kp - 1 ? czmask : 0u) | (tj == T - 1 && tj >= kp ? crmask : 0u);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned dm = (tj == ti && cs > 4 * gs + i) ? (unsigned)kOOB : 0u;
+        bst_i(t[tri(ti, tj)][i], rM, (base[i] + (unsigned)shift) | msk | dm, 64 * tj);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (l == 0)
+    a.status[b] = fin_bad ? MPCQP_STATUS_NONFINITE : (piv_bad ? MPCQP_STATUS_NOT_CONVEX : 0);
+}
+
+template <int T>
+static int launch_sweep_t(const SweepArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((sweep_mfma_kernel<T>), dim3(a.batch), dim3(64), 0, st, a);
+  MPCQP_CHECK_LAUNCH("sweep_mfma_kernel");
+  return MPCQP_OK;
+}
+
+// tiles of the padded index space, or 0 when the MFMA sweep does not apply
+int sweep_tiles(int dtype, int n, int m) {
+  if (dtype != MPCQP_F32 || n < 1 || m < 0) return 0;
+  const int np = (n + 15) / 16 * 16;
+  const int T = (np + m + 15) / 16;
+  return (T >= 5 && T <= 12) ? T : 0;
+}
+
+int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void* G, int64_t sG,
+                 void* M, int32_t* status, hipStream_t st) {
+  SweepArgs a;
+  a.batch = batch; a.n = n; a.m = m;
+  a.np = (n + 15) / 16 * 16;
+  a.kp = a.np / 16;
+  a.H = (const float*)H; a.sH = sH;
+  a.G = (const float*)G; a.sG = sG;
+  a.M = (float*)M;
+  a.status = status;
+  switch (sweep_tiles(MPCQP_F32, n, m)) {
+    case 5: return launch_sweep_t<5>(a, st);
+    case 6: return launch_sweep_t<6>(a, st);
+    case 7: return launch_sweep_t<7>(a, st);
+    case 8: return launch_sweep_t<8>(a, st);
+    case 9: return launch_sweep_t<9>(a, st);
+    case 10: return launch_sweep_t<10>(a, st);
+    case 11: return launch_sweep_t<11>(a, st);
+    case 12: return launch_sweep_t<12>(a, st);
+    default:
+      set_error("mpcqp_sweep: padded n + m = %d outside the MFMA sweep's 65..192", (n + 15) / 16 * 16 + m);
+      return MPCQP_ENOTSUP;
+  }
+}
+
+}  // namespace mpcqp
+
+extern "C" int mpcqp_sweep(int dtype, int batch, int n, int m, const void* H, int64_t strideH,
+                           const void* G, int64_t strideG, void* M, int32_t* status,
+                           void* stream) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(dtype == MPCQP_F32, "mpcqp_sweep: only MPCQP_F32 runs on the MFMA sweep");
+  MPCQP_CHECK_ARG(batch >= 0 && n >= 1 && m >= 0, "mpcqp_sweep: bad sizes");
+  MPCQP_CHECK_ARG(H && M && status && (m == 0 || G), "mpcqp_sweep: H, M, status (and G) required");
+  MPCQP_CHECK_ARG(strideH >= 0 && strideG >= 0, "mpcqp_sweep: negative stride");
+  MPCQP_CHECK_ARG(sweep_tiles(dtype, n, m) > 0, "mpcqp_sweep: padded n + m = %d outside 65..192",
+                  (n + 15) / 16 * 16 + m);
+  if (batch == 0) return MPCQP_OK;
+  return sweep_launch(batch, n, m, H, strideH, G, strideG, M, status, (hipStream_t)stream);
+}

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CS = os.path.join(ROOT, "model_predictive_control_amd", "csrc")
 LIB = os.path.join(ROOT, "model_predictive_control_amd", "lib", "libmpcqp_timing.so")
 SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.hip", "quad_box.hip",
-        "solve_qp.hip", "bicycle.hip", "misc.hip"]
+        "solve_qp.hip", "sweep.hip", "bicycle.hip", "misc.hip"]
 PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/recheck", "GI: scan+argmax", "GI: pivot col+ratio", "GI: sweep"]
 
 if "--build" in sys.argv:
@@ -18,7 +18,8 @@ if "--build" in sys.argv:
     for s in SRCS:
         o = f"/tmp/timing_{s}.o"
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
-                        "-DMPCQP_PHASE_TIMING", "-I", os.path.join(ROOT, "include"), "-c",
+                        "-DMPCQP_PHASE_TIMING", "-I", os.path.join(ROOT, "include"), "-c"]
+                       + (["-mllvm", "-pragma-unroll-threshold=1000000"] if s == "sweep.hip" else []) + [
                         os.path.join(CS, s), "-o", o], check=True)
         objs.append(o)
     subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "--offload-arch=gfx950", "-o", LIB] + objs, check=True)
