@@ -223,17 +223,21 @@ int mpcqp_solve_qp(int dtype, int batch, int n, int m,
  * on the pre-swept matrix.  Same arguments, results and status codes as
  * mpcqp_solve_qp / mpcqp_solve_box.
  *   mpcqp_solve_qp_workspace: bytes the _ws calls need for (dtype, batch, n,
- *     m) -- batch * (n+m)(n+m+1)/2 floats -- or 0 where the path does not
+ *     m) -- about batch * (n+m)^2 floats -- or 0 where the path does not
  *     apply (fp64, n + m <= 64, padded n + m > 192); with 0 or ws == NULL the
  *     _ws calls are the plain ones.
  *   mpcqp_sweep: M = SWEEP_z([[H, G'], [G, 0]]) = [[-H^-1, H^-1 G'],
- *     [G H^-1, -G H^-1 G']] packed lower over n + m per instance (dense
- *     stride), status[b] = 0 / MPCQP_STATUS_NOT_CONVEX / MPCQP_STATUS_NONFINITE.
- *     MPCQP_F32 only; 64 < 16*ceil(n/16) + m <= 192.
+ *     [G H^-1, -G H^-1 G']] over n + m per instance, packed lower (full = 0)
+ *     or dense row-major (full = 1); status[b] = 0 / MPCQP_STATUS_NOT_CONVEX /
+ *     MPCQP_STATUS_NONFINITE.  MPCQP_F32 only; 64 < 16*ceil(n/16) + m <= 192.
+ *   The _ws solves run mpcqp_sweep (dense) -> a product-form active set on
+ *     the swept matrix (one instance per wavefront, solve_pf.hip) -> the
+ *     workgroup kernel for any instance with more than 64 active constraints.
  */
 size_t mpcqp_solve_qp_workspace(int dtype, int batch, int n, int m);
 int mpcqp_sweep(int dtype, int batch, int n, int m, const void* H, int64_t strideH,
-                const void* G, int64_t strideG, void* M, int32_t* status, void* stream);
+                const void* G, int64_t strideG, void* M, int full, int32_t* status,
+                void* stream);
 int mpcqp_solve_qp_ws(int dtype, int batch, int n, int m,
                       const void* H, int64_t strideH, const void* f, int64_t stridef,
                       const void* G, int64_t strideG, const void* hl, const void* hu,

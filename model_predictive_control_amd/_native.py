@@ -54,7 +54,7 @@ SIGNATURES = {
     "mpcqp_solve_qp": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64,
                             _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i, _d, _vp]),
     "mpcqp_solve_qp_workspace": (ctypes.c_size_t, [_i, _i, _i, _i]),
-    "mpcqp_sweep": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "mpcqp_sweep": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i, _vp, _vp]),
     "mpcqp_solve_qp_ws": (_i, [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i64,
                                _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i, _d, _vp, ctypes.c_size_t,
                                _vp]),

@@ -412,10 +412,10 @@ def solve_qp(H, f, G=None, hl=None, hu=None, lb=None, ub=None, *, max_iter: int 
     return z, y, status
 
 
-def sweep(H, G=None):
+def sweep(H, G=None, *, full: bool = False):
     """Batched M = SWEEP_z([[H, G'], [G, 0]]) (libmpcqp ``mpcqp_sweep``, fp32,
-    MFMA): returns (M packed lower over n + m per instance, status) with
-    M = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']]."""
+    MFMA): returns (M, status) with M = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']]
+    over n + m per instance, packed lower, or dense (n+m, n+m) if ``full``."""
     dt, dev = H.dtype, H.device
     H = _dev(H, dt, dev)
     nH = int(H.shape[-1])
@@ -426,10 +426,11 @@ def sweep(H, G=None):
     sG, bG = (0, None) if G is None else _inst(G, 2, "G")
     batch = _batch_of((sH, bH), (sG, bG))
     nt = n + m
-    M = torch.empty((batch, nt * (nt + 1) // 2), dtype=dt, device=dev)
+    shape = (batch, nt, nt) if full else (batch, nt * (nt + 1) // 2)
+    M = torch.empty(shape, dtype=dt, device=dev)
     status = torch.empty((batch,), dtype=torch.int32, device=dev)
     rc = _lib().mpcqp_sweep(_code(dt), batch, n, m, _ptr(H), sH, _ptr(G), sG, _ptr(M),
-                            _ptr(status), _stream())
+                            int(bool(full)), _ptr(status), _stream())
     nat.check(rc, "mpcqp_sweep")
     return M, status
 

@@ -61,8 +61,10 @@ int solve_box_wg(int dtype, int batch, int n, const void* H, int64_t sH, const v
                  const void* Ms = nullptr);
 int max_qp_size_dtype(int dtype);
 size_t qp_ws_bytes(int dtype, int batch, int n, int m);
-// sweep.hip
-int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void* G, int64_t sG,
-                 void* M, int32_t* status, hipStream_t st);
+int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const void* f,
+                     int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
+                     int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
+                     void* z, void* y, int32_t* status, int max_iter, double tol, void* ws,
+                     hipStream_t st);
 
 }  // namespace mpcqp

@@ -185,9 +185,7 @@ extern "C" int mpcqp_solve_box_ws(int dtype, int batch, int n, const void* H, in
   MPCQP_CHECK_ARG(H && f && z && status, "mpcqp_solve_box_ws: H, f, z, status are required");
   MPCQP_CHECK_ARG(strideH >= 0 && stridef >= 0 && strideLb >= 0 && strideUb >= 0,
                   "mpcqp_solve_box_ws: negative stride");
-  hipStream_t st = (hipStream_t)stream;
-  int rc = sweep_launch(batch, n, 0, H, strideH, nullptr, 0, ws, status, st);
-  if (rc != MPCQP_OK) return rc;
-  return solve_box_wg(dtype, batch, n, H, strideH, f, stridef, lb, strideLb, ub, strideUb, z,
-                      status, max_iter, tol, st, ws);
+  return solve_two_kernel(batch, n, 0, H, strideH, f, stridef, nullptr, 0, nullptr, nullptr, 0, lb,
+                          strideLb, ub, strideUb, z, nullptr, status, max_iter, tol, ws,
+                          (hipStream_t)stream);
 }

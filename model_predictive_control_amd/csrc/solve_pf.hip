@@ -1,0 +1,571 @@
+// solve_pf.hip -- the mixed primal/dual active set of solve_qp.hip (wg.hpp
+// gi_mixed) in PRODUCT FORM on the pre-swept matrix of sweep.hip, one QP
+// instance per wavefront.  This is the fp32 path of mpcqp_solve_qp_ws /
+// mpcqp_solve_box_ws (BASELINE configs 3 and 5: the per-step QP of
+// session_4/main.py:115-116 with the input box main.py:68-69 and the state
+// box main.py:58-61).
+//
+// gi_mixed keeps the current swept matrix M = SWEEP_P(M0) (P = fixed z and
+// active rows, M0 = SWEEP_z(K) from sweep.hip) in registers and applies one
+// rank-1 sweep of the whole (n+m)^2 matrix per iteration, behind workgroup
+// barriers.  With S = -M0[P,P] (positive definite while the active
+// constraints are independent) every entry that iteration needs follows from
+// M0 and S^-1 alone:
+//     M[i,p] = M0[i,p] + M0[i,P] v,      v = S^-1 M0[P,p]        (i, p not in P)
+//     M[a,p] = -s_a v_a                  (a in P; s_a = -1 fixed z, +1 active row)
+//     M[a,b] = s_a s_b S^-1[a,b]
+// so an iteration reads column p and the |P| active columns of M0 (rows of
+// the symmetric dense M0, coalesced), and updates S^-1 by a bordered-inverse
+// rank-1 step (add) or a Schur rank-1 step (drop): O((n+m)|P| + |P|^2)
+// instead of O((n+m)^2), with no barrier and with register state small
+// enough for several instances per SIMD.
+//
+// Layout: index i = lane + 64 r (r < NR); slot j of the active set = lane j,
+// which holds row j of S^-1 in 64 registers (unused slots are zero rows and
+// columns), the index a_j and its bound.  More than 64 active constraints
+// (n > 64 only) hands the instance to the workgroup kernel (kStatusRetry).
+// The refinement (iterative refinement of the final active set against the
+// ORIGINAL H, G with fp64 accumulation) follows gi_mixed.
+#include "common.hpp"
+
+namespace mpcqp {
+
+constexpr int kSlots = 64;
+constexpr int kStatusRetry = 0x7f;  // internal: hand the instance to qp_wg_kernel
+
+struct PfArgs {
+  int batch, n, m;
+  const float* H; int64_t sH;  // packed lower n x n (refinement)
+  const float* f; int64_t sf;
+  const float* G; int64_t sG;  // m x n row-major (refinement)
+  const float* hl; const float* hu; int64_t sh;
+  const float* lb; int64_t sLb;
+  const float* ub; int64_t sUb;
+  const float* M0;             // sweep.hip full output, (n+m)^2 per instance
+  float* z; float* y; int32_t* status;
+  int* retry_count; int* retry_list;
+  int max_iter, refine;
+  float tol;
+};
+
+__device__ __forceinline__ float bperm(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(lane << 2, __float_as_int(v)));
+}
+
+template <int NR, typename V>
+__device__ __forceinline__ V pick(const V (&x)[NR], int i) {
+  // value at index i (uniform) from lane i % 64, register i / 64
+  V v = x[0];
+#pragma unroll
+  for (int r = 1; r < NR; ++r) v = ((i >> 6) == r) ? x[r] : v;
+  return readlane(v, i & 63);
+}
+
+template <int NR>
+__global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
+  __shared__ float xb[NR * kWave];
+  __shared__ double red[8 * kWave];
+  __shared__ double rsum[NR * kWave];
+  const int b = blockIdx.x, l = threadIdx.x;
+  const int n = a.n, m = a.m, nt = n + m;
+  const float* M0 = a.M0 + (int64_t)b * nt * nt;
+  const float* fb = a.f + (int64_t)b * a.sf;
+  const float inf = Lim<float>::inf();
+  const int pre = a.status[b];  // sweep status
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
+
+  float lo[NR], hi[NR], sl[NR], su[NR], fz[NR], scl[NR], val[NR], mu[NR], s0[NR];
+  int st[NR], slot[NR];
+  bool bad = false, nonfin = false;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int i = l + kWave * r;
+    float lv = -inf, uv = inf, fi = 0.f;
+    if (i < n) {
+      if (a.lb) lv = a.lb[(int64_t)b * a.sLb + i];
+      if (a.ub) uv = a.ub[(int64_t)b * a.sUb + i];
+      fi = fb[i];
+    } else if (i < nt) {
+      if (a.hl) lv = a.hl[(int64_t)b * a.sh + (i - n)];
+      if (a.hu) uv = a.hu[(int64_t)b * a.sh + (i - n)];
+    }
+    bad |= i < nt && (!(lv <= uv) || lv == inf || uv == -inf);
+    nonfin |= !finite(fi);
+    lo[r] = lv;
+    hi[r] = uv;
+    fz[r] = fi;
+    sl[r] = finite(lv) ? 1.f / (1.f + fabsf(lv)) : __builtin_nanf("");
+    su[r] = finite(uv) ? 1.f / (1.f + fabsf(uv)) : __builtin_nanf("");
+    st[r] = i < nt ? 0 : 3;
+    slot[r] = -1;
+    val[r] = 0.f;
+    mu[r] = 0.f;
+    scl[r] = i < nt ? fabsf(M0[(int64_t)i * nt + i]) : 0.f;
+    s0[r] = 0.f;
+  }
+  // active-set slots: lane j = slot j
+  int aidx = -1, sisz = 0;
+  float sbnd = 0.f;
+  float S[kSlots];
+#pragma unroll
+  for (int j = 0; j < kSlots; ++j) S[j] = 0.f;
+  uint64_t used = 0;
+
+  int code = MPCQP_STATUS_OPTIMAL, iters = 0;
+  if (pre) {
+    code = pre;
+  } else if (__builtin_amdgcn_ballot_w64(nonfin)) {
+    code = MPCQP_STATUS_NONFINITE;
+  } else if (__builtin_amdgcn_ballot_w64(bad)) {
+    code = MPCQP_STATUS_INFEASIBLE;
+  }
+  if (code != MPCQP_STATUS_OPTIMAL) goto out;
+
+  {
+    const float dep_tol = 2e-5f;
+    // ---------------------------------------------------------- helpers
+    // value at index a_j in lane j (0 in unused slots)
+    auto gather = [&](const float (&x)[NR]) -> float {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) xb[l + kWave * r] = x[r];
+      __syncthreads();
+      const float v = aidx >= 0 ? xb[aidx] : 0.f;
+      __syncthreads();
+      return v;
+    };
+    // lane i: (S^-1 t)_i
+    auto smul = [&](float t) -> float {
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < kSlots; ++j) q = fmaf(S[j], readlane(t, j), q);
+      return q;
+    };
+    // out += sum_t c_t M0[row_t, :] for kB rows at a time: every row's loads
+    // are issued before the first FMA (one memory round trip per batch)
+    constexpr int kB = 8;
+    auto axpy_rows = [&](const int (&row)[kB], const float (&c)[kB], float (&out)[NR]) {
+      float v[kB][NR];
+#pragma unroll
+      for (int t = 0; t < kB; ++t) {
+        const float* rp = M0 + (int64_t)row[t] * nt;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int i = l + kWave * r;
+          v[t][r] = i < nt ? rp[i] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < kB; ++t)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) out[r] = fmaf(c[t], v[t][r], out[r]);
+    };
+    // out += sign * M0[:, P] q  (rows a_j of the symmetric M0); fixed_z_f:
+    // coefficient -f_a on the fixed z instead (rows contribute nothing)
+    auto pcols = [&](float q, float (&out)[NR], float sign, bool fixed_z_f) {
+      uint64_t mm = used;
+      while (mm) {
+        int row[kB];
+        float c[kB];
+#pragma unroll
+        for (int t = 0; t < kB; ++t) {
+          row[t] = 0;
+          c[t] = 0.f;
+          if (mm) {
+            const int j = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            const int aj = readlane(aidx, j);
+            row[t] = aj;
+            c[t] = fixed_z_f ? (aj < n ? -fb[aj] : 0.f) : sign * readlane(q, j);
+          }
+        }
+        axpy_rows(row, c, out);
+      }
+    };
+    // out += M0[:, z] c_z with c_z = coef(j) for j < n
+    auto zcols = [&](auto&& coef, float (&out)[NR]) {
+      for (int j0 = 0; j0 < n; j0 += kB) {
+        int row[kB];
+        float c[kB];
+#pragma unroll
+        for (int t = 0; t < kB; ++t) {
+          const int j = j0 + t;
+          row[t] = j < n ? j : 0;
+          c[t] = j < n ? coef(j) : 0.f;
+        }
+        axpy_rows(row, c, out);
+      }
+    };
+    // exact state from s = M w (gi_mixed refresh) in product form:
+    //   y = M0[:, Pc] w_Pc = s0 - M0[:, fixed z] f,  q = S^-1 (y_P - w'_P),
+    //   (Ms w')_i = y_i + M0[i, P] q (i not in P), -q_i (i in P);  s = J_R Ms w'
+    auto refresh = [&]() {
+      float yv[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) yv[r] = s0[r];
+      pcols(0.f, yv, 1.f, true);
+      const float ys = gather(yv);
+      const float t = aidx >= 0 ? ys - (sisz ? sbnd : -sbnd) : 0.f;
+      const float q = smul(t);
+      pcols(q, yv, 1.f, false);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int i = l + kWave * r;
+        const bool isz = i < n;
+        const bool act = st[r] == 1 || st[r] == 2;
+        const float qi = bperm(q, slot[r] < 0 ? 0 : slot[r]);
+        const float msw = act ? -qi : yv[r];
+        const float s = (act && isz) ? -msw : msw;
+        const float bnd = (st[r] == 1) ? lo[r] : hi[r];
+        const float mval = isz ? fz[r] - s : s;
+        const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
+        val[r] = act ? bnd : (isz ? s : -s);
+        mu[r] = act ? sside * mval : 0.f;
+      }
+    };
+    auto scan = [&](float& viol, int& p) {
+      viol = -inf;
+      p = 0;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int i = l + kWave * r;
+        const float vl = (lo[r] - val[r]) * sl[r];  // NaN (never wins) for infinite bounds
+        const float vu = (val[r] - hi[r]) * su[r];
+        float v = (st[r] == 0) ? fmaxf(vl, vu) : -inf;
+        v = (v == v) ? v : -inf;
+        const bool take = v > viol;
+        viol = take ? v : viol;
+        p = take ? i : p;
+      }
+      wave_argmax(viol, p);
+      p = uniform(p);
+      viol = readlane(viol, 0);
+    };
+    // S^-1 of P + {p}: bordered inverse, S^-1 += w w' / sigma with w = v
+    // and w_snew = 1 (row/column snew were zero)
+    auto s_add = [&](float v, int snew, float sigma) {
+      const float w = (l == snew) ? 1.f : v;
+      const float is = 1.f / sigma;
+#pragma unroll
+      for (int j = 0; j < kSlots; ++j) S[j] = fmaf(w, readlane(w, j) * is, S[j]);
+    };
+    // S^-1 of P - {slot q}: Schur step, then row/column q exactly zero
+    auto s_drop = [&](int q, float dqq) {
+      float rq = 0.f;
+#pragma unroll
+      for (int j = 0; j < kSlots; ++j) {
+        const float rj = readlane(S[j], q);
+        rq = (l == j) ? rj : rq;
+      }
+      const float c = -rq / dqq;
+#pragma unroll
+      for (int j = 0; j < kSlots; ++j) {
+        const float rj = readlane(S[j], q);
+        S[j] = (l == q || j == q) ? 0.f : fmaf(c, rj, S[j]);
+      }
+    };
+    auto s_diag = [&](int q) -> float {
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < kSlots; ++j) d = (j == q) ? readlane(S[j], q) : d;
+      return d;
+    };
+
+    // ---------------------------------------------- s0 = M0[:, z] f
+    zcols([&](int j) { return fb[j]; }, s0);
+
+    MPCQP_PHASE(0);
+    refresh();
+    MPCQP_PHASE(1);
+    bool active = true;
+    for (int pass = 0; pass < 3 && active; ++pass) {
+      while (true) {
+        float viol;
+        int p;
+        scan(viol, p);
+        if (!(viol > a.tol)) break;
+        const float valp0 = pick<NR>(val, p);
+        float valp = valp0;
+        const float lop = pick<NR>(lo, p), hip = pick<NR>(hi, p);
+        const int side = (valp < lop) ? 1 : 2;
+        const float tgt = (side == 1) ? lop : hip;
+        const bool pz = p < n;
+        const float epsp = pz ? -1.f : 1.f;
+        const float sidesign = ((side == 1) ? 1.f : -1.f) * (pz ? 1.f : -1.f);
+        const float sgn = (tgt > valp) ? 1.f : -1.f;
+        const float scp = pick<NR>(scl, p);
+        float tau = 0.f;
+        bool added = false;
+        while (!added) {
+          if (++iters > a.max_iter) {
+            code = MPCQP_STATUS_MAXITER;
+            goto out;
+          }
+          // column p of the current M
+          float col[NR];
+          {
+            const float* row = M0 + (int64_t)p * nt;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+              const int i = l + kWave * r;
+              col[r] = i < nt ? row[i] : 0.f;
+            }
+          }
+          MPCQP_PHASE(2);
+          const float u = gather(col);
+          const float v = smul(u);
+          MPCQP_PHASE(3);
+          pcols(v, col, 1.f, false);
+          MPCQP_PHASE(4);
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            const bool act = st[r] == 1 || st[r] == 2;
+            const float vs = bperm(v, slot[r] < 0 ? 0 : slot[r]);
+            col[r] = act ? ((i < n) ? vs : -vs) : col[r];
+          }
+          const float mpp = pick<NR>(col, p);
+          const bool dep = !(-mpp > dep_tol * scp);
+          const float dtds = dep ? sidesign : sgn * epsp * fast_rcp(mpp);
+          const float t2 = dep ? inf : fabsf(tgt - valp);
+          float ti = inf;
+          int k = 0;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            const bool act = st[r] == 1 || st[r] == 2;
+            const float dq = col[r] * dtds;
+            const float dmu = act ? ((st[r] == 1) ? dq : -dq) : 0.f;
+            float t = (act && dmu < 0.f) ? -mu[r] / dmu : inf;
+            t = (t == t) ? t : inf;
+            const bool take = t < ti;
+            ti = take ? t : ti;
+            k = take ? i : k;
+          }
+          wave_argmin(ti, k);
+          k = uniform(k);
+          ti = readlane(ti, 0);
+          if (!(ti < inf) && !(t2 < inf)) {
+            code = MPCQP_STATUS_INFEASIBLE;
+            goto out;
+          }
+          const bool partial = ti < t2;
+          const float s_eff = partial ? ti : t2;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            const bool act = st[r] == 1 || st[r] == 2;
+            const float dq = col[r] * dtds;
+            const float dmu = act ? ((st[r] == 1) ? dq : -dq) : 0.f;
+            const float dval = (st[r] == 0) ? ((i < n) ? -dq : dq) : 0.f;
+            val[r] = fmaf(s_eff, dval, val[r]);
+            mu[r] = fmaf(s_eff, dmu, mu[r]);
+          }
+          tau = fmaf(s_eff, dtds, tau);
+          MPCQP_PHASE(5);
+          if (partial) {
+            // k leaves the active set
+            if (!dep) valp = fmaf(sgn, s_eff, valp);
+            const int q = uniform(pick<NR>(slot, k));
+            const float d = s_diag(q);
+            if (!(d > 0.f)) {
+              code = MPCQP_STATUS_NOT_CONVEX;
+              goto out;
+            }
+            s_drop(q, d);
+            used &= ~(1ull << q);
+            if (l == q) aidx = -1;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+              const bool me = l + kWave * r == k;
+              st[r] = me ? 0 : st[r];
+              mu[r] = me ? 0.f : mu[r];
+              slot[r] = me ? -1 : slot[r];
+            }
+          } else {
+            // p joins the active set
+            if (!(mpp < 0.f)) {
+              code = MPCQP_STATUS_NOT_CONVEX;
+              goto out;
+            }
+            if (~used == 0) {
+              code = kStatusRetry;
+              goto out;
+            }
+            const int snew = __builtin_ctzll(~used);
+            s_add(v, snew, -mpp);
+            used |= 1ull << snew;
+            if (l == snew) {
+              aidx = p;
+              sbnd = tgt;
+              sisz = pz ? 1 : 0;
+            }
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+              const bool me = l + kWave * r == p;
+              st[r] = me ? side : st[r];
+              mu[r] = me ? sidesign * tau : mu[r];
+              val[r] = me ? tgt : val[r];
+              slot[r] = me ? snew : slot[r];
+            }
+          }
+          added = !partial;
+          MPCQP_PHASE(6);
+        }
+      }
+      MPCQP_PHASE(2);
+      refresh();
+      MPCQP_PHASE(1);
+      {
+        float viol;
+        int p;
+        scan(viol, p);
+        active = viol > a.tol;
+      }
+    }
+    if (active) code = MPCQP_STATUS_MAXITER;
+    MPCQP_PHASE(2);
+
+    // ------------------------------------------- iterative refinement
+    const float* Hb = a.H + (int64_t)b * a.sH;
+    const float* Gb = m ? a.G + (int64_t)b * a.sG : nullptr;
+    for (int it = 0; it < a.refine; ++it) {
+      float x[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int i = l + kWave * r;
+        const bool isz = i < n;
+        const bool act = st[r] == 1 || st[r] == 2;
+        const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
+        x[r] = (st[r] == 3) ? 0.f : (isz ? val[r] : (act ? sside * mu[r] : 0.f));
+      }
+      // yk = K x in fp64, K = [[H, G'], [G, 0]]: row sweeps over packed H
+      // and over G; the row-direction sums reduce 8 rows at a time in LDS
+      double yk[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) yk[r] = 0.0;
+      for (int r = l; r < NR * kWave; r += kWave) rsum[r] = 0.0;
+      for (int j0 = 0; j0 < nt; j0 += 8) {
+        // 8 rows of K: H row j (lanes i <= j of packed H) or G row j - n
+        float hv[8][NR];
+        double xj[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int j = j0 + t;
+          const float* rp = j < n ? Hb + (int64_t)j * (j + 1) / 2
+                                  : (j < nt ? Gb + (int64_t)(j - n) * n : Hb);
+          const int lim = j < n ? j : (j < nt ? n - 1 : -1);
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            hv[t][r] = i <= lim ? rp[i] : 0.f;
+          }
+          xj[t] = j < nt ? (double)pick<NR>(x, j) : 0.0;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int j = j0 + t;
+          double part = 0.0;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            const double h = hv[t][r];
+            // H row: the diagonal counts once (through yk); G row: all z
+            part = (j >= n || i < j) ? fma(h, (double)x[r], part) : part;
+            yk[r] = fma(h, xj[t], yk[r]);
+          }
+          red[t * kWave + l] = part;
+        }
+        __syncthreads();
+        {
+          const int rr = l & 7, qq = l >> 3;
+          double s = 0.0;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) s += red[rr * kWave + qq * 8 + t];
+          s += __shfl_xor(s, 8, kWave);
+          s += __shfl_xor(s, 16, kWave);
+          s += __shfl_xor(s, 32, kWave);
+          if (qq == 0 && j0 + rr < nt) rsum[j0 + rr] += s;
+        }
+        __syncthreads();
+      }
+      float w[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int i = l + kWave * r;
+        const bool isz = i < n;
+        const bool act = st[r] == 1 || st[r] == 2;
+        const double yi = yk[r] + rsum[i < NR * kWave ? i : 0];
+        const double bnd = (st[r] == 1) ? (double)lo[r] : (double)hi[r];
+        const bool inS = isz ? (st[r] == 0) : act;
+        const double e = isz ? yi + (double)fz[r] : yi - bnd;
+        w[r] = (inS && i < nt) ? (float)e : 0.f;
+      }
+      __syncthreads();
+      // sv = M w (w on free z and active rows): y2 = M0[:, free z] w
+      float y2[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) y2[r] = 0.f;
+      zcols([&](int j) { return pick<NR>(w, j); }, y2);
+      const float ys = gather(y2);
+      const float wsl = gather(w);
+      const float q = smul(aidx >= 0 ? ys - wsl : 0.f);
+      pcols(q, y2, 1.f, false);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int i = l + kWave * r;
+        const bool isz = i < n;
+        const bool act = st[r] == 1 || st[r] == 2;
+        const float qi = bperm(q, slot[r] < 0 ? 0 : slot[r]);
+        const float sv = act ? -qi : y2[r];
+        const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
+        val[r] = (isz && st[r] == 0) ? val[r] + sv : val[r];
+        mu[r] = (!isz && act) ? mu[r] + sside * sv : mu[r];
+      }
+    }
+  }
+out:
+  MPCQP_PHASE(7);
+  {
+    const bool ok = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int i = l + kWave * r;
+      const bool isz = i < n;
+      const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
+      const float lam = (st[r] == 1 || st[r] == 2) ? sside * mu[r] : 0.f;
+      if (code == kStatusRetry) continue;
+      if (isz) a.z[(int64_t)b * n + i] = ok ? fminf(fmaxf(val[r], lo[r]), hi[r]) : __builtin_nanf("");
+      else if (a.y && i < nt) a.y[(int64_t)b * m + (i - n)] = ok ? lam : __builtin_nanf("");
+    }
+    if (l == 0) {
+      a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
+      if (code == kStatusRetry) a.retry_list[atomicAdd(a.retry_count, 1)] = b;
+    }
+  }
+#ifdef MPCQP_PHASE_TIMING
+  mpcqp_clk.flush();
+#endif
+}
+
+int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
+              const float* G, int64_t sG, const float* hl, const float* hu, int64_t sh,
+              const float* lb, int64_t sLb, const float* ub, int64_t sUb, const float* M0,
+              float* z, float* y, int32_t* status, int* retry_count, int* retry_list,
+              int max_iter, int refine, float tol, hipStream_t st) {
+  PfArgs a{batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, M0, z, y, status,
+           retry_count, retry_list, max_iter, refine, tol};
+  if (n + m <= 2 * kWave)
+    hipLaunchKernelGGL((qp_pf_kernel<2>), dim3(batch), dim3(kWave), 0, st, a);
+  else
+    hipLaunchKernelGGL((qp_pf_kernel<3>), dim3(batch), dim3(kWave), 0, st, a);
+  MPCQP_CHECK_LAUNCH("qp_pf_kernel");
+  return MPCQP_OK;
+}
+
+}  // namespace mpcqp
+
+#ifdef MPCQP_PHASE_TIMING
+MPCQP_DEBUG_PHASE_READER(mpcqp_debug_phase_cycles_pf)
+#endif

@@ -12,13 +12,16 @@
 // Per instance: stage K = [[H, G'], [G, 0]] into registers, sweep every z
 // index in (K -> [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']], i.e. the dual
 // matrix comes for free), then run the mixed primal/dual active set.
+#include <cstdlib>
+
 #include "wg.hpp"
 
 namespace mpcqp {
 
 int sweep_tiles(int dtype, int n, int m);
 int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void* G, int64_t sG,
-                 void* M, int32_t* status, hipStream_t st);
+                 void* M, int full, int32_t* status, hipStream_t st);
+int hip_fail(hipError_t e, const char* where);
 
 template <typename T>
 struct QpArgs {
@@ -33,9 +36,12 @@ struct QpArgs {
   int max_iter;
   int refine;
   T tol;
-  // pre-swept M (sweep.hip: packed lower over n + m, stride (n+m)(n+m+1)/2)
+  // pre-swept M (sweep.hip, full: dense (n+m) x (n+m) row-major per instance)
   // and its per-instance status in status[]; nullptr: sweep in the kernel
   const T* Ms;
+  // retry mode (solve_pf.hip hand-off): solve only the instances listed
+  const int* retry_count;
+  const int* retry_list;
 };
 
 // Pivots per barrier in the initial sweep-in: the replicas cost BK*(BR+BC)
@@ -49,8 +55,7 @@ struct QpBlock {
 // Two waves per SIMD: a 512-thread workgroup fits once per CU, a 256-thread
 // one twice (VGPR budget 256).
 template <typename T, class S>
-__global__ __launch_bounds__(S::threads) __attribute__((amdgpu_waves_per_eu(2)))
-void qp_wg_kernel(QpArgs<T> a) {
+__device__ __forceinline__ void qp_wg_body(const QpArgs<T>& a, const int b) {
   using L = WLds<T, S>;
   constexpr int BR = S::BR, BC = S::BC;
   constexpr int NMAX = L::NMAX;
@@ -59,7 +64,6 @@ void qp_wg_kernel(QpArgs<T> a) {
   T* lo = sm + L::oLo;
   T* hi = sm + L::oHi;
   T* fs = sm + L::oF;
-  const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int n = a.n, m = a.m, nt = n + m;
   const T inf = Lim<T>::inf();
@@ -68,7 +72,7 @@ void qp_wg_kernel(QpArgs<T> a) {
   PhaseClock mpcqp_clk;
 #endif
   // status written by the pre-sweep (read before anyone writes it back)
-  const int pre = a.Ms ? a.status[b] : 0;
+  const int pre = (a.Ms && !a.retry_list) ? a.status[b] : 0;
   int bad = 0, nonfin = 0;
   for (int i = tid; i < NMAX; i += S::threads) {
     T l = -inf, u = inf, fi = T(0);
@@ -92,7 +96,7 @@ void qp_wg_kernel(QpArgs<T> a) {
   M.init(tid);
   const T* Hb = a.H + (int64_t)b * a.sH;
   const T* Gb = a.G ? a.G + (int64_t)b * a.sG : nullptr;
-  const T* Mb = a.Ms ? a.Ms + (int64_t)b * ((int64_t)nt * (nt + 1) / 2) : nullptr;
+  const T* Mb = a.Ms ? a.Ms + (int64_t)b * ((int64_t)nt * nt) : nullptr;
 #pragma unroll
   for (int r = 0; r < BR; ++r)
 #pragma unroll
@@ -100,7 +104,7 @@ void qp_wg_kernel(QpArgs<T> a) {
       const int i = M.bi * BR + r, j = M.bj * BC + c;
       T v = T(0);
       if (Mb) {
-        if (i < nt && j < nt) v = (j <= i) ? Mb[i * (i + 1) / 2 + j] : Mb[j * (j + 1) / 2 + i];
+        if (i < nt && j < nt) v = Mb[(int64_t)i * nt + j];
       } else if (i < n && j < n) {
         v = (j <= i) ? Hb[i * (i + 1) / 2 + j] : Hb[j * (j + 1) / 2 + i];
       } else if (i < nt && j < n) {
@@ -191,9 +195,30 @@ void qp_wg_kernel(QpArgs<T> a) {
 }
 
 template <typename T, class S>
+__global__ __launch_bounds__(S::threads) __attribute__((amdgpu_waves_per_eu(2)))
+void qp_wg_kernel(QpArgs<T> a) {
+  qp_wg_body<T, S>(a, blockIdx.x);
+}
+
+// hand-offs of solve_pf.hip: persistent workgroups walk the list
+template <typename T, class S>
+__global__ __launch_bounds__(S::threads) __attribute__((amdgpu_waves_per_eu(2)))
+void qp_wg_retry_kernel(QpArgs<T> a) {
+  const int cnt = *a.retry_count;
+  for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
+    qp_wg_body<T, S>(a, a.retry_list[t]);
+    __syncthreads();
+  }
+}
+
+template <typename T, class S>
 static int launch_qp_bs(const QpArgs<T>& a, hipStream_t st) {
   const size_t bytes = (size_t)WLds<T, S>::total * sizeof(T);
-  hipLaunchKernelGGL((qp_wg_kernel<T, S>), dim3(a.batch), dim3(S::threads), bytes, st, a);
+  if (a.retry_list)  // one persistent workgroup per CU walks the hand-off list
+    hipLaunchKernelGGL((qp_wg_retry_kernel<T, S>), dim3(a.batch < 256 ? a.batch : 256),
+                       dim3(S::threads), bytes, st, a);
+  else
+    hipLaunchKernelGGL((qp_wg_kernel<T, S>), dim3(a.batch), dim3(S::threads), bytes, st, a);
   MPCQP_CHECK_LAUNCH("qp_wg_kernel");
   return MPCQP_OK;
 }
@@ -226,7 +251,8 @@ static int solve_qp_t(int batch, int n, int m, const void* H, int64_t sH, const 
                       int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
                       int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
                       void* z, void* y, int32_t* status, int max_iter, double tol,
-                      hipStream_t st, const void* Ms = nullptr) {
+                      hipStream_t st, const void* Ms = nullptr,
+                      const int* retry_count = nullptr, const int* retry_list = nullptr) {
   QpArgs<T> a;
   a.batch = batch; a.n = n; a.m = m;
   a.H = (const T*)H; a.sH = sH;
@@ -241,6 +267,8 @@ static int solve_qp_t(int batch, int n, int m, const void* H, int64_t sH, const 
   a.refine = sizeof(T) == 4 ? 2 : 1;
   a.tol = tol > 0 ? (T)tol : (sizeof(T) == 8 ? (T)1e-12 : (T)1e-6);
   a.Ms = (const T*)Ms;
+  a.retry_count = retry_count;
+  a.retry_list = retry_list;
   return launch_qp<T>(a, st);
 }
 
@@ -256,14 +284,59 @@ int solve_box_wg(int dtype, int batch, int n, const void* H, int64_t sH, const v
                            ub, sUb, z, nullptr, status, max_iter, tol, st, Ms);
 }
 
-// Workspace of the two-kernel path (MFMA pre-sweep + qp_wg_kernel): the
-// packed swept matrix per instance, or 0 where that path does not apply
-// (fp64, or n + m within the 256-thread kernel where the in-kernel sweep is
-// cheap).
+// Workspace of the two-kernel path (MFMA pre-sweep -> product-form active
+// set -> workgroup kernel for hand-offs): the dense swept matrix per
+// instance, then the hand-off counter and list; 0 where that path does not
+// apply (fp64, or n + m within the 256-thread kernel where the in-kernel
+// sweep is cheap).
+static size_t ws_m0_bytes(int batch, int n, int m) {
+  const size_t nt = (size_t)(n + m);
+  return ((size_t)batch * nt * nt * sizeof(float) + 255) / 256 * 256;
+}
+
 size_t qp_ws_bytes(int dtype, int batch, int n, int m) {
   if (batch <= 0 || n + m <= 64 || sweep_tiles(dtype, n, m) == 0) return 0;
-  const size_t nt = (size_t)(n + m);
-  return (size_t)batch * (nt * (nt + 1) / 2) * sizeof(float);
+  return ws_m0_bytes(batch, n, m) + 256 + (size_t)batch * sizeof(int);
+}
+
+int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
+              const float* G, int64_t sG, const float* hl, const float* hu, int64_t sh,
+              const float* lb, int64_t sLb, const float* ub, int64_t sUb, const float* M0,
+              float* z, float* y, int32_t* status, int* retry_count, int* retry_list,
+              int max_iter, int refine, float tol, hipStream_t st);
+
+// refinement steps of the product-form kernel (MPCQP_PF_REFINE overrides;
+// a tuning knob, default 1: the fp64 residual against the original data
+// brings z to the fp32 data floor in one step)
+static int pf_refine() {
+  const char* v = getenv("MPCQP_PF_REFINE");
+  return v ? atoi(v) : 1;
+}
+
+// fp32, n + m > 64: sweep (MFMA) -> product-form active set, one instance per
+// wavefront -> qp_wg_kernel for the instances with more than 64 active
+// constraints (none at configs 3 and 5).
+int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const void* f,
+                     int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
+                     int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
+                     void* z, void* y, int32_t* status, int max_iter, double tol, void* ws,
+                     hipStream_t st) {
+  char* w = (char*)ws;
+  float* M0 = (float*)w;
+  int* cnt = (int*)(w + ws_m0_bytes(batch, n, m));
+  int* list = cnt + 64;
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int), st);
+  if (e != hipSuccess) return hip_fail(e, "mpcqp_solve_qp_ws: hipMemsetAsync");
+  int rc = sweep_launch(batch, n, m, H, sH, G, sG, M0, 1, status, st);
+  if (rc != MPCQP_OK) return rc;
+  const int mi = max_iter > 0 ? max_iter : 3 * (n + m) + 30;
+  const float tl = tol > 0 ? (float)tol : 1e-6f;
+  rc = launch_pf(batch, n, m, (const float*)H, sH, (const float*)f, sf, (const float*)G, sG,
+                 (const float*)hl, (const float*)hu, sh, (const float*)lb, sLb, (const float*)ub,
+                 sUb, M0, (float*)z, (float*)y, status, cnt, list, mi, pf_refine(), tl, st);
+  if (rc != MPCQP_OK) return rc;
+  return solve_qp_t<float>(batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, z, y,
+                           status, max_iter, tol, st, M0, cnt, list);
 }
 
 int max_qp_size_dtype(int dtype) {
@@ -322,11 +395,9 @@ extern "C" int mpcqp_solve_qp_ws(int dtype, int batch, int n, int m, const void*
   MPCQP_CHECK_ARG(strideH >= 0 && stridef >= 0 && strideG >= 0 && strideh >= 0 &&
                       strideLb >= 0 && strideUb >= 0,
                   "mpcqp_solve_qp_ws: negative stride");
-  hipStream_t st = (hipStream_t)stream;
-  int rc = sweep_launch(batch, n, m, H, strideH, G, strideG, ws, status, st);
-  if (rc != MPCQP_OK) return rc;
-  return solve_qp_t<float>(batch, n, m, H, strideH, f, stridef, G, strideG, hl, hu, strideh, lb,
-                           strideLb, ub, strideUb, z, y, status, max_iter, tol, st, ws);
+  return solve_two_kernel(batch, n, m, H, strideH, f, stridef, G, strideG, hl, hu, strideh, lb,
+                          strideLb, ub, strideUb, z, y, status, max_iter, tol, ws,
+                          (hipStream_t)stream);
 }
 
 #ifdef MPCQP_PHASE_TIMING

@@ -7,12 +7,14 @@
 // before its first iteration.  In qp_wg_kernel this is n rank-1 updates of
 // the (n+m)^2 matrix, each behind a barrier (65 % of config 5's solve time).
 // Here it is the same sweep in 16-pivot blocks: per block k, with
-// D = M_kk, R_i = M_ki (the block row) and Ds = SWEEP(D) = -D^-1,
-//     M_ij += R_i' (Ds R_j)        (i >= j, both != k)   -- MFMA
-//     M_ki  = D^-1 R_i  (i < k),   M_ik = R_i' D^-1 (i > k),   M_kk = Ds
-// which is Goodnight's a_ij - a_ik a_kj / a_kk with a_kk -> D.  Sweeping every
-// z block leaves M above (the 16 x 16 SWEEP(D) runs on the VALU with DPP
-// row_newbcast / ds_bpermute broadcasts).
+// D = M_kk = L L' (Cholesky), R_i = M_ki (the block row), W_i = L^-1 R_i,
+//     M_ij -= W_i' W_j             (i >= j, both != k)   -- MFMA
+//     M_ki  = L^-T W_i  (i < k),   M_ik = W_i' L^-1 (i > k),   M_kk = -L^-T L^-1
+// which is Goodnight's a_ij - a_ik a_kj / a_kk with a_kk -> D, in the
+// symmetric square-root form (as accurate as the unblocked sweep; the
+// explicit-D^-1 form is not).  Sweeping every z block leaves M above (L^-1 of
+// each 16 x 16 block runs on the VALU with DPP row_newbcast / ds_bpermute
+// broadcasts).
 //
 // Layout: one instance per wavefront, the lower block triangle of the padded
 // matrix held as T(T+1)/2 MFMA C-layout tiles in registers (mfma.hpp: lane
@@ -23,8 +25,8 @@
 // with identity pivots (sweeping a decoupled unit pivot changes nothing
 // else), rows at np..np+m-1.  T = ceil((np + m) / 16) <= 12.
 //
-// Input H packed lower (n(n+1)/2), G (m x n) row-major; output M packed lower
-// over the original n + m indices.  status[b]: 0, MPCQP_STATUS_NOT_CONVEX (a
+// Input H packed lower (n(n+1)/2), G (m x n) row-major; output M over the
+// original n + m indices, packed lower or (full) dense row-major.  status[b]: 0, MPCQP_STATUS_NOT_CONVEX (a
 // pivot <= 0: H not positive definite) or MPCQP_STATUS_NONFINITE;
 // mpcqp_solve_qp_ws / mpcqp_solve_box_ws consume M and that status.
 #include "common.hpp"
@@ -33,7 +35,7 @@
 namespace mpcqp {
 
 struct SweepArgs {
-  int batch, n, m, np, kp;
+  int batch, n, m, np, kp, full;
   const float* H; int64_t sH;
   const float* G; int64_t sG;
   float* M;
@@ -55,36 +57,41 @@ __device__ __forceinline__ float row_bcast(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + P, 0xf, 0xf, false));
 }
 
-// SWEEP of a symmetric 16 x 16 C-layout tile in place (-> -D^-1); bad |= a
-// pivot that is not > 0.
-__device__ __forceinline__ void sweep16(mf4& d, int g, int c, bool& bad) {
+// Inverse Cholesky factor of a symmetric positive definite 16 x 16 C-layout
+// tile: row operations that reduce A to L' (scale pivot row p by 1/sqrt(a_pp),
+// eliminate below it) applied to X = I leave X = L^-1 (A = L L').  bad |= a
+// pivot that is not > 0.  The blocked sweep below applies D^-1 = L^-T L^-1
+// as W' W with W = L^-1 R: forming D^-1 explicitly and multiplying by it
+// loses ~100x accuracy on ill-conditioned pivot blocks (config-3 Hessians).
+__device__ __forceinline__ void chol_inv16(mf4 a, mf4& x, int g, int c, bool& bad) {
 #pragma unroll
   for (int p = 0; p < 16; ++p) {
     const int gp = p >> 2, ip = p & 3;
-    const float piv = readlane(d[ip], 16 * gp + p);
+    const float piv = readlane(a[ip], 16 * gp + p);
     bad |= !(piv > 0.f);
-    const float inv = 1.f / piv;
+    const float r = 1.f / __builtin_sqrtf(piv);
     float col[4];
     switch (p) {  // row_newbcast needs an immediate lane
 #define MPCQP_RB(P_)                                               \
   case P_:                                                         \
-    for (int i = 0; i < 4; ++i) col[i] = row_bcast<P_>(d[i]);      \
+    for (int i = 0; i < 4; ++i) col[i] = row_bcast<P_>(a[i]);      \
     break;
       MPCQP_RB(0) MPCQP_RB(1) MPCQP_RB(2) MPCQP_RB(3) MPCQP_RB(4) MPCQP_RB(5) MPCQP_RB(6)
       MPCQP_RB(7) MPCQP_RB(8) MPCQP_RB(9) MPCQP_RB(10) MPCQP_RB(11) MPCQP_RB(12) MPCQP_RB(13)
       MPCQP_RB(14) MPCQP_RB(15)
 #undef MPCQP_RB
     }
-    // row p, column c: lane (gp, c), register ip
-    const float rowv = __int_as_float(
-        __builtin_amdgcn_ds_bpermute(4 * (16 * gp + c), __float_as_int(d[ip])));
-    const bool iscol = c == p;
+    // scaled pivot rows: lane (gp, c), register ip
+    const float ra = r * __int_as_float(
+        __builtin_amdgcn_ds_bpermute(4 * (16 * gp + c), __float_as_int(a[ip])));
+    const float rx = r * __int_as_float(
+        __builtin_amdgcn_ds_bpermute(4 * (16 * gp + c), __float_as_int(x[ip])));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float t = col[i] * inv;
-      const float gen = fmaf(-t, rowv, d[i]);
-      const bool isrow = (i == ip) && (g == gp);
-      d[i] = iscol ? (isrow ? -inv : t) : (isrow ? rowv * inv : gen);
+      const int R = 4 * g + i;
+      const float mlt = col[i] * r;
+      a[i] = (R == p) ? ra : (R > p ? fmaf(-mlt, ra, a[i]) : a[i]);
+      x[i] = (R == p) ? rx : (R > p ? fmaf(-mlt, rx, x[i]) : x[i]);
     }
   }
 }
@@ -166,70 +173,104 @@ void sweep_mfma_kernel(SweepArgs a) {
   for (int i = 0; i < 4; ++i) eye[i] = (4 * g + i == c) ? 1.f : 0.f;
   const mf4 zero = {0.f, 0.f, 0.f, 0.f};
 
-  // ---- blocked sweep over the z blocks
+  // ---- blocked sweep over the z blocks: with D = M_kk = L L', R_j = M_kj,
+  // W_j = L^-1 R_j:  M_ij -= W_i' W_j,  M_kj = L^-T W_j,  M_kk = -L^-T L^-1
 #pragma unroll
   for (int k = 0; k < T; ++k) {
     if (k < kp) {  // uniform
-      mf4 ds = t[tri(k, k)];
-      sweep16(ds, g, c, bad);
+      mf4 li = eye;
+      chol_inv16(t[tri(k, k)], li, g, c, bad);  // L^-1
       __builtin_amdgcn_sched_barrier(0);
-      mf4 R[T];
+      const mf4 lit = mm(li, eye, zero);  // L^-T (exact transpose)
+      mf4 W[T];
 #pragma unroll
       for (int i = 0; i < T; ++i) {
-        if (i < k) R[i] = t[tri(k, i)];
-        else if (i > k) R[i] = mm(t[tri(i, k)], eye, zero);  // M_ik' (exact)
+        if (i == k) continue;
+        const mf4 r = (i < k) ? t[tri(k, i)] : mm(t[tri(i, k)], eye, zero);  // M_ki
+        W[i] = mm(lit, r, zero);  // L^-1 M_ki
       }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < T; ++j) {
         if (j == k) continue;
-        const mf4 v = mm(ds, R[j], zero);  // Ds R_j = -D^-1 R_j (Ds symmetric)
+        const mf4 wn = -W[j];
 #pragma unroll
         for (int i = j; i < T; ++i)
-          if (i != k) t[tri(i, j)] = mm(R[i], v, t[tri(i, j)]);
-        if (j < k) t[tri(k, j)] = -v;
+          if (i != k) t[tri(i, j)] = mm(W[i], wn, t[tri(i, j)]);
         __builtin_amdgcn_sched_barrier(0);
       }
-      const mf4 dinv = -ds;
 #pragma unroll
-      for (int i = k + 1; i < T; ++i) t[tri(i, k)] = mm(R[i], dinv, zero);
-      t[tri(k, k)] = ds;
+      for (int i = 0; i < T; ++i) {
+        if (i < k) t[tri(k, i)] = mm(li, W[i], zero);        // L^-T W_i = D^-1 M_ki
+        else if (i > k) t[tri(i, k)] = mm(W[i], li, zero);   // W_i' L^-1 = M_ik D^-1
+      }
+      t[tri(k, k)] = mm(li, -li, zero);  // -L^-T L^-1 = -D^-1
     }
   }
 
-  // ---- store M packed lower over the original n + m indices
+  // ---- store M over the original n + m indices: packed lower, or full
+  // row-major (a.full: the product-form solver reads columns as rows)
   const bool fin_bad = __builtin_amdgcn_ballot_w64(nonfin) != 0;
   const bool piv_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
-  const rsrc_t rM = mk_rsrc(a.M + (int64_t)b * ((int64_t)nt * (nt + 1) / 2),
-                            (int64_t)nt * (nt + 1) / 2 * 4);
+  const int64_t msz = a.full ? (int64_t)nt * nt : (int64_t)nt * (nt + 1) / 2;
+  const rsrc_t rM = mk_rsrc(a.M + (int64_t)b * msz, msz * 4);
   // opaque lane id: keeps the load phase's index math from being CSE'd into
   // (and kept live until) the stores
   int ls = l;
   asm volatile("" : "+v"(ls));
   const int gs = ls >> 4, cs = ls & 15;
-  // tile-space column -> original column (pad: masked)
-  const unsigned czmask = (16 * (kp - 1) + cs < n) ? 0u : (unsigned)kOOB;     // last z tile column
-  const unsigned crmask = (16 * (T - 1) + cs - np < m) ? 0u : (unsigned)kOOB;  // last row tile column
+  auto orig = [&](int X) { return X < n ? X : (X < np ? -1 : (X - np < m ? n + X - np : -1)); };
+  if (!a.full) {
+    // tile-space column -> original column (pad: masked)
+    const unsigned czmask = (16 * (kp - 1) + cs < n) ? 0u : (unsigned)kOOB;     // last z tile column
+    const unsigned crmask = (16 * (T - 1) + cs - np < m) ? 0u : (unsigned)kOOB;  // last row tile column
 #pragma unroll
-  for (int ti = 0; ti < T; ++ti) {
-    unsigned base[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int R = 16 * ti + 4 * gs + i;
-      const int r = R < n ? R : (R < np ? -1 : (R - np < m ? n + R - np : -1));
-      base[i] = r >= 0 ? 4 * (r * (r + 1) / 2 + cs) : kOOB;
-    }
-#pragma unroll
-    for (int tj = 0; tj <= ti; ++tj) {
-      // column orig = C (z) or C - np + n (rows); diagonal tiles keep r >= c
-      const int shift = tj < kp ? 0 : 4 * (n - np);
-      const unsigned msk = (tj == kp - 1 ? czmask : 0u) | (tj == T - 1 && tj >= kp ? crmask : 0u);
+    for (int ti = 0; ti < T; ++ti) {
+      unsigned base[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const unsigned dm = (tj == ti && cs > 4 * gs + i) ? (unsigned)kOOB : 0u;
-        bst_i(t[tri(ti, tj)][i], rM, (base[i] + (unsigned)shift) | msk | dm, 64 * tj);
+        const int r = orig(16 * ti + 4 * gs + i);
+        base[i] = r >= 0 ? 4 * (r * (r + 1) / 2 + cs) : kOOB;
       }
-      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int tj = 0; tj <= ti; ++tj) {
+        // column orig = C (z) or C - np + n (rows); diagonal tiles keep r >= c
+        const int shift = tj < kp ? 0 : 4 * (n - np);
+        const unsigned msk = (tj == kp - 1 ? czmask : 0u) | (tj == T - 1 && tj >= kp ? crmask : 0u);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const unsigned dm = (tj == ti && cs > 4 * gs + i) ? (unsigned)kOOB : 0u;
+          bst_i(t[tri(ti, tj)][i], rM, (base[i] + (unsigned)shift) | msk | dm, 64 * tj);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
+  } else {
+    // tile (rb, cb) in C layout -> rows of block rb, columns of block cb;
+    // part: 0 all, 1 only c <= r (diagonal, from the lower tile), 2 only c > r
+    auto put = [&](const mf4& v, int rb, int cb, int part) {
+      const int cc = orig(16 * cb + cs);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rr = 4 * gs + i, r = orig(16 * rb + rr);
+        const bool keep = r >= 0 && cc >= 0 && (part == 0 || (part == 1 ? cs <= rr : cs > rr));
+        bst(v[i], rM, keep ? 4 * (r * nt + cc) : kOOB);
+      }
+    };
+#pragma unroll
+    for (int ti = 0; ti < T; ++ti)
+#pragma unroll
+      for (int tj = 0; tj <= ti; ++tj) {
+        const mf4 tt = mm(t[tri(ti, tj)], eye, zero);  // transpose (exact)
+        if (ti == tj) {
+          put(t[tri(ti, tj)], ti, tj, 1);
+          put(tt, ti, tj, 2);
+        } else {
+          put(t[tri(ti, tj)], ti, tj, 0);
+          put(tt, tj, ti, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
   }
   if (l == 0)
     a.status[b] = fin_bad ? MPCQP_STATUS_NONFINITE : (piv_bad ? MPCQP_STATUS_NOT_CONVEX : 0);
@@ -251,9 +292,9 @@ int sweep_tiles(int dtype, int n, int m) {
 }
 
 int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void* G, int64_t sG,
-                 void* M, int32_t* status, hipStream_t st) {
+                 void* M, int full, int32_t* status, hipStream_t st) {
   SweepArgs a;
-  a.batch = batch; a.n = n; a.m = m;
+  a.batch = batch; a.n = n; a.m = m; a.full = full ? 1 : 0;
   a.np = (n + 15) / 16 * 16;
   a.kp = a.np / 16;
   a.H = (const float*)H; a.sH = sH;
@@ -278,8 +319,8 @@ int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void*
 }  // namespace mpcqp
 
 extern "C" int mpcqp_sweep(int dtype, int batch, int n, int m, const void* H, int64_t strideH,
-                           const void* G, int64_t strideG, void* M, int32_t* status,
-                           void* stream) {
+                           const void* G, int64_t strideG, void* M, int full,
+                           int32_t* status, void* stream) {
   using namespace mpcqp;
   MPCQP_CHECK_ARG(dtype == MPCQP_F32, "mpcqp_sweep: only MPCQP_F32 runs on the MFMA sweep");
   MPCQP_CHECK_ARG(batch >= 0 && n >= 1 && m >= 0, "mpcqp_sweep: bad sizes");
@@ -288,5 +329,5 @@ extern "C" int mpcqp_sweep(int dtype, int batch, int n, int m, const void* H, in
   MPCQP_CHECK_ARG(sweep_tiles(dtype, n, m) > 0, "mpcqp_sweep: padded n + m = %d outside 65..192",
                   (n + 15) / 16 * 16 + m);
   if (batch == 0) return MPCQP_OK;
-  return sweep_launch(batch, n, m, H, strideH, G, strideG, M, status, (hipStream_t)stream);
+  return sweep_launch(batch, n, m, H, strideH, G, strideG, M, full, status, (hipStream_t)stream);
 }

@@ -31,40 +31,64 @@ def _swept(H, G=None):
     return np.block([[-Hi, Hi @ G.T], [G @ Hi, -G @ Hi @ G.T]])
 
 
+@pytest.mark.parametrize("full", [False, True])
 @pytest.mark.parametrize("n", [65, 80, 100, 150, 160, 192])
-def test_sweep_box(dev, n):
-    """M = -H^-1 for every tile count T = 5..12, ragged n included."""
+def test_sweep_box(dev, n, full):
+    """M = -H^-1 for every tile count T = 5..12, ragged n included; packed
+    and dense output."""
     rng = np.random.default_rng(300 + n)
     b = 4
     Hs = [_spd(rng, n) for _ in range(b)]
     Hp = np.stack([oc.pack_lower(H) for H in Hs]).astype(np.float32)
-    M, st = batched.sweep(_t(Hp, dev, f32))
+    M, st = batched.sweep(_t(Hp, dev, f32), full=full)
     assert (st.cpu().numpy() == 0).all(), st
     M = M.double()
     for i in range(b):
         ref = _swept(oc.unpack_lower(Hp[i].astype(np.float64), n))
-        got = batched.unpack_lower(M[i], n).cpu().numpy()
+        got = (M[i] if full else batched.unpack_lower(M[i], n)).cpu().numpy()
+        if full:
+            assert np.array_equal(got, got.T)
         err = np.abs(got - ref).max() / np.abs(ref).max()
         assert err < 2e-5, err
 
 
+@pytest.mark.parametrize("full", [False, True])
 @pytest.mark.parametrize("n,m", [(60, 120), (40, 60), (100, 28), (50, 30)])
-def test_sweep_rows(dev, n, m):
+def test_sweep_rows(dev, n, m, full):
     """Rows G: M = [[-H^-1, H^-1 G'], [G H^-1, -G H^-1 G']] (z padded to 16)."""
     rng = np.random.default_rng(7 * n + m)
     b = 3
     Hs = [_spd(rng, n) for _ in range(b)]
     Gs = rng.normal(size=(b, m, n)).astype(np.float32)
     Hp = np.stack([oc.pack_lower(H) for H in Hs]).astype(np.float32)
-    M, st = batched.sweep(_t(Hp, dev, f32), _t(Gs, dev, f32))
+    M, st = batched.sweep(_t(Hp, dev, f32), _t(Gs, dev, f32), full=full)
     assert (st.cpu().numpy() == 0).all(), st
     M = M.double()
     for i in range(b):
         H = oc.unpack_lower(Hp[i].astype(np.float64), n)
         ref = _swept(H, Gs[i].astype(np.float64))
-        got = batched.unpack_lower(M[i], n + m).cpu().numpy()
+        got = (M[i] if full else batched.unpack_lower(M[i], n + m)).cpu().numpy()
         err = np.abs(got - ref).max() / np.abs(ref).max()
         assert err < 2e-5, err
+
+
+@pytest.mark.parametrize("n,m,cond", [(60, 120, 1e4), (160, 0, 1e4), (100, 20, 1e5)])
+def test_sweep_ill_conditioned(dev, n, m, cond):
+    """cond(H) up to 1e5 (config-3 Hessians reach ~1e4): the square-root block
+    form must stay at the accuracy of an unblocked fp32 sweep."""
+    rng = np.random.default_rng(int(cond) + n)
+    b = 3
+    Hs = [_spd(rng, n, cond=cond) for _ in range(b)]
+    Gs = rng.normal(size=(b, m, n)).astype(np.float32) if m else None
+    Hp = np.stack([oc.pack_lower(H) for H in Hs]).astype(np.float32)
+    M, st = batched.sweep(_t(Hp, dev, f32), None if Gs is None else _t(Gs, dev, f32), full=True)
+    assert (st.cpu().numpy() == 0).all(), st
+    for i in range(b):
+        H = oc.unpack_lower(Hp[i].astype(np.float64), n)
+        ref = _swept(H, None if Gs is None else Gs[i].astype(np.float64))
+        # unblocked fp32 sweep error scales as cond * eps32 (~6e-8 * cond)
+        err = np.abs(M[i].double().cpu().numpy() - ref).max() / np.abs(ref).max()
+        assert err < 2e-8 * cond, err
 
 
 def test_sweep_shared_H_batched_G(dev):
@@ -146,3 +170,24 @@ def test_qp_rows_presweep(dev):
         zr = _oracle_two_sided(oc.unpack_lower(c(Hp[i]), n), c(f[i]), c(Gs[i]), c(hl[i]), c(hu[i]),
                                -1.5 * np.ones(n), 1.5 * np.ones(n))
         assert np.abs(zz[i] - zr).max() < 1e-4, np.abs(zz[i] - zr).max()
+
+
+def test_box_many_active_hands_off(dev):
+    """More than 64 active bounds (n = 120, large gradient): the product-form
+    kernel hands the instance to the workgroup kernel; results still match
+    the oracle, alongside instances that stay on the product-form path."""
+    rng = np.random.default_rng(77)
+    n, b = 120, 6
+    Hs = [_spd(rng, n, cond=10.0) for _ in range(b)]
+    Hp = np.stack([oc.pack_lower(H) for H in Hs])
+    f = rng.normal(size=(b, n)) * np.array([200.0, 1.0, 200.0, 1.0, 300.0, 2.0])[:, None]
+    z, st = batched.solve_box(_t(Hp, dev, f32), _t(f, dev, f32), -1.0, 1.0)
+    assert (batched.status_code(st) == 0).all(), batched.status_code(st)
+    z = z.double().cpu().numpy()
+    c = lambda a: a.astype(np.float32).astype(np.float64)  # noqa: E731
+    nact = []
+    for i in range(b):
+        zr = oq.box_qp(oc.unpack_lower(c(Hp[i]), n), c(f[i]), -np.ones(n), np.ones(n))[0]
+        nact.append(int((np.abs(np.abs(zr) - 1) < 1e-9).sum()))
+        assert np.abs(z[i] - zr).max() < 5e-5, (i, np.abs(z[i] - zr).max())
+    assert max(nact) > 64 and min(nact) < 64, nact

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CS = os.path.join(ROOT, "model_predictive_control_amd", "csrc")
 LIB = os.path.join(ROOT, "model_predictive_control_amd", "lib", "libmpcqp_timing.so")
 SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.hip", "quad_box.hip",
-        "solve_qp.hip", "sweep.hip", "bicycle.hip", "misc.hip"]
+        "solve_qp.hip", "sweep.hip", "solve_pf.hip", "bicycle.hip", "misc.hip"]
 PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/recheck", "GI: scan+argmax", "GI: pivot col+ratio", "GI: sweep"]
 
 if "--build" in sys.argv:
@@ -33,7 +33,9 @@ import bench  # noqa: E402
 from model_predictive_control_amd import _native, batched  # noqa: E402
 
 lib = _native.load()
-cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+arg = sys.argv[1] if len(sys.argv) > 1 else "2"
+pf = arg.startswith("pf")
+cfg = int(arg[2:] if pf else arg)
 reader = lib.mpcqp_debug_phase_cycles if cfg == 2 else lib.mpcqp_debug_phase_cycles_qp
 reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = (ctypes.c_ulonglong * 8)()
@@ -57,6 +59,17 @@ elif cfg == 55:
     a = A(); a.batch = 32768; a.slots = 1; a.horizon = 0; a.reps = 1
     w = bench.CONFIGS[5](a, torch.device("cuda"), 0)
     run = lambda: w._condense(0)  # noqa: E731
+    waves = a.batch * R
+elif pf:
+    # qp_pf_kernel of config 3 / 5 (one wave per instance)
+    reader = lib.mpcqp_debug_phase_cycles_pf
+    reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    PHASES = ["setup + s0", "refresh", "scan + col load", "gather + S^-1 u", "M0[:,P] v",
+              "ratio + update", "S^-1 update", "refinement"]
+    a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1
+    w = bench.CONFIGS[cfg](a, torch.device("cuda"), 0)
+    w._condense(0)
+    run = lambda: w._solve(0)  # noqa: E731
     waves = a.batch * R
 else:
     # qp_wg_kernel of config 3 / 5 (phases 0..3: K load, z sweep-in, GI, refinement)
