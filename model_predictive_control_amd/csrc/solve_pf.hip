@@ -42,6 +42,7 @@ struct PfArgs {
   const float* lb; int64_t sLb;
   const float* ub; int64_t sUb;
   const float* M0;             // sweep.hip full output, (n+m)^2 per instance
+  const float* s0;             // sweep.hip: M0[:, z] f, (n+m) per instance
   float* z; float* y; int32_t* status;
   int* retry_count; int* retry_list;
   int max_iter, refine;
@@ -52,18 +53,36 @@ __device__ __forceinline__ float bperm(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(lane << 2, __float_as_int(v)));
 }
 
+// LDS exchange inside the single-wave workgroup: a wave's LDS operations
+// execute in issue order, so only the compiler must not move them (no
+// s_barrier, and no fence that would drain the outstanding global loads)
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int NR, typename V>
 __device__ __forceinline__ V pick(const V (&x)[NR], int i) {
-  // value at index i (uniform) from lane i % 64, register i / 64
-  V v = x[0];
+  // value at index i (uniform) from lane i % 64, register i / 64: read every
+  // register's lane, then select on the (scalar) results -- a select over
+  // x[r] first gets folded into a dynamically indexed private array (scratch)
+  V v = readlane(x[0], i & 63);
 #pragma unroll
-  for (int r = 1; r < NR; ++r) v = ((i >> 6) == r) ? x[r] : v;
-  return readlane(v, i & 63);
+  for (int r = 1; r < NR; ++r) {
+    const V w = readlane(x[r], i & 63);
+    v = ((i >> 6) == r) ? w : v;
+  }
+  return v;
 }
 
 template <int NR>
 __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
   __shared__ float xb[NR * kWave];
+  // per-index bounds and scales live in LDS (read by the scan and the
+  // output only): keeps them out of the register budget
+  __shared__ float s_lo[NR * kWave], s_hi[NR * kWave], s_sl[NR * kWave], s_su[NR * kWave],
+      s_scl[NR * kWave];
+  __shared__ __attribute__((aligned(16))) float sx[kSlots];  // slot-vector broadcast
   __shared__ double red[8 * kWave];
   __shared__ double rsum[NR * kWave];
   const int b = blockIdx.x, l = threadIdx.x;
@@ -76,7 +95,7 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
   PhaseClock mpcqp_clk;
 #endif
 
-  float lo[NR], hi[NR], sl[NR], su[NR], fz[NR], scl[NR], val[NR], mu[NR], s0[NR];
+  float fz[NR], val[NR], mu[NR], s0[NR];
   int st[NR], slot[NR];
   bool bad = false, nonfin = false;
 #pragma unroll
@@ -93,17 +112,17 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
     }
     bad |= i < nt && (!(lv <= uv) || lv == inf || uv == -inf);
     nonfin |= !finite(fi);
-    lo[r] = lv;
-    hi[r] = uv;
+    s_lo[i] = lv;
+    s_hi[i] = uv;
     fz[r] = fi;
-    sl[r] = finite(lv) ? 1.f / (1.f + fabsf(lv)) : __builtin_nanf("");
-    su[r] = finite(uv) ? 1.f / (1.f + fabsf(uv)) : __builtin_nanf("");
+    s_sl[i] = finite(lv) ? 1.f / (1.f + fabsf(lv)) : __builtin_nanf("");
+    s_su[i] = finite(uv) ? 1.f / (1.f + fabsf(uv)) : __builtin_nanf("");
     st[r] = i < nt ? 0 : 3;
     slot[r] = -1;
     val[r] = 0.f;
     mu[r] = 0.f;
-    scl[r] = i < nt ? fabsf(M0[(int64_t)i * nt + i]) : 0.f;
-    s0[r] = 0.f;
+    s_scl[i] = i < nt ? fabsf(M0[(int64_t)i * nt + i]) : 0.f;
+    s0[r] = i < nt ? a.s0[(int64_t)b * nt + i] : 0.f;
   }
   // active-set slots: lane j = slot j
   int aidx = -1, sisz = 0;
@@ -130,16 +149,31 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
     auto gather = [&](const float (&x)[NR]) -> float {
 #pragma unroll
       for (int r = 0; r < NR; ++r) xb[l + kWave * r] = x[r];
-      __syncthreads();
+      wave_lds_sync();
       const float v = aidx >= 0 ? xb[aidx] : 0.f;
-      __syncthreads();
+      wave_lds_sync();
       return v;
     };
+    // slot vector t (lane j) to every lane through LDS: 16 broadcast b128
+    // reads instead of 64 v_readlane (which pile up in SGPRs and spill)
+    auto bcast_slots = [&](float t) __attribute__((always_inline)) {
+      wave_lds_sync();
+      sx[l] = t;
+      wave_lds_sync();
+    };
+    auto slot4 = [&](int j4) __attribute__((always_inline)) { return *reinterpret_cast<const float4*>(&sx[4 * j4]); };
     // lane i: (S^-1 t)_i
-    auto smul = [&](float t) -> float {
+    auto smul = [&](float t) __attribute__((always_inline)) -> float {
+      bcast_slots(t);
       float q = 0.f;
 #pragma unroll
-      for (int j = 0; j < kSlots; ++j) q = fmaf(S[j], readlane(t, j), q);
+      for (int j4 = 0; j4 < kSlots / 4; ++j4) {
+        const float4 tv = slot4(j4);
+        q = fmaf(S[4 * j4 + 0], tv.x, q);
+        q = fmaf(S[4 * j4 + 1], tv.y, q);
+        q = fmaf(S[4 * j4 + 2], tv.z, q);
+        q = fmaf(S[4 * j4 + 3], tv.w, q);
+      }
       return q;
     };
     // out += sum_t c_t M0[row_t, :] for kB rows at a time: every row's loads
@@ -183,24 +217,43 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
         axpy_rows(row, c, out);
       }
     };
-    // out += M0[:, z] c_z with c_z = coef(j) for j < n
+    // out += M0[:, z] c_z with c_z = coef(j) for j < n; the next batch's
+    // rows are in flight while the current one is accumulated
     auto zcols = [&](auto&& coef, float (&out)[NR]) {
-      for (int j0 = 0; j0 < n; j0 += kB) {
-        int row[kB];
-        float c[kB];
+      auto load = [&](int j0, float (&v)[kB][NR], float (&c)[kB]) {
 #pragma unroll
         for (int t = 0; t < kB; ++t) {
-          const int j = j0 + t;
-          row[t] = j < n ? j : 0;
-          c[t] = j < n ? coef(j) : 0.f;
+          const int j = j0 + t < n ? j0 + t : 0;
+          c[t] = j0 + t < n ? coef(j0 + t) : 0.f;
+          const float* rp = M0 + (int64_t)j * nt;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            v[t][r] = i < nt ? rp[i] : 0.f;
+          }
         }
-        axpy_rows(row, c, out);
+      };
+      float v[kB][NR], c[kB];
+      load(0, v, c);
+      for (int j0 = 0; j0 < n; j0 += kB) {
+        float vn[kB][NR], cn[kB];
+        load(j0 + kB < n ? j0 + kB : 0, vn, cn);
+#pragma unroll
+        for (int t = 0; t < kB; ++t)
+#pragma unroll
+          for (int r = 0; r < NR; ++r) out[r] = fmaf(c[t], v[t][r], out[r]);
+#pragma unroll
+        for (int t = 0; t < kB; ++t) {
+          c[t] = cn[t];
+#pragma unroll
+          for (int r = 0; r < NR; ++r) v[t][r] = vn[t][r];
+        }
       }
     };
     // exact state from s = M w (gi_mixed refresh) in product form:
     //   y = M0[:, Pc] w_Pc = s0 - M0[:, fixed z] f,  q = S^-1 (y_P - w'_P),
     //   (Ms w')_i = y_i + M0[i, P] q (i not in P), -q_i (i in P);  s = J_R Ms w'
-    auto refresh = [&]() {
+    auto refresh = [&]() __attribute__((always_inline)) {
       float yv[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) yv[r] = s0[r];
@@ -217,21 +270,21 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
         const float qi = bperm(q, slot[r] < 0 ? 0 : slot[r]);
         const float msw = act ? -qi : yv[r];
         const float s = (act && isz) ? -msw : msw;
-        const float bnd = (st[r] == 1) ? lo[r] : hi[r];
+        const float bnd = (st[r] == 1) ? s_lo[i] : s_hi[i];
         const float mval = isz ? fz[r] - s : s;
         const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
         val[r] = act ? bnd : (isz ? s : -s);
         mu[r] = act ? sside * mval : 0.f;
       }
     };
-    auto scan = [&](float& viol, int& p) {
+    auto scan = [&](float& viol, int& p) __attribute__((always_inline)) {
       viol = -inf;
       p = 0;
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         const int i = l + kWave * r;
-        const float vl = (lo[r] - val[r]) * sl[r];  // NaN (never wins) for infinite bounds
-        const float vu = (val[r] - hi[r]) * su[r];
+        const float vl = (s_lo[i] - val[r]) * s_sl[i];  // NaN (never wins) for infinite bounds
+        const float vu = (val[r] - s_hi[i]) * s_su[i];
         float v = (st[r] == 0) ? fmaxf(vl, vu) : -inf;
         v = (v == v) ? v : -inf;
         const bool take = v > viol;
@@ -244,36 +297,45 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
     };
     // S^-1 of P + {p}: bordered inverse, S^-1 += w w' / sigma with w = v
     // and w_snew = 1 (row/column snew were zero)
-    auto s_add = [&](float v, int snew, float sigma) {
+    auto s_add = [&](float v, int snew, float sigma) __attribute__((always_inline)) {
       const float w = (l == snew) ? 1.f : v;
-      const float is = 1.f / sigma;
+      const float wi = w / sigma;
+      bcast_slots(w);
 #pragma unroll
-      for (int j = 0; j < kSlots; ++j) S[j] = fmaf(w, readlane(w, j) * is, S[j]);
-    };
-    // S^-1 of P - {slot q}: Schur step, then row/column q exactly zero
-    auto s_drop = [&](int q, float dqq) {
-      float rq = 0.f;
-#pragma unroll
-      for (int j = 0; j < kSlots; ++j) {
-        const float rj = readlane(S[j], q);
-        rq = (l == j) ? rj : rq;
-      }
-      const float c = -rq / dqq;
-#pragma unroll
-      for (int j = 0; j < kSlots; ++j) {
-        const float rj = readlane(S[j], q);
-        S[j] = (l == q || j == q) ? 0.f : fmaf(c, rj, S[j]);
+      for (int j4 = 0; j4 < kSlots / 4; ++j4) {
+        const float4 wv = slot4(j4);
+        S[4 * j4 + 0] = fmaf(wi, wv.x, S[4 * j4 + 0]);
+        S[4 * j4 + 1] = fmaf(wi, wv.y, S[4 * j4 + 1]);
+        S[4 * j4 + 2] = fmaf(wi, wv.z, S[4 * j4 + 2]);
+        S[4 * j4 + 3] = fmaf(wi, wv.w, S[4 * j4 + 3]);
       }
     };
-    auto s_diag = [&](int q) -> float {
-      float d = 0.f;
+    // row q of S^-1 (lane q's registers) to LDS
+    auto s_row = [&](int q) __attribute__((always_inline)) {
+      wave_lds_sync();
+      if (l == q) {
 #pragma unroll
-      for (int j = 0; j < kSlots; ++j) d = (j == q) ? readlane(S[j], q) : d;
-      return d;
+        for (int j4 = 0; j4 < kSlots / 4; ++j4)
+          *reinterpret_cast<float4*>(&sx[4 * j4]) =
+              float4{S[4 * j4], S[4 * j4 + 1], S[4 * j4 + 2], S[4 * j4 + 3]};
+      }
+      wave_lds_sync();
     };
-
-    // ---------------------------------------------- s0 = M0[:, z] f
-    zcols([&](int j) { return fb[j]; }, s0);
+    // S^-1 of P - {slot q} (row q already in sx): Schur step, then row and
+    // column q exactly zero
+    auto s_drop = [&](int q, float dqq) __attribute__((always_inline)) {
+      const float c = -sx[l] / dqq;  // -S[l][q] / S[q][q]  (symmetric)
+#pragma unroll
+      for (int j4 = 0; j4 < kSlots / 4; ++j4) {
+        const float4 rv = slot4(j4);
+        const float r4[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = 4 * j4 + e;
+          S[j] = (l == q || j == q) ? 0.f : fmaf(c, r4[e], S[j]);
+        }
+      }
+    };
 
     MPCQP_PHASE(0);
     refresh();
@@ -287,14 +349,14 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
         if (!(viol > a.tol)) break;
         const float valp0 = pick<NR>(val, p);
         float valp = valp0;
-        const float lop = pick<NR>(lo, p), hip = pick<NR>(hi, p);
+        const float lop = s_lo[p], hip = s_hi[p];
         const int side = (valp < lop) ? 1 : 2;
         const float tgt = (side == 1) ? lop : hip;
         const bool pz = p < n;
         const float epsp = pz ? -1.f : 1.f;
         const float sidesign = ((side == 1) ? 1.f : -1.f) * (pz ? 1.f : -1.f);
         const float sgn = (tgt > valp) ? 1.f : -1.f;
-        const float scp = pick<NR>(scl, p);
+        const float scp = s_scl[p];
         float tau = 0.f;
         bool added = false;
         while (!added) {
@@ -368,7 +430,8 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
             // k leaves the active set
             if (!dep) valp = fmaf(sgn, s_eff, valp);
             const int q = uniform(pick<NR>(slot, k));
-            const float d = s_diag(q);
+            s_row(q);
+            const float d = sx[q];
             if (!(d > 0.f)) {
               code = MPCQP_STATUS_NOT_CONVEX;
               goto out;
@@ -446,38 +509,43 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
 #pragma unroll
       for (int r = 0; r < NR; ++r) yk[r] = 0.0;
       for (int r = l; r < NR * kWave; r += kWave) rsum[r] = 0.0;
+      wave_lds_sync();
       for (int j0 = 0; j0 < nt; j0 += 8) {
-        // 8 rows of K: H row j (lanes i <= j of packed H) or G row j - n
-        float hv[8][NR];
-        double xj[8];
+        // 8 rows of K, two halves of 4: H row j (lanes i <= j of packed H)
+        // or G row j - n
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int j = j0 + t;
-          const float* rp = j < n ? Hb + (int64_t)j * (j + 1) / 2
-                                  : (j < nt ? Gb + (int64_t)(j - n) * n : Hb);
-          const int lim = j < n ? j : (j < nt ? n - 1 : -1);
+        for (int h0 = 0; h0 < 8; h0 += 4) {
+          float hv[4][NR];
+          double xj[4];
 #pragma unroll
-          for (int r = 0; r < NR; ++r) {
-            const int i = l + kWave * r;
-            hv[t][r] = i <= lim ? rp[i] : 0.f;
+          for (int t = 0; t < 4; ++t) {
+            const int j = j0 + h0 + t;
+            const float* rp = j < n ? Hb + (int64_t)j * (j + 1) / 2
+                                    : (j < nt ? Gb + (int64_t)(j - n) * n : Hb);
+            const int lim = j < n ? j : (j < nt ? n - 1 : -1);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+              const int i = l + kWave * r;
+              hv[t][r] = i <= lim ? rp[i] : 0.f;
+            }
+            xj[t] = j < nt ? (double)pick<NR>(x, j) : 0.0;
           }
-          xj[t] = j < nt ? (double)pick<NR>(x, j) : 0.0;
-        }
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int j = j0 + t;
-          double part = 0.0;
+          for (int t = 0; t < 4; ++t) {
+            const int j = j0 + h0 + t;
+            double part = 0.0;
 #pragma unroll
-          for (int r = 0; r < NR; ++r) {
-            const int i = l + kWave * r;
-            const double h = hv[t][r];
-            // H row: the diagonal counts once (through yk); G row: all z
-            part = (j >= n || i < j) ? fma(h, (double)x[r], part) : part;
-            yk[r] = fma(h, xj[t], yk[r]);
+            for (int r = 0; r < NR; ++r) {
+              const int i = l + kWave * r;
+              const double hh = hv[t][r];
+              // H row: the diagonal counts once (through yk); G row: all z
+              part = (j >= n || i < j) ? fma(hh, (double)x[r], part) : part;
+              yk[r] = fma(hh, xj[t], yk[r]);
+            }
+            red[(h0 + t) * kWave + l] = part;
           }
-          red[t * kWave + l] = part;
         }
-        __syncthreads();
+        wave_lds_sync();
         {
           const int rr = l & 7, qq = l >> 3;
           double s = 0.0;
@@ -488,7 +556,7 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
           s += __shfl_xor(s, 32, kWave);
           if (qq == 0 && j0 + rr < nt) rsum[j0 + rr] += s;
         }
-        __syncthreads();
+        wave_lds_sync();
       }
       float w[NR];
 #pragma unroll
@@ -497,17 +565,17 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
         const bool isz = i < n;
         const bool act = st[r] == 1 || st[r] == 2;
         const double yi = yk[r] + rsum[i < NR * kWave ? i : 0];
-        const double bnd = (st[r] == 1) ? (double)lo[r] : (double)hi[r];
+        const double bnd = (st[r] == 1) ? (double)s_lo[i] : (double)s_hi[i];
         const bool inS = isz ? (st[r] == 0) : act;
         const double e = isz ? yi + (double)fz[r] : yi - bnd;
         w[r] = (inS && i < nt) ? (float)e : 0.f;
       }
-      __syncthreads();
+      wave_lds_sync();
       // sv = M w (w on free z and active rows): y2 = M0[:, free z] w
       float y2[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) y2[r] = 0.f;
-      zcols([&](int j) { return pick<NR>(w, j); }, y2);
+      zcols([&](int j) __attribute__((always_inline)) { return pick<NR>(w, j); }, y2);
       const float ys = gather(y2);
       const float wsl = gather(w);
       const float q = smul(aidx >= 0 ? ys - wsl : 0.f);
@@ -536,7 +604,7 @@ out:
       const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
       const float lam = (st[r] == 1 || st[r] == 2) ? sside * mu[r] : 0.f;
       if (code == kStatusRetry) continue;
-      if (isz) a.z[(int64_t)b * n + i] = ok ? fminf(fmaxf(val[r], lo[r]), hi[r]) : __builtin_nanf("");
+      if (isz) a.z[(int64_t)b * n + i] = ok ? fminf(fmaxf(val[r], s_lo[i]), s_hi[i]) : __builtin_nanf("");
       else if (a.y && i < nt) a.y[(int64_t)b * m + (i - n)] = ok ? lam : __builtin_nanf("");
     }
     if (l == 0) {
@@ -552,9 +620,9 @@ out:
 int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
               const float* G, int64_t sG, const float* hl, const float* hu, int64_t sh,
               const float* lb, int64_t sLb, const float* ub, int64_t sUb, const float* M0,
-              float* z, float* y, int32_t* status, int* retry_count, int* retry_list,
-              int max_iter, int refine, float tol, hipStream_t st) {
-  PfArgs a{batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, M0, z, y, status,
+              const float* s0, float* z, float* y, int32_t* status, int* retry_count,
+              int* retry_list, int max_iter, int refine, float tol, hipStream_t st) {
+  PfArgs a{batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, M0, s0, z, y, status,
            retry_count, retry_list, max_iter, refine, tol};
   if (n + m <= 2 * kWave)
     hipLaunchKernelGGL((qp_pf_kernel<2>), dim3(batch), dim3(kWave), 0, st, a);

@@ -20,7 +20,8 @@ namespace mpcqp {
 
 int sweep_tiles(int dtype, int n, int m);
 int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void* G, int64_t sG,
-                 void* M, int full, int32_t* status, hipStream_t st);
+                 void* M, int full, int32_t* status, hipStream_t st, const void* f, int64_t sf,
+                 void* s0);
 int hip_fail(hipError_t e, const char* where);
 
 template <typename T>
@@ -294,16 +295,20 @@ static size_t ws_m0_bytes(int batch, int n, int m) {
   return ((size_t)batch * nt * nt * sizeof(float) + 255) / 256 * 256;
 }
 
+static size_t ws_s0_bytes(int batch, int n, int m) {
+  return ((size_t)batch * (size_t)(n + m) * sizeof(float) + 255) / 256 * 256;
+}
+
 size_t qp_ws_bytes(int dtype, int batch, int n, int m) {
   if (batch <= 0 || n + m <= 64 || sweep_tiles(dtype, n, m) == 0) return 0;
-  return ws_m0_bytes(batch, n, m) + 256 + (size_t)batch * sizeof(int);
+  return ws_m0_bytes(batch, n, m) + ws_s0_bytes(batch, n, m) + 256 + (size_t)batch * sizeof(int);
 }
 
 int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
               const float* G, int64_t sG, const float* hl, const float* hu, int64_t sh,
               const float* lb, int64_t sLb, const float* ub, int64_t sUb, const float* M0,
-              float* z, float* y, int32_t* status, int* retry_count, int* retry_list,
-              int max_iter, int refine, float tol, hipStream_t st);
+              const float* s0, float* z, float* y, int32_t* status, int* retry_count,
+              int* retry_list, int max_iter, int refine, float tol, hipStream_t st);
 
 // refinement steps of the product-form kernel (MPCQP_PF_REFINE overrides;
 // a tuning knob, default 1: the fp64 residual against the original data
@@ -323,17 +328,18 @@ int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const v
                      hipStream_t st) {
   char* w = (char*)ws;
   float* M0 = (float*)w;
-  int* cnt = (int*)(w + ws_m0_bytes(batch, n, m));
+  float* s0 = (float*)(w + ws_m0_bytes(batch, n, m));
+  int* cnt = (int*)(w + ws_m0_bytes(batch, n, m) + ws_s0_bytes(batch, n, m));
   int* list = cnt + 64;
   hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int), st);
   if (e != hipSuccess) return hip_fail(e, "mpcqp_solve_qp_ws: hipMemsetAsync");
-  int rc = sweep_launch(batch, n, m, H, sH, G, sG, M0, 1, status, st);
+  int rc = sweep_launch(batch, n, m, H, sH, G, sG, M0, 1, status, st, f, sf, s0);
   if (rc != MPCQP_OK) return rc;
   const int mi = max_iter > 0 ? max_iter : 3 * (n + m) + 30;
   const float tl = tol > 0 ? (float)tol : 1e-6f;
   rc = launch_pf(batch, n, m, (const float*)H, sH, (const float*)f, sf, (const float*)G, sG,
                  (const float*)hl, (const float*)hu, sh, (const float*)lb, sLb, (const float*)ub,
-                 sUb, M0, (float*)z, (float*)y, status, cnt, list, mi, pf_refine(), tl, st);
+                 sUb, M0, s0, (float*)z, (float*)y, status, cnt, list, mi, pf_refine(), tl, st);
   if (rc != MPCQP_OK) return rc;
   return solve_qp_t<float>(batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, z, y,
                            status, max_iter, tol, st, M0, cnt, list);

@@ -40,6 +40,10 @@ struct SweepArgs {
   const float* G; int64_t sG;
   float* M;
   int32_t* status;
+  // optional (full only): s0 = M[:, z] f per instance (n + m), the free
+  // response the product-form solver starts from
+  const float* f; int64_t sf;
+  float* s0;
 };
 
 __device__ __forceinline__ constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
@@ -257,6 +261,19 @@ void sweep_mfma_kernel(SweepArgs a) {
         bst(v[i], rM, keep ? 4 * (r * nt + cc) : kOOB);
       }
     };
+    // s0 = M F with F_j = f of z block j in every column (MFMA, from the
+    // tiles and their transposes on their way out)
+    const bool want_s0 = a.s0 != nullptr;
+    mf4 F[T], acc[T];
+#pragma unroll
+    for (int tj = 0; tj < T; ++tj) {
+      acc[tj] = zero;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int z = 16 * tj + 4 * gs + i;
+        F[tj][i] = (want_s0 && tj < kp && z < n) ? a.f[(int64_t)b * a.sf + z] : 0.f;
+      }
+    }
 #pragma unroll
     for (int ti = 0; ti < T; ++ti)
 #pragma unroll
@@ -269,8 +286,21 @@ void sweep_mfma_kernel(SweepArgs a) {
           put(t[tri(ti, tj)], ti, tj, 0);
           put(tt, tj, ti, 0);
         }
+        if (want_s0) {
+          if (tj < kp) acc[ti] = mm(tt, F[tj], acc[ti]);                       // M_ij f_j
+          if (ti != tj && ti < kp) acc[tj] = mm(t[tri(ti, tj)], F[ti], acc[tj]);  // M_ji f_i
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
+    if (want_s0 && cs == 0) {
+#pragma unroll
+      for (int ti = 0; ti < T; ++ti)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = orig(16 * ti + 4 * gs + i);
+          if (r >= 0) a.s0[(int64_t)b * nt + r] = acc[ti][i];
+        }
+    }
   }
   if (l == 0)
     a.status[b] = fin_bad ? MPCQP_STATUS_NONFINITE : (piv_bad ? MPCQP_STATUS_NOT_CONVEX : 0);
@@ -292,9 +322,11 @@ int sweep_tiles(int dtype, int n, int m) {
 }
 
 int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void* G, int64_t sG,
-                 void* M, int full, int32_t* status, hipStream_t st) {
+                 void* M, int full, int32_t* status, hipStream_t st, const void* f, int64_t sf,
+                 void* s0) {
   SweepArgs a;
   a.batch = batch; a.n = n; a.m = m; a.full = full ? 1 : 0;
+  a.f = (const float*)f; a.sf = sf; a.s0 = full ? (float*)s0 : nullptr;
   a.np = (n + 15) / 16 * 16;
   a.kp = a.np / 16;
   a.H = (const float*)H; a.sH = sH;
@@ -329,5 +361,6 @@ extern "C" int mpcqp_sweep(int dtype, int batch, int n, int m, const void* H, in
   MPCQP_CHECK_ARG(sweep_tiles(dtype, n, m) > 0, "mpcqp_sweep: padded n + m = %d outside 65..192",
                   (n + 15) / 16 * 16 + m);
   if (batch == 0) return MPCQP_OK;
-  return sweep_launch(batch, n, m, H, strideH, G, strideG, M, full, status, (hipStream_t)stream);
+  return sweep_launch(batch, n, m, H, strideH, G, strideG, M, full, status, (hipStream_t)stream,
+                      nullptr, 0, nullptr);
 }
