@@ -306,6 +306,227 @@ void sweep_mfma_kernel(SweepArgs a) {
     a.status[b] = fin_bad ? MPCQP_STATUS_NONFINITE : (piv_bad ? MPCQP_STATUS_NOT_CONVEX : 0);
 }
 
+// ------------------------------------------------------------ rows variant
+// m > 0, dense output (the product-form solver's input): only the z columns
+// of the lower block triangle live in registers -- zz (KP(KP+1)/2 tiles) and
+// G z (TR x KP tiles, row tile ir, z tile k) -- and the row-row block, which
+// the sweep only ever subtracts into, is formed at the end as
+//     M_GG = -G H^-1 G' = -M_Gz G'       (MFMA against G' re-read from HBM)
+// so the register file holds 42 instead of 78 tiles at config 3 (KP = 4,
+// TR = 8) and the kernel runs without spills.
+template <int KP>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
+void sweep_rows_kernel(SweepArgs a) {
+  constexpr int TRM = 12 - KP;  // row tiles held at most (np + m <= 192)
+  constexpr int NZ = KP * (KP + 1) / 2;
+  const int b = blockIdx.x;
+  const int l = threadIdx.x, g = l >> 4, c = l & 15;
+  const int n = a.n, m = a.m, np = a.np, nt = n + m;
+  const int tr = (m + 15) / 16;
+  const float* Hb = a.H + (int64_t)b * a.sH;
+  const float* Gb = a.G + (int64_t)b * a.sG;
+  const rsrc_t rH = mk_rsrc(Hb, (int64_t)n * (n + 1) / 2 * 4);
+  const rsrc_t rG = mk_rsrc(Gb, (int64_t)m * n * 4);
+  mf4 Z[NZ], Gt[TRM][KP];
+  bool nonfin = false;
+  // zz: packed H, mirrored on the diagonal tiles, unit pad pivots
+#pragma unroll
+  for (int ti = 0; ti < KP; ++ti)
+#pragma unroll
+    for (int tj = 0; tj <= ti; ++tj) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * ti + 4 * g + i, cc = 16 * tj + c;
+        const int hi = r > cc ? r : cc, lo = r > cc ? cc : r;
+        const float v = bld(rH, hi < n ? 4 * (hi * (hi + 1) / 2 + lo) : kOOB) +
+                        ((r == cc && r >= n) ? 1.f : 0.f);
+        nonfin |= !finite(v);
+        Z[tri(ti, tj)][i] = v;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  // G z: G[rho][z], rho = 16 ir + 4g + i, z = 16 k + c
+#pragma unroll
+  for (int ir = 0; ir < TRM; ++ir)
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rho = 16 * ir + 4 * g + i, z = 16 * k + c;
+        const float v = bld(rG, (rho < m && z < n) ? 4 * (rho * n + z) : kOOB);
+        nonfin |= !finite(v);
+        Gt[ir][k][i] = v;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  bool bad = false;
+  mf4 eye;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) eye[i] = (4 * g + i == c) ? 1.f : 0.f;
+  const mf4 zero = {0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    mf4 li = eye;
+    chol_inv16(Z[tri(k, k)], li, g, c, bad);  // L^-1
+    __builtin_amdgcn_sched_barrier(0);
+    const mf4 lit = mm(li, eye, zero);
+    mf4 Wz[KP];
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      if (i == k) continue;
+      const mf4 r = (i < k) ? Z[tri(k, i)] : mm(Z[tri(i, k)], eye, zero);
+      Wz[i] = mm(lit, r, zero);
+    }
+    // zz block
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      if (j == k) continue;
+      const mf4 wn = -Wz[j];
+#pragma unroll
+      for (int i = j; i < KP; ++i)
+        if (i != k) Z[tri(i, j)] = mm(Wz[i], wn, Z[tri(i, j)]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // row tiles, one W at a time: M_rho,j -= W_rho' W_j, M_rho,k = W_rho' L^-1
+#pragma unroll
+    for (int ir = 0; ir < TRM; ++ir) {
+      if (ir < tr) {  // uniform
+        const mf4 wr = mm(lit, mm(Gt[ir][k], eye, zero), zero);  // L^-1 M_k,rho
+#pragma unroll
+        for (int j = 0; j < KP; ++j)
+          if (j != k) Gt[ir][j] = mm(wr, -Wz[j], Gt[ir][j]);
+        Gt[ir][k] = mm(wr, li, zero);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      if (i < k) Z[tri(k, i)] = mm(li, Wz[i], zero);
+      else if (i > k) Z[tri(i, k)] = mm(Wz[i], li, zero);
+    }
+    Z[tri(k, k)] = mm(li, -li, zero);
+  }
+
+  const bool fin_bad = __builtin_amdgcn_ballot_w64(nonfin) != 0;
+  const bool piv_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+  const rsrc_t rM = mk_rsrc(a.M + (int64_t)b * nt * nt, (int64_t)nt * nt * 4);
+  int ls = l;
+  asm volatile("" : "+v"(ls));
+  const int gs = ls >> 4, cs = ls & 15;
+  // dense store of a C-layout tile: rows rb / columns cb of the ORIGINAL
+  // index space (z tile k -> 16k, row tile ir -> n + 16 ir); part as in the
+  // generic kernel (1: c <= r only, 2: c > r only)
+  auto put = [&](const mf4& v, int rb, bool rrow, int cb, bool crow, int part) {
+    const int c0 = crow ? 16 * cb + cs : 16 * cb + cs;
+    const int cc = crow ? (c0 < m ? n + c0 : -1) : (c0 < n ? c0 : -1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = 4 * gs + i, r0 = 16 * rb + rr;
+      const int r = rrow ? (r0 < m ? n + r0 : -1) : (r0 < n ? r0 : -1);
+      const bool keep = r >= 0 && cc >= 0 && (part == 0 || (part == 1 ? cs <= rr : cs > rr));
+      bst(v[i], rM, keep ? 4 * (r * nt + cc) : kOOB);
+    }
+  };
+  const bool want_s0 = a.s0 != nullptr;
+  mf4 F[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int z = 16 * k + 4 * gs + i;
+      F[k][i] = (want_s0 && z < n) ? a.f[(int64_t)b * a.sf + z] : 0.f;
+    }
+  // zz tiles and the z part of s0
+  {
+    mf4 acc[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) acc[k] = zero;
+#pragma unroll
+    for (int ti = 0; ti < KP; ++ti)
+#pragma unroll
+      for (int tj = 0; tj <= ti; ++tj) {
+        const mf4 tt = mm(Z[tri(ti, tj)], eye, zero);
+        if (ti == tj) {
+          put(Z[tri(ti, tj)], ti, false, tj, false, 1);
+          put(tt, ti, false, tj, false, 2);
+        } else {
+          put(Z[tri(ti, tj)], ti, false, tj, false, 0);
+          put(tt, tj, false, ti, false, 0);
+        }
+        if (want_s0) {
+          acc[ti] = mm(tt, F[tj], acc[ti]);
+          if (ti != tj) acc[tj] = mm(Z[tri(ti, tj)], F[ti], acc[tj]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    if (want_s0 && cs == 0) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * k + 4 * gs + i;
+          if (r < n) a.s0[(int64_t)b * nt + r] = acc[k][i];
+        }
+    }
+  }
+  // G z tiles (and their transposes, the z-row block), the row part of s0,
+  // then the row-row block -M_Gz G'
+#pragma unroll
+  for (int ir = 0; ir < TRM; ++ir) {
+    if (ir < tr) {
+      mf4 acc = zero;
+      mf4 tts[KP];
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        tts[k] = mm(Gt[ir][k], eye, zero);
+        put(Gt[ir][k], ir, true, k, false, 0);
+        put(tts[k], k, false, ir, true, 0);
+        if (want_s0) acc = mm(tts[k], F[k], acc);
+      }
+      if (want_s0 && cs == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rho = 16 * ir + 4 * gs + i;
+          if (rho < m) a.s0[(int64_t)b * nt + n + rho] = acc[i];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      for (int jr = 0; jr <= ir; ++jr) {
+        mf4 gg = zero;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+          mf4 gt;  // G(jr, k)' in C layout: lane (g, c) holds G[16 jr + c][16 k + 4g + e]
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rho = 16 * jr + cs, z = 16 * k + 4 * gs + e;
+            gt[e] = bld(rG, (rho < m && z < n) ? 4 * (rho * n + z) : kOOB);
+          }
+          gg = mm(tts[k], gt, gg);  // M_Gz(ir, k) G(jr, k)'
+        }
+        gg = -gg;
+        const mf4 ggt = mm(gg, eye, zero);
+        if (jr == ir) {
+          put(gg, ir, true, jr, true, 1);
+          put(ggt, ir, true, jr, true, 2);
+        } else {
+          put(gg, ir, true, jr, true, 0);
+          put(ggt, jr, true, ir, true, 0);
+        }
+      }
+    }
+  }
+  if (l == 0)
+    a.status[b] = fin_bad ? MPCQP_STATUS_NONFINITE : (piv_bad ? MPCQP_STATUS_NOT_CONVEX : 0);
+}
+
+template <int KP>
+static int launch_sweep_rows(const SweepArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((sweep_rows_kernel<KP>), dim3(a.batch), dim3(64), 0, st, a);
+  MPCQP_CHECK_LAUNCH("sweep_rows_kernel");
+  return MPCQP_OK;
+}
+
 template <int T>
 static int launch_sweep_t(const SweepArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((sweep_mfma_kernel<T>), dim3(a.batch), dim3(64), 0, st, a);
@@ -333,6 +554,17 @@ int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void*
   a.G = (const float*)G; a.sG = sG;
   a.M = (float*)M;
   a.status = status;
+  if (full && m > 0) {
+    switch (a.kp) {
+      case 1: return launch_sweep_rows<1>(a, st);
+      case 2: return launch_sweep_rows<2>(a, st);
+      case 3: return launch_sweep_rows<3>(a, st);
+      case 4: return launch_sweep_rows<4>(a, st);
+      case 5: return launch_sweep_rows<5>(a, st);
+      case 6: return launch_sweep_rows<6>(a, st);
+      default: break;  // wider z blocks: the generic kernel
+    }
+  }
   switch (sweep_tiles(MPCQP_F32, n, m)) {
     case 5: return launch_sweep_t<5>(a, st);
     case 6: return launch_sweep_t<6>(a, st);
