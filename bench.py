@@ -372,7 +372,7 @@ class Config3:
         wf = sweep_flops_per_instance(n, m) * bsz
         r_c = roof("condense_kernel<float,4>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
                    traffic.get("condense"), {"bytes_per_launch": cb})
-        r_w = roof("sweep_mfma_kernel<12>", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
+        r_w = roof("sweep_rows_kernel<4>", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
                    traffic.get("sweep"), {"flops_per_launch": wf})
         r_p = roof("qp_pf_kernel<3>", "hbm", sb, t_p, HBM_PEAK_GBS, "GB/s",
                    traffic.get("solve_pf"), {"bytes_per_launch": sb,
