@@ -178,7 +178,11 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
     };
     // out += sum_t c_t M0[row_t, :] for kB rows at a time: every row's loads
     // are issued before the first FMA (one memory round trip per batch)
-    constexpr int kB = 8;
+#ifndef MPCQP_PF_KB
+#define MPCQP_PF_KB 8
+#endif
+    constexpr int kB = MPCQP_PF_KB;  // active rows per memory round trip
+    constexpr int kZB = 8;           // z rows per batch in zcols (double-buffered)
     auto axpy_rows = [&](const int (&row)[kB], const float (&c)[kB], float (&out)[NR]) {
       float v[kB][NR];
 #pragma unroll
@@ -197,8 +201,7 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
     };
     // out += sign * M0[:, P] q  (rows a_j of the symmetric M0); fixed_z_f:
     // coefficient -f_a on the fixed z instead (rows contribute nothing)
-    auto pcols = [&](float q, float (&out)[NR], float sign, bool fixed_z_f) {
-      uint64_t mm = used;
+    auto pcols = [&](float q, float (&out)[NR], float sign, bool fixed_z_f, uint64_t mm) {
       while (mm) {
         int row[kB];
         float c[kB];
@@ -220,9 +223,9 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
     // out += M0[:, z] c_z with c_z = coef(j) for j < n; the next batch's
     // rows are in flight while the current one is accumulated
     auto zcols = [&](auto&& coef, float (&out)[NR]) {
-      auto load = [&](int j0, float (&v)[kB][NR], float (&c)[kB]) {
+      auto load = [&](int j0, float (&v)[kZB][NR], float (&c)[kZB]) {
 #pragma unroll
-        for (int t = 0; t < kB; ++t) {
+        for (int t = 0; t < kZB; ++t) {
           const int j = j0 + t < n ? j0 + t : 0;
           c[t] = j0 + t < n ? coef(j0 + t) : 0.f;
           const float* rp = M0 + (int64_t)j * nt;
@@ -233,17 +236,17 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
           }
         }
       };
-      float v[kB][NR], c[kB];
+      float v[kZB][NR], c[kZB];
       load(0, v, c);
-      for (int j0 = 0; j0 < n; j0 += kB) {
-        float vn[kB][NR], cn[kB];
-        load(j0 + kB < n ? j0 + kB : 0, vn, cn);
+      for (int j0 = 0; j0 < n; j0 += kZB) {
+        float vn[kZB][NR], cn[kZB];
+        load(j0 + kZB < n ? j0 + kZB : 0, vn, cn);
 #pragma unroll
-        for (int t = 0; t < kB; ++t)
+        for (int t = 0; t < kZB; ++t)
 #pragma unroll
           for (int r = 0; r < NR; ++r) out[r] = fmaf(c[t], v[t][r], out[r]);
 #pragma unroll
-        for (int t = 0; t < kB; ++t) {
+        for (int t = 0; t < kZB; ++t) {
           c[t] = cn[t];
 #pragma unroll
           for (int r = 0; r < NR; ++r) v[t][r] = vn[t][r];
@@ -257,11 +260,11 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
       float yv[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) yv[r] = s0[r];
-      pcols(0.f, yv, 1.f, true);
+      pcols(0.f, yv, 1.f, true, used);
       const float ys = gather(yv);
       const float t = aidx >= 0 ? ys - (sisz ? sbnd : -sbnd) : 0.f;
       const float q = smul(t);
-      pcols(q, yv, 1.f, false);
+      pcols(q, yv, 1.f, false, used);
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         const int i = l + kWave * r;
@@ -364,8 +367,12 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
             code = MPCQP_STATUS_MAXITER;
             goto out;
           }
-          // column p of the current M
-          float col[NR];
+          // column p of the current M.  The first kB active rows of M0 are
+          // loaded in the same memory round trip as column p (their indices
+          // are known; only their coefficients v wait for the column)
+          float col[NR], v0[kB][NR];
+          int j0[kB];
+          uint64_t mrest = used;
           {
             const float* row = M0 + (int64_t)p * nt;
 #pragma unroll
@@ -373,12 +380,34 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
               const int i = l + kWave * r;
               col[r] = i < nt ? row[i] : 0.f;
             }
+#pragma unroll
+            for (int t = 0; t < kB; ++t) {
+              j0[t] = -1;
+              int aj = 0;
+              if (mrest) {
+                j0[t] = __builtin_ctzll(mrest);
+                mrest &= mrest - 1;
+                aj = readlane(aidx, j0[t]);
+              }
+              const float* rp = M0 + (int64_t)aj * nt;
+#pragma unroll
+              for (int r = 0; r < NR; ++r) {
+                const int i = l + kWave * r;
+                v0[t][r] = i < nt ? rp[i] : 0.f;
+              }
+            }
           }
           MPCQP_PHASE(2);
           const float u = gather(col);
           const float v = smul(u);
           MPCQP_PHASE(3);
-          pcols(v, col, 1.f, false);
+#pragma unroll
+          for (int t = 0; t < kB; ++t) {
+            const float c = j0[t] >= 0 ? readlane(v, j0[t]) : 0.f;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) col[r] = fmaf(c, v0[t][r], col[r]);
+          }
+          pcols(v, col, 1.f, false, mrest);
           MPCQP_PHASE(4);
 #pragma unroll
           for (int r = 0; r < NR; ++r) {
@@ -510,29 +539,35 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
       for (int r = 0; r < NR; ++r) yk[r] = 0.0;
       for (int r = l; r < NR * kWave; r += kWave) rsum[r] = 0.0;
       wave_lds_sync();
+      // 8 rows of K per reduction step, loaded 4 at a time: H row j (lanes
+      // i <= j of packed H) or G row j - n; the next 4 rows are in flight
+      // while the current 4 are accumulated (loads overlap the FMAs and the
+      // LDS reduction instead of one exposed round trip per half)
+      auto kload = [&](int j0, float (&hv)[4][NR]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = j0 + t;
+          const float* rp = j < n ? Hb + (int64_t)j * (j + 1) / 2
+                                  : (j < nt ? Gb + (int64_t)(j - n) * n : Hb);
+          const int lim = j < n ? j : (j < nt ? n - 1 : -1);
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            hv[t][r] = i <= lim ? rp[i] : 0.f;
+          }
+        }
+      };
+      float hv[4][NR];
+      kload(0, hv);
       for (int j0 = 0; j0 < nt; j0 += 8) {
-        // 8 rows of K, two halves of 4: H row j (lanes i <= j of packed H)
-        // or G row j - n
 #pragma unroll
         for (int h0 = 0; h0 < 8; h0 += 4) {
-          float hv[4][NR];
-          double xj[4];
+          float hn[4][NR];
+          kload(j0 + h0 + 4, hn);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             const int j = j0 + h0 + t;
-            const float* rp = j < n ? Hb + (int64_t)j * (j + 1) / 2
-                                    : (j < nt ? Gb + (int64_t)(j - n) * n : Hb);
-            const int lim = j < n ? j : (j < nt ? n - 1 : -1);
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-              const int i = l + kWave * r;
-              hv[t][r] = i <= lim ? rp[i] : 0.f;
-            }
-            xj[t] = j < nt ? (double)pick<NR>(x, j) : 0.0;
-          }
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int j = j0 + h0 + t;
+            const double xj = j < nt ? (double)pick<NR>(x, j) : 0.0;
             double part = 0.0;
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
@@ -540,10 +575,14 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
               const double hh = hv[t][r];
               // H row: the diagonal counts once (through yk); G row: all z
               part = (j >= n || i < j) ? fma(hh, (double)x[r], part) : part;
-              yk[r] = fma(hh, xj[t], yk[r]);
+              yk[r] = fma(hh, xj, yk[r]);
             }
             red[(h0 + t) * kWave + l] = part;
           }
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) hv[t][r] = hn[t][r];
         }
         wave_lds_sync();
         {
@@ -579,7 +618,7 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
       const float ys = gather(y2);
       const float wsl = gather(w);
       const float q = smul(aidx >= 0 ? ys - wsl : 0.f);
-      pcols(q, y2, 1.f, false);
+      pcols(q, y2, 1.f, false, used);
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         const int i = l + kWave * r;
