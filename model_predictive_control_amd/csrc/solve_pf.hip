@@ -31,6 +31,7 @@
 namespace mpcqp {
 
 constexpr int kSlots = 64;
+constexpr int kKChunk = 1536;  // floats of K rows per refinement chunk (6 KB of LDS)
 constexpr int kStatusRetry = 0x7f;  // internal: hand the instance to qp_wg_kernel
 
 struct PfArgs {
@@ -85,6 +86,9 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
   __shared__ __attribute__((aligned(16))) float sx[kSlots];  // slot-vector broadcast
   __shared__ double red[8 * kWave];
   __shared__ double rsum[NR * kWave];
+  __shared__ float kbuf[kKChunk];  // refinement: rows of K staged per chunk
+  static_assert(kKChunk >= 8 * NR * kWave, "8 rows of K (<= NR*64 floats each) must fit one chunk");
+  static_assert(kKChunk % kWave == 0, "chunk is whole wave loads");
   const int b = blockIdx.x, l = threadIdx.x;
   const int n = a.n, m = a.m, nt = n + m;
   const float* M0 = a.M0 + (int64_t)b * nt * nt;
@@ -539,64 +543,72 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
       for (int r = 0; r < NR; ++r) yk[r] = 0.0;
       for (int r = l; r < NR * kWave; r += kWave) rsum[r] = 0.0;
       wave_lds_sync();
-      // 8 rows of K per reduction step, loaded 4 at a time: H row j (lanes
-      // i <= j of packed H) or G row j - n; the next 4 rows are in flight
-      // while the current 4 are accumulated (loads overlap the FMAs and the
-      // LDS reduction instead of one exposed round trip per half)
-      auto kload = [&](int j0, float (&hv)[4][NR]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = j0 + t;
-          const float* rp = j < n ? Hb + (int64_t)j * (j + 1) / 2
-                                  : (j < nt ? Gb + (int64_t)(j - n) * n : Hb);
-          const int lim = j < n ? j : (j < nt ? n - 1 : -1);
-#pragma unroll
-          for (int r = 0; r < NR; ++r) {
-            const int i = l + kWave * r;
-            hv[t][r] = i <= lim ? rp[i] : 0.f;
+      // Rows of K stream through LDS in chunks of up to kKChunk floats:
+      // packed H rows (row j = lanes i <= j, contiguous) then G rows (n each,
+      // contiguous).  A chunk is a whole number of 8-row groups; its loads are
+      // all issued before the first LDS store (one memory round trip per
+      // chunk instead of one per 4 rows).  Per 8-row group the row-direction
+      // sums reduce in LDS as before.
+      auto kpass = [&](const float* base, int jb, int je, bool isH) __attribute__((always_inline)) {
+        auto rstart = [&](int j) -> int64_t {
+          return isH ? (int64_t)j * (j + 1) / 2 : (int64_t)(j - jb) * n;
+        };
+        for (int j0 = jb; j0 < je;) {
+          const int64_t c0 = rstart(j0);
+          int j1 = j0;
+          while (j1 < je) {
+            const int jn = j1 + 8 < je ? j1 + 8 : je;
+            if (rstart(jn) - c0 > kKChunk) break;
+            j1 = jn;
           }
+          const int cnt = (int)(rstart(j1) - c0);
+          {
+            float tmp[kKChunk / kWave];
+#pragma unroll
+            for (int k = 0; k < kKChunk / kWave; ++k) {
+              const int e = l + kWave * k;
+              tmp[k] = e < cnt ? base[c0 + e] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < kKChunk / kWave; ++k) kbuf[l + kWave * k] = tmp[k];
+          }
+          wave_lds_sync();
+          for (int g = j0; g < j1; g += 8) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const int j = g + t;
+              const int lim = j < j1 ? (isH ? j : n - 1) : -1;
+              const int ro = (int)(rstart(j < j1 ? j : j0) - c0);
+              const double xj = j < j1 ? (double)pick<NR>(x, j) : 0.0;
+              double part = 0.0;
+#pragma unroll
+              for (int r = 0; r < NR; ++r) {
+                const int i = l + kWave * r;
+                const double hh = i <= lim ? kbuf[ro + i] : 0.f;
+                // H row: the diagonal counts once (through yk); G row: all z
+                part = (!isH || i < j) ? fma(hh, (double)x[r], part) : part;
+                yk[r] = fma(hh, xj, yk[r]);
+              }
+              red[t * kWave + l] = part;
+            }
+            wave_lds_sync();
+            {
+              const int rr = l & 7, qq = l >> 3;
+              double sm = 0.0;
+#pragma unroll
+              for (int t = 0; t < 8; ++t) sm += red[rr * kWave + qq * 8 + t];
+              sm += __shfl_xor(sm, 8, kWave);
+              sm += __shfl_xor(sm, 16, kWave);
+              sm += __shfl_xor(sm, 32, kWave);
+              if (qq == 0 && g + rr < j1) rsum[g + rr] += sm;
+            }
+            wave_lds_sync();
+          }
+          j0 = j1;
         }
       };
-      float hv[4][NR];
-      kload(0, hv);
-      for (int j0 = 0; j0 < nt; j0 += 8) {
-#pragma unroll
-        for (int h0 = 0; h0 < 8; h0 += 4) {
-          float hn[4][NR];
-          kload(j0 + h0 + 4, hn);
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int j = j0 + h0 + t;
-            const double xj = j < nt ? (double)pick<NR>(x, j) : 0.0;
-            double part = 0.0;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-              const int i = l + kWave * r;
-              const double hh = hv[t][r];
-              // H row: the diagonal counts once (through yk); G row: all z
-              part = (j >= n || i < j) ? fma(hh, (double)x[r], part) : part;
-              yk[r] = fma(hh, xj, yk[r]);
-            }
-            red[(h0 + t) * kWave + l] = part;
-          }
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int r = 0; r < NR; ++r) hv[t][r] = hn[t][r];
-        }
-        wave_lds_sync();
-        {
-          const int rr = l & 7, qq = l >> 3;
-          double s = 0.0;
-#pragma unroll
-          for (int t = 0; t < 8; ++t) s += red[rr * kWave + qq * 8 + t];
-          s += __shfl_xor(s, 8, kWave);
-          s += __shfl_xor(s, 16, kWave);
-          s += __shfl_xor(s, 32, kWave);
-          if (qq == 0 && j0 + rr < nt) rsum[j0 + rr] += s;
-        }
-        wave_lds_sync();
-      }
+      kpass(Hb, 0, n, true);
+      if (m) kpass(Gb, n, nt, false);
       float w[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
