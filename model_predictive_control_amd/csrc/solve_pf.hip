@@ -191,11 +191,11 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
       float v[kB][NR];
 #pragma unroll
       for (int t = 0; t < kB; ++t) {
-        const float* rp = M0 + (int64_t)row[t] * nt;
+        const float* rp = M0 + (int64_t)(row[t] < 0 ? 0 : row[t]) * nt;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
           const int i = l + kWave * r;
-          v[t][r] = i < nt ? rp[i] : 0.f;
+          v[t][r] = (row[t] >= 0 && i < nt) ? rp[i] : 0.f;  // row -1: empty entry, no load
         }
       }
 #pragma unroll
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
         float c[kB];
 #pragma unroll
         for (int t = 0; t < kB; ++t) {
-          row[t] = 0;
+          row[t] = -1;
           c[t] = 0.f;
           if (mm) {
             const int j = __builtin_ctzll(mm);
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
 #pragma unroll
               for (int r = 0; r < NR; ++r) {
                 const int i = l + kWave * r;
-                v0[t][r] = i < nt ? rp[i] : 0.f;
+                v0[t][r] = (j0[t] >= 0 && i < nt) ? rp[i] : 0.f;  // empty slots load nothing
               }
             }
           }
