@@ -579,7 +579,7 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
               const int j = g + t;
               const int lim = j < j1 ? (isH ? j : n - 1) : -1;
               const int ro = (int)(rstart(j < j1 ? j : j0) - c0);
-              const double xj = j < j1 ? (double)pick<NR>(x, j) : 0.0;
+              const double xj = j < j1 ? (double)xb[j] : 0.0;  // LDS broadcast
               double part = 0.0;
 #pragma unroll
               for (int r = 0; r < NR; ++r) {
@@ -607,6 +607,11 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
           j0 = j1;
         }
       };
+      // x_j of each row comes from an LDS broadcast (xb is free until the
+      // gathers below)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) xb[l + kWave * r] = x[r];
+      wave_lds_sync();
       kpass(Hb, 0, n, true);
       if (m) kpass(Gb, n, nt, false);
       float w[NR];
