@@ -26,7 +26,7 @@ from . import _native as nat
 __all__ = [
     "condense", "solve_box", "mpc_box", "solve_poly", "solve_qp", "sweep", "riccati", "gemv",
     "rollout",
-    "pack_lower", "unpack_lower", "status_code", "status_iters",
+    "pack_lower", "unpack_lower", "status_code", "status_iters", "workspace_bytes",
 ]
 
 
@@ -53,17 +53,38 @@ def _ptr(t):
 _WS: dict = {}
 
 
-def _workspace(nbytes: int, dev) -> torch.Tensor | None:
-    """Device scratch for the two-kernel QP path, cached per (device, size):
-    a buffer is never freed or replaced, so HIP graphs captured over a call
-    keep a valid pointer."""
+def _workspace(nbytes: int, dev, ws: torch.Tensor | None = None) -> torch.Tensor | None:
+    """Device scratch of the two-kernel QP path (swept matrix, s0, hand-off
+    counter and list).
+
+    * ``ws`` given: the caller's buffer is used as is (checked for size).
+    * inside a HIP-graph capture: a fresh buffer, which the graph's private
+      pool keeps for the graph's lifetime; never a cached one, so a later
+      resize of the cache cannot pull memory out from under a captured graph.
+    * otherwise: one grow-only buffer per (device, stream).  Kernels on one
+      stream run in order, so solves on the same stream may share it; solves
+      on different streams get different buffers.  Growing drops the smaller
+      buffer (the caching allocator reuses it stream-ordered on that stream).
+    """
     if nbytes <= 0:
         return None
-    key = (str(dev), int(nbytes))
-    ws = _WS.get(key)
-    if ws is None:
-        ws = _WS[key] = torch.empty((int(nbytes),), dtype=torch.uint8, device=dev)
-    return ws
+    if ws is not None:
+        if ws.device.type != "cuda" or ws.numel() * ws.element_size() < nbytes:
+            raise ValueError(f"workspace must be a device buffer of >= {nbytes} bytes")
+        return ws
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty((int(nbytes),), dtype=torch.uint8, device=dev)
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        _WS.pop(key, None)
+        buf = _WS[key] = torch.empty((int(nbytes),), dtype=torch.uint8, device=dev)
+    return buf
+
+
+def workspace_bytes(dtype: torch.dtype, batch: int, n: int, m: int = 0) -> int:
+    """Bytes of the ``ws=`` buffer solve_box (m = 0) / solve_qp need."""
+    return int(_lib().mpcqp_solve_qp_workspace(_code(dtype), batch, n, m))
 
 
 def _dev(x, dtype, device):
@@ -222,8 +243,9 @@ def _bound(v, n, dt, dev):
 
 
 def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, tol: float = 0.0,
-              out: tuple | None = None, presweep: bool = True):
+              out: tuple | None = None, presweep: bool = True, ws: torch.Tensor | None = None):
     """Batched  min 1/2 z'Hz + f'z  s.t.  lb <= z <= ub.  Returns (z, status).
+    ``ws``: optional caller-owned scratch (``workspace_bytes(dtype, batch, n)``).
 
     fp32 with n > 64: the -H^-1 sweep runs first as its own MFMA kernel
     (``mpcqp_solve_box_ws``) unless ``presweep=False``."""
@@ -247,7 +269,7 @@ def solve_box(H, f, lb=None, ub=None, *, max_iter: int = 0, tol: float = 0.0,
         z, status = out
     lib = _lib()
     wsb = int(lib.mpcqp_solve_qp_workspace(_code(dt), batch, n, 0)) if presweep else 0
-    ws = _workspace(wsb, dev)
+    ws = _workspace(wsb, dev, ws)
     rc = lib.mpcqp_solve_box_ws(_code(dt), batch, n, _ptr(H), sH, _ptr(f), sf, _ptr(lbt), slb,
                                 _ptr(ubt), sub, _ptr(z), _ptr(status), int(max_iter), float(tol),
                                 _ptr(ws), wsb, _stream())
@@ -360,7 +382,8 @@ class PolyQP:
 
 # ------------------------------------------ general QP, per-instance rows
 def solve_qp(H, f, G=None, hl=None, hu=None, lb=None, ub=None, *, max_iter: int = 0,
-             tol: float = 0.0, out: tuple | None = None, presweep: bool = True):
+             tol: float = 0.0, out: tuple | None = None, presweep: bool = True,
+             ws: torch.Tensor | None = None):
     """Batched  min 1/2 z'Hz + f'z  s.t.  lb <= z <= ub,  hl <= G z <= hu.
 
     Every operand may be per instance (leading batch dim) or shared: H packed
@@ -370,6 +393,7 @@ def solve_qp(H, f, G=None, hl=None, hu=None, lb=None, ub=None, *, max_iter: int 
     (``mpcqp_solve_qp_ws``) unless ``presweep=False``.
     Returns (z, y, status); y (batch, m) are the row multipliers
     (y > 0 at the upper bound, y < 0 at the lower bound).
+    ``ws``: optional caller-owned scratch (``workspace_bytes(dtype, batch, n, m)``).
     """
     dt, dev = f.dtype, f.device
     f = _dev(f, dt, dev)
@@ -403,7 +427,7 @@ def solve_qp(H, f, G=None, hl=None, hu=None, lb=None, ub=None, *, max_iter: int 
         z, y, status = out
     lib = _lib()
     wsb = int(lib.mpcqp_solve_qp_workspace(_code(dt), batch, n, m)) if presweep else 0
-    ws = _workspace(wsb, dev)
+    ws = _workspace(wsb, dev, ws)
     rc = lib.mpcqp_solve_qp_ws(_code(dt), batch, n, m, _ptr(H), sH, _ptr(f), sf, _ptr(G), sG,
                                _ptr(hl), _ptr(hu), sh, _ptr(lbt), slb, _ptr(ubt), sub, _ptr(z),
                                _ptr(y), _ptr(status), int(max_iter), float(tol), _ptr(ws), wsb,

@@ -80,7 +80,11 @@ def solve_discrete_are(A, B, Q, R, tol: float = 1e-13, max_horizon: int = 1 << 1
             return P[0]
         prev = P[0]
         N *= 2
-    return prev
+    # scipy.linalg.solve_discrete_are (FHC.py:97,126) raises when it fails;
+    # so does this limit when the recursion has not settled by max_horizon
+    raise np.linalg.LinAlgError(
+        f"solve_discrete_are: Riccati recursion not converged to tol={tol:g} "
+        f"within horizon {max_horizon}")
 
 
 class AutoCruising(LinearSystem):

@@ -25,6 +25,7 @@ collision rows of main.py:95-104 are non-convex and out of scope.
 from __future__ import annotations
 
 import inspect
+import warnings
 
 import numpy as np
 import torch
@@ -40,9 +41,23 @@ class MPCController:
                  state_box: bool = True, dtype=torch.float64, device=None) -> None:
         self.N = N
         self.ts = ts
-        self.params = params or VehicleParameters()
+        # The prediction model is linearised on device (mpcqp_bicycle_rti),
+        # which reads the kinematic parameters; a model passed in (main.py:
+        # 250-251 passes KinematicBicycle(params)) therefore supplies them.
+        mparams = getattr(model, "params", None) if model is not None else None
+        if params is None:
+            params = mparams or VehicleParameters()
+        elif mparams is not None and _kinematic(mparams) != _kinematic(params):
+            raise ValueError("MPCController: model.params and params disagree on the "
+                             "kinematic fields (axis_front, axis_rear, acceleration, friction); "
+                             "the device linearisation can use only one set")
+        self.params = params
         self.model = model or KinematicBicycle(self.params)
         self.x_obs = x_obs
+        if x_obs is not None:
+            warnings.warn("MPCController: x_obs is ignored -- the collision rows of "
+                          "main.py:95-104 are non-convex and not part of the QP path",
+                          stacklevel=2)
         self.nx, self.nu = 4, 2
         # weights of main.py:72-74
         Q = np.diag([1., 6., 0.2, 0.05]) if Q is None else np.asarray(Q, float)
@@ -56,13 +71,11 @@ class MPCController:
         self.Q, self.QN, self.R = t(Q), t(QN), t(R)
         p = self.params
         # input box of main.py:68-69 (drive, steer), repeated over the horizon
-        self.lb_inputs = np.array([p.min_drive, -p.max_steer])
-        self.ub_inputs = np.array([p.max_drive, p.max_steer])
+        self.lb_inputs, self.ub_inputs = p.input_box()
         self.lbz = t(np.tile(self.lb_inputs, N))
         self.ubz = t(np.tile(self.ub_inputs, N))
         # state box of main.py:58-61 on x_1..x_N (the g rows of main.py:99-100)
-        self.lb_states = np.array([p.min_pos_x, p.min_pos_y, p.min_heading, p.min_vel])
-        self.ub_states = np.array([p.max_pos_x, p.max_pos_y, p.max_heading, p.max_vel])
+        self.lb_states, self.ub_states = p.state_box()
         self.state_box = state_box
         if state_box and N * (self.nx + self.nu) > batched.max_qp_size(dtype):
             raise ValueError(f"state box needs N*(nx+nu) <= {batched.max_qp_size(dtype)} (N={N})")
@@ -136,6 +149,11 @@ class MPCController:
     def __call__(self, y):
         """main.py:121-129: solve for measured state y, return u[0]."""
         return self.reshape_input(self.solve(y))[0]
+
+
+def _kinematic(p) -> tuple:
+    """The parameter fields the device bicycle model reads (bicycle.hip)."""
+    return (float(p.axis_front), float(p.axis_rear), float(p.acceleration), float(p.friction))
 
 
 def simulate(x0, dynamics, n_steps: int, policy):

@@ -66,3 +66,38 @@ class ControllerLog:
     solver_success: list = field(default_factory=list)
     state_prediction: list = field(default_factory=list)
     input_prediction: list = field(default_factory=list)
+
+
+def state_box_rows(problem: Problem, x0, N: int | None = None):
+    """The state box x_min <= x_k <= x_max on x_1..x_N of a session-2/3
+    ``Problem`` in condensed form, as the rows of ``batched.solve_poly`` /
+    ``batched.solve_qp``:
+
+        x_k = A^k x0 + sum_{j<k} A^{k-1-j} B u_j     (stage-major z = [u_0..u_{N-1}])
+        hl = x_min - Phi x0  <=  Gam z  <=  x_max - Phi x0 = hu
+
+    x0 is (nx,) or (batch, nx).  Returns (G (N*nx, N*nu), hl, hu) with hl/hu
+    (N*nx,) or (batch, N*nx).  Host-side problem setup (numpy), like the
+    reference's own problem data (session_2/problem.py:4-33)."""
+    N = problem.N if N is None else int(N)
+    A = np.asarray(problem.A, float)
+    B = np.asarray(problem.B, float)
+    nx, nu = B.shape
+    x0 = np.asarray(x0, float)
+    single = x0.ndim == 1
+    X0 = x0.reshape(-1, nx)
+    G = np.zeros((N * nx, N * nu))
+    Phi = np.zeros((N * nx, nx))
+    Ak = np.eye(nx)
+    AkB = [B]
+    for k in range(N):
+        Ak = A @ Ak
+        Phi[k * nx:(k + 1) * nx] = Ak
+        if k:
+            AkB.append(A @ AkB[-1])
+        for j in range(k + 1):
+            G[k * nx:(k + 1) * nx, j * nu:(j + 1) * nu] = AkB[k - j]
+    free = X0 @ Phi.T
+    hl = np.tile(problem.x_min, N)[None, :] - free
+    hu = np.tile(problem.x_max, N)[None, :] - free
+    return (G, hl[0], hu[0]) if single else (G, hl, hu)

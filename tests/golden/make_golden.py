@@ -14,6 +14,8 @@ boxqp_cfg2.npz -- config 2 (double integrator of FHC.py:136-142, N=20,
                  cross-checked against the oracle active-set solver and
                  certified by KKT residuals (the reference's own solver,
                  CasADi/IPOPT, is not installed: parity vs IPOPT unpinned).
+vehicle.npz   -- every field of session_4's ``VehicleParameters`` dataclass,
+                 imported from /root/reference/session_4/parameters.py.
 polyqp_s2.npz -- session-2/3 problem data with input box and state box
                  (x_1..x_N), solved by the Goldfarb-Idnani oracle, KKT
                  certified.
@@ -154,6 +156,21 @@ def make_problems():
     return out
 
 
+def make_vehicle():
+    import dataclasses
+    import importlib
+
+    sys.path.insert(0, os.path.join(REF, "session_4"))
+    mod = importlib.import_module("parameters")
+    p = mod.VehicleParameters()
+    out = {f.name: np.array(float(getattr(p, f.name))) for f in dataclasses.fields(p)}
+    out["_field_order"] = np.array([f.name for f in dataclasses.fields(p)])
+    del sys.modules["parameters"]
+    sys.path.pop(0)
+    np.savez_compressed(os.path.join(HERE, "vehicle.npz"), **out)
+    return out
+
+
 def make_boxqp_cfg2(s1):
     from oracle import condense as oc
     from oracle import qp as oq
@@ -209,6 +226,7 @@ def make_polyqp_s2(pr):
 if __name__ == "__main__":
     s1 = make_session1()
     pr = make_problems()
+    make_vehicle()
     make_boxqp_cfg2(s1)
     make_polyqp_s2(pr)
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

@@ -156,3 +156,27 @@ def test_mpc_closed_loop_reaches_origin(dev):
     xs = mpc.simulate(np.array([0.3, -0.1, 0.0, 0.0]), fwd_euler(KinematicBicycle(p), 0.08), 60, ctrl)
     assert xs.shape == (61, 4)
     assert np.linalg.norm(xs[-1]) < np.linalg.norm(xs[0])
+
+
+def test_dare_limit_raises_when_not_converged(dev):
+    """scipy's solve_discrete_are (FHC.py:97) raises on failure; the Riccati
+    limit must not hand back an unconverged iterate either."""
+    A = np.array([[1.0]])
+    B = np.array([[1e-4]])  # convergence time ~1/(B sqrt(Q/R)) = 1e4 stages
+    with pytest.raises(np.linalg.LinAlgError):
+        fhc.solve_discrete_are(A, B, np.eye(1), np.eye(1), max_horizon=256)
+    P = fhc.solve_discrete_are(np.array([[1.0]]), np.array([[1.0]]), np.eye(1), np.eye(1))
+    assert abs(P[0, 0] - (1 + 5 ** 0.5) / 2) < 1e-12  # P = 1 + P/(1+P)
+
+
+def test_mpc_controller_uses_model_params(dev):
+    """A controller built on a plant with changed friction (session4_sol.py:
+    461-462) linearises with that friction, not the nominal one."""
+    from model_predictive_control_amd.bicycle import KinematicBicycle
+
+    p = VehicleParameters(friction=0.8)
+    ctrl = mpc.MPCController(20, 0.08, model=KinematicBicycle(p), sqp_iters=1, state_box=False)
+    assert ctrl.params.friction == 0.8
+    nominal = mpc.MPCController(20, 0.08, sqp_iters=1, state_box=False)
+    x0 = np.array([0.3, -0.1, 0.0, 0.4])
+    assert np.abs(ctrl.solve(x0)["x"] - nominal.solve(x0)["x"]).max() > 1e-6

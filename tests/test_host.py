@@ -61,6 +61,45 @@ def test_problems_match_reference(golden):
     assert log.solver_success == [] and log.state_prediction == [] and log.input_prediction == []
 
 
+def test_vehicle_parameters_match_reference(golden):
+    """Field names, order and defaults of session_4/parameters.py:4-54."""
+    import dataclasses
+
+    ref = golden("vehicle.npz")
+    p = VehicleParameters()
+    names = [f.name for f in dataclasses.fields(p)]
+    assert names == [str(s) for s in ref["_field_order"]]
+    for k in names:
+        assert float(getattr(p, k)) == float(ref[k]), k
+    assert VehicleParameters(max_steer=0.2).max_steer == 0.2
+    lo, hi = p.input_box()
+    assert np.array_equal(lo, [p.min_drive, -p.max_steer]) and np.array_equal(hi, [p.max_drive, p.max_steer])
+    lo, hi = p.state_box()  # [p_x, p_y, psi, v]  (main.py:58-61)
+    assert np.array_equal(lo, [p.min_pos_x, p.min_pos_y, p.min_heading, p.min_vel])
+    assert np.array_equal(hi, [p.max_pos_x, p.max_pos_y, p.max_heading, p.max_vel])
+
+
+def test_state_box_rows_rollout():
+    """Condensed state box rows: Gam z + Phi x0 is the rollout of z."""
+    p = problems.Problem()
+    rng = np.random.default_rng(3)
+    X0 = rng.normal(size=(5, 2))
+    G, hl, hu = problems.state_box_rows(p, X0, N=7)
+    assert G.shape == (14, 7) and hl.shape == (5, 14) and hu.shape == (5, 14)
+    z = rng.normal(size=7)
+    for b in range(5):
+        x, xs = X0[b], []
+        for k in range(7):
+            x = p.A @ x + p.B @ z[k:k + 1]
+            xs.append(x)
+        xs = np.concatenate(xs)
+        # x_k in [x_min, x_max]  <=>  hl <= G z <= hu
+        assert np.allclose(G @ z - hl[b], xs - np.tile(p.x_min, 7))
+        assert np.allclose(hu[b] - G @ z, np.tile(p.x_max, 7) - xs)
+    G1, hl1, _ = problems.state_box_rows(p, X0[0])
+    assert G1.shape == (p.N * 2, p.N) and hl1.shape == (p.N * 2,)
+
+
 def test_bicycle_batched_matches_numpy_and_fd():
     p = VehicleParameters()
     rng = np.random.default_rng(0)
@@ -119,3 +158,20 @@ def test_gloo_world2_shard_gather(tmp_path, total):
     mp.spawn(_gloo_worker, args=(2, port, total, out), nprocs=2, join=True)
     res = torch.load(out, weights_only=True)
     assert res["ok"] and res["max"] == 2.0
+
+
+def test_mpc_controller_model_params_and_x_obs():
+    """MPCController plans with the model's kinematic parameters; a conflicting
+    params argument is an error, and x_obs (collision rows) is ignored with a
+    warning -- checked before any device work, so on CPU."""
+    from model_predictive_control_amd import mpc
+
+    bad = VehicleParameters(friction=0.8)
+    with pytest.raises(ValueError):
+        mpc.MPCController(10, 0.08, VehicleParameters(), model=bicycle.KinematicBicycle(bad))
+    with pytest.warns(UserWarning):
+        with pytest.raises(RuntimeError):  # no GPU here: the device check comes next
+            mpc.MPCController(10, 0.08, x_obs=np.zeros(2))
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError):
+            mpc.MPCController(10, 0.08, model=bicycle.KinematicBicycle(bad))
