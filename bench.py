@@ -20,11 +20,13 @@ condensing really runs per instance, as the north star's "synthetic
 contract; they are parity/roofline cases and not the headline line:
   3  FE-linearised bicycle (parameters.py), N=30, ts=0.08, state box (x_1..x_N)
      + input box, per-instance per-stage (A_k, B_k, c_k), fp32, B=65,536:
-     mpcqp_condense(TV: H, f, Gam, xbar) + row bounds + mpcqp_solve_qp
+     mpcqp_mpc_qp (condense(TV) + rows + MFMA sweep + product-form active set
+     refined against the dynamics in fp64)
   4  random stable LTI nx=12, nu=4, N=50, 40 random polytope rows (h>0),
      shared condense, fp64, B=131,072 per GPU: f = F x0 + mpcqp_solve_poly
   5  config-4 plant perturbed per instance and stage, N=40, input box, fp32,
-     B=32,768 per GPU: mpcqp_condense(TV: H, f) + mpcqp_solve_box (n = 160)
+     B=32,768 per GPU: mpcqp_mpc_qp without state box (condense(TV, MFMA) +
+     sweep + product-form active set, n = 160)
 
 In every config the inputs are resident in HBM before the timed region, and
 steps cycle over distinct x0 batches ("slots").  Each slot's step is captured
@@ -322,37 +324,24 @@ class Config3:
         self.xmin, self.xmax = xmin, xmax
         self.lbz = t(np.tile([p.min_drive, -p.max_steer], N))
         self.ubz = t(np.tile([p.max_drive, p.max_steer], N))
-        self.out = {"H": torch.empty((bsz, n * (n + 1) // 2), dtype=dt, device=dev),
-                    "f": torch.empty((bsz, n), dtype=dt, device=dev),
-                    "Gam": torch.empty((bsz, m, n), dtype=dt, device=dev),
-                    "xbar": torch.empty((bsz, m), dtype=dt, device=dev)}
-        self.hl = torch.empty((bsz, m), dtype=dt, device=dev)
-        self.hu = torch.empty((bsz, m), dtype=dt, device=dev)
         self.Z = torch.empty((S, bsz, n), dtype=dt, device=dev)
         self.Y = torch.empty((bsz, m), dtype=dt, device=dev)
         self.ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
+        self.ws = torch.empty((batched.mpc_qp_workspace_bytes(dt, bsz, nx, self.nu, N),),
+                              dtype=torch.uint8, device=dev)
 
     def workload(self):
         return {"workload": "cfg3: FE-linearised bicycle (parameters.py), ts=0.08, N=30, "
                             "Q=diag(1,6,.2,.05), QN=100Q, R=diag(1,.01), state box x_1..x_N + "
                             "input box, per-instance per-stage (A_k,B_k,c_k) about the zero-input "
-                            "rollout; condense(TV) + solve_qp",
+                            "rollout; one mpcqp_mpc_qp call: condense(TV) + rows + sweep + pf "
+                            "(refined against the dynamics in fp64)",
                 "horizon": self.N, "nx": self.nx, "nu": self.nu, "rows": self.m}
 
-    def _condense(self, s):
-        batched.condense(self.A[s], self.B[s], self.Q_t, self.R_t, self.QN_t, self.N,
-                         x0=self.X0_t[s], c=self.c[s], tv=True, outputs=("H", "f", "Gam", "xbar"),
-                         out=self.out)
-        torch.sub(self.xmin_t, self.out["xbar"], out=self.hl)
-        torch.sub(self.xmax_t, self.out["xbar"], out=self.hu)
-
-    def _solve(self, s):
-        batched.solve_qp(self.out["H"], self.out["f"], self.out["Gam"], self.hl, self.hu,
-                         self.lbz, self.ubz, out=(self.Z[s], self.Y, self.ST[s]))
-
     def step(self, s):
-        self._condense(s)
-        self._solve(s)
+        batched.mpc_qp(self.A[s], self.B[s], self.Q_t, self.R_t, self.QN_t, self.N, self.X0_t[s],
+                       xlo=self.xmin_t, xhi=self.xmax_t, lb=self.lbz, ub=self.ubz, c=self.c[s],
+                       tv=True, out=(self.Z[s], self.Y, self.ST[s]), ws=self.ws)
 
     def status(self):
         return self.ST
@@ -360,46 +349,57 @@ class Config3:
     def kernels(self, traffic):
         R = self.args.reps
         bsz, nx, nu, N, n, m = self.args.batch, self.nx, self.nu, self.N, self.n, self.m
-        self._condense(0)
-        t_c = time_kernel(lambda: batched.condense(
-            self.A[0], self.B[0], self.Q_t, self.R_t, self.QN_t, self.N, x0=self.X0_t[0],
-            c=self.c[0], tv=True, outputs=("H", "f", "Gam", "xbar"), out=self.out), R, self.dev)
-        t_s = time_kernel(lambda: self._solve(0), R, self.dev)
-        t_w = sweep_time(self.out["H"], self.out["Gam"], n, m, R, self.dev)
-        t_p = max(t_s - t_w, 1e-6)
+        out = {"H": torch.empty((bsz, n * (n + 1) // 2), dtype=self.dtype, device=self.dev),
+               "f": torch.empty((bsz, n), dtype=self.dtype, device=self.dev),
+               "Gam": torch.empty((bsz, m, n), dtype=self.dtype, device=self.dev),
+               "xbar": torch.empty((bsz, m), dtype=self.dtype, device=self.dev)}
+
+        def cond():
+            batched.condense(self.A[0], self.B[0], self.Q_t, self.R_t, self.QN_t, self.N,
+                             x0=self.X0_t[0], c=self.c[0], tv=True,
+                             outputs=("H", "f", "Gam", "xbar"), out=out)
+        cond()
+        t_c = time_kernel(cond, R, self.dev)
+        t_s = time_kernel(lambda: self.step(0), R, self.dev)
+        t_w = sweep_time(out["H"], out["Gam"], n, m, R, self.dev)
+        del out
+        t_p = max(t_s - t_c - t_w, 1e-6)
         cb = condense_bytes_per_instance(nx, nu, N, 4, tv=True, gam=True, xbar=True) * bsz
-        sb = solve_bytes_per_instance(n, 4, m, G=True) * bsz
+        # pf reads M0, s0 and the dynamics (A_k, B_k, c_k, x0) for the refinement
+        pb = ((n + m) ** 2 + (n + m) + N * (nx * nx + nx * nu + nx) + nx + n + 2 * m) * 4 * bsz
         wf = sweep_flops_per_instance(n, m) * bsz
         r_c = roof("condense_kernel<float,4>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
                    traffic.get("condense"), {"bytes_per_launch": cb})
         r_w = roof("sweep_rows_kernel<4>", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
                    traffic.get("sweep"), {"flops_per_launch": wf})
-        r_p = roof("qp_pf_kernel<3>", "hbm", sb, t_p, HBM_PEAK_GBS, "GB/s",
-                   traffic.get("solve_pf"), {"bytes_per_launch": sb,
-                                             "note": "time = solve_qp - sweep"})
+        r_p = roof("qp_pf_kernel<3,true>", "hbm", pb, t_p, HBM_PEAK_GBS, "GB/s",
+                   traffic.get("solve_pf"), {"bytes_per_launch": pb,
+                                             "note": "time = mpc_qp - condense - sweep "
+                                                     "(includes the rows kernel)"})
         extra = {"kernel_us": {"condense": round(t_c * 1e3, 2), "sweep": round(t_w * 1e3, 2),
-                               "solve_pf": round(t_p * 1e3, 2), "solve_qp": round(t_s * 1e3, 2)}}
+                               "solve_pf": round(t_p * 1e3, 2), "mpc_qp": round(t_s * 1e3, 2)}}
         rs = sorted([(t_c, r_c), (t_w, r_w), (t_p, r_p)], key=lambda x: -x[0])
         return rs[0][1], {"roofline_other": [r for _, r in rs[1:]]}, extra
 
     def check(self):
         """fp64 oracle (explicit condensing + Goldfarb-Idnani) on a few
-        instances of slot 0, from the same (A_k, B_k, c_k, x0)."""
+        instances of slot 0, from the same fp32-valued (A_k, B_k, c_k, x0,
+        weights, bounds) the device saw."""
         from oracle import condense as oc
         from oracle import qp as oq
 
-        N, nu = self.N, self.nu
+        N = self.N
+        r = lambda t: t.double().cpu().numpy()  # noqa: E731
         errs = []
-        A, B, c = self.A[0].double().cpu().numpy(), self.B[0].double().cpu().numpy(), \
-            self.c[0].double().cpu().numpy()
+        A, B, c, X0 = r(self.A[0]), r(self.B[0]), r(self.c[0]), r(self.X0_t[0])
+        Q, QN, Rm = r(self.Q_t), r(self.QN_t), r(self.R_t)
+        xlo, xhi, lb, ub = r(self.xmin_t), r(self.xmax_t), r(self.lbz), r(self.ubz)
         Z = self.Z[0].double().cpu().numpy()
         code = batched.status_code(self.ST[0]).cpu().numpy()
-        for i in range(min(4, self.args.batch)):
-            d = oc.condense(A[i], B[i], self.Qn, self.Rn, self.QNn, N, x0=self.X0[0, i], c=c[i])
+        for i in range(min(self.args.check, self.args.batch)):
+            d = oc.condense(A[i], B[i], Q, Rm, QN, N, x0=X0[i], c=c[i])
             G = np.vstack([d["Gam"], -d["Gam"]])
-            h = np.concatenate([np.tile(self.xmax, N) - d["xbar"], -(np.tile(self.xmin, N) - d["xbar"])])
-            lb = np.tile([self.p.min_drive, -self.p.max_steer], N)
-            ub = np.tile([self.p.max_drive, self.p.max_steer], N)
+            h = np.concatenate([xhi - d["xbar"], -(xlo - d["xbar"])])
             try:
                 zr = oq.poly_qp(d["H"], d["f"], G, h, lb, ub)[0]
             except ValueError:
@@ -552,29 +552,24 @@ class Config5:
             self.X0_t.append((3.0 * torch.randn((bsz, nx), generator=g, device=dev, dtype=dt)).contiguous())
         self.Q_t, self.R_t = t(self.Qn), t(self.Rn)
         self.lb, self.ub = -0.5, 0.5
-        self.out = {"H": torch.empty((bsz, n * (n + 1) // 2), dtype=dt, device=dev),
-                    "f": torch.empty((bsz, n), dtype=dt, device=dev)}
         self.Z = torch.empty((S, bsz, n), dtype=dt, device=dev)
         self.ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
         self.lb_t = torch.full((n,), self.lb, dtype=dt, device=dev)
         self.ub_t = torch.full((n,), self.ub, dtype=dt, device=dev)
+        self.ws = torch.empty((batched.mpc_qp_workspace_bytes(dt, bsz, nx, nu, N, False),),
+                              dtype=torch.uint8, device=dev)
 
     def workload(self):
         return {"workload": "cfg5: config-4 plant (nx=12, nu=4) with per-instance per-stage "
                             "perturbation A_k=A+0.01*D_k, B_k=B+0.01*E_k, N=40, |u|<=0.5, "
-                            "re-condensed every step: condense(TV) + solve_box (n=160)",
+                            "re-condensed every step; one mpcqp_mpc_qp call: condense(TV, MFMA) + "
+                            "sweep (n=160) + pf (refined against the dynamics in fp64)",
                 "horizon": self.N, "nx": self.nx, "nu": self.nu}
 
-    def _condense(self, s):
-        batched.condense(self.A[s], self.B[s], self.Q_t, self.R_t, self.Q_t, self.N,
-                         x0=self.X0_t[s], tv=True, outputs=("H", "f"), out=self.out)
-
-    def _solve(self, s):
-        batched.solve_box(self.out["H"], self.out["f"], self.lb_t, self.ub_t, out=(self.Z[s], self.ST[s]))
-
     def step(self, s):
-        self._condense(s)
-        self._solve(s)
+        batched.mpc_qp(self.A[s], self.B[s], self.Q_t, self.R_t, self.Q_t, self.N, self.X0_t[s],
+                       lb=self.lb_t, ub=self.ub_t, tv=True, out=(self.Z[s], None, self.ST[s]),
+                       ws=self.ws)
 
     def status(self):
         return self.ST
@@ -582,11 +577,18 @@ class Config5:
     def kernels(self, traffic):
         R = self.args.reps
         bsz, nx, nu, N, n = self.args.batch, self.nx, self.nu, self.N, self.n
-        self._condense(0)
-        t_c = time_kernel(lambda: self._condense(0), R, self.dev)
-        t_s = time_kernel(lambda: self._solve(0), R, self.dev)
-        t_w = sweep_time(self.out["H"], None, n, 0, R, self.dev)
-        t_p = max(t_s - t_w, 1e-6)
+        out = {"H": torch.empty((bsz, n * (n + 1) // 2), dtype=self.dtype, device=self.dev),
+               "f": torch.empty((bsz, n), dtype=self.dtype, device=self.dev)}
+
+        def cond():
+            batched.condense(self.A[0], self.B[0], self.Q_t, self.R_t, self.Q_t, self.N,
+                             x0=self.X0_t[0], tv=True, outputs=("H", "f"), out=out)
+        cond()
+        t_c = time_kernel(cond, R, self.dev)
+        t_s = time_kernel(lambda: self.step(0), R, self.dev)
+        t_w = sweep_time(out["H"], None, n, 0, R, self.dev)
+        del out
+        t_p = max(t_s - t_c - t_w, 1e-6)
         fl = condense_flops_per_instance(nx, nu, N) * bsz
         cb = condense_bytes_per_instance(nx, nu, N, 4, tv=True) * bsz
         # the survey's condensing flop formula counts the explicit Gam'QGam
@@ -598,12 +600,13 @@ class Config5:
         wf = sweep_flops_per_instance(n) * bsz
         r_w = roof("sweep_mfma_kernel<10>", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
                    traffic.get("sweep"), {"flops_per_launch": wf})
-        sb = solve_bytes_per_instance(n, 4) * bsz
-        r_p = roof("qp_pf_kernel<3>", "hbm", sb, t_p, HBM_PEAK_GBS, "GB/s",
-                   traffic.get("solve_pf"), {"bytes_per_launch": sb,
-                                             "note": "time = solve_box - sweep"})
+        # pf reads M0, s0 and the dynamics (A_k, B_k, x0) for the refinement
+        pb = (n * n + n + N * (nx * nx + nx * nu) + nx + n) * 4 * bsz
+        r_p = roof("qp_pf_kernel<3,true>", "hbm", pb, t_p, HBM_PEAK_GBS, "GB/s",
+                   traffic.get("solve_pf"), {"bytes_per_launch": pb,
+                                             "note": "time = mpc_qp - condense - sweep"})
         extra = {"kernel_us": {"condense": round(t_c * 1e3, 2), "sweep": round(t_w * 1e3, 2),
-                               "solve_pf": round(t_p * 1e3, 2), "solve_box": round(t_s * 1e3, 2)}}
+                               "solve_pf": round(t_p * 1e3, 2), "mpc_qp": round(t_s * 1e3, 2)}}
         rs = sorted([(t_c, r_c), (t_w, r_w), (t_p, r_p)], key=lambda x: -x[0])
         return rs[0][1], {"roofline_other": [r for _, r in rs[1:]]}, extra
 
@@ -614,10 +617,11 @@ class Config5:
         N = self.N
         A, B = self.A[0].double().cpu().numpy(), self.B[0].double().cpu().numpy()
         X0 = self.X0_t[0].double().cpu().numpy()
+        Q, Rm = self.Q_t.double().cpu().numpy(), self.R_t.double().cpu().numpy()
         Z = self.Z[0].double().cpu().numpy()
         errs = []
-        for i in range(min(2, self.args.batch)):
-            d = oc.condense(A[i], B[i], self.Qn, self.Rn, self.Qn, N, x0=X0[i])
+        for i in range(min(self.args.check, self.args.batch)):
+            d = oc.condense(A[i], B[i], Q, Rm, Q, N, x0=X0[i])
             zr = oq.box_qp(d["H"], d["f"], np.full(self.n, self.lb), np.full(self.n, self.ub))[0]
             errs.append(np.abs(Z[i] - zr).max())
         return float(max(errs))
@@ -657,6 +661,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--reps", type=int, default=20, help="launches per kernel-timing graph")
+    ap.add_argument("--check", type=int, default=16, help="instances checked against the oracle")
     ap.add_argument("--mode", choices=("fused", "split"), default="fused", help="config 2 only")
     ap.add_argument("--traffic", default=None,
                     help="JSON with PMC-measured HBM bytes per launch {kernel: bytes} "

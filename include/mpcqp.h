@@ -16,6 +16,10 @@
  *                       (lbx/ubx, main.py:68-69,97-98).
  *   mpcqp_mpc_box    <- both of the above fused for the input-box OCP
  *                       (MPCController.solve end to end, one launch).
+ *   mpcqp_mpc_qp     <- MPCController.solve end to end with the input box AND
+ *                       the state box (main.py:58-61,68-69; session4_sol.py:
+ *                       176-181): condense + QP in one call, fp32 refined
+ *                       against the dynamics in fp64.
  *   mpcqp_solve_poly <- the same call with general rows hl <= G z <= hu (state box
  *                       lbg/ubg of main.py:58-61,99-100 after condensing, or
  *                       arbitrary polytopes -- BASELINE config 4).
@@ -250,6 +254,39 @@ int mpcqp_solve_box_ws(int dtype, int batch, int n,
                        const void* lb, int64_t strideLb, const void* ub, int64_t strideUb,
                        void* z, int32_t* status, int max_iter, double tol,
                        void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * One MPC step with input box and state box, end to end (the whole
+ * MPCController.solve of session_4/main.py:115-116 for the OCP of
+ * main.py:41-113 with lbx/ubx, main.py:68-69, and lbg/ubg on x_1..x_N,
+ * main.py:58-61; session4_sol.py:176-181):
+ *     min  sum_{k<N} x_k'Q x_k + u_k'R u_k + x_N'Qf x_N
+ *     s.t. x_{k+1} = A_k x_k + B_k u_k + c_k,   lb <= z <= ub,
+ *          xlo <= [x_1; ..; x_N] <= xhi
+ * Plant, weights, c and x0 exactly as in mpcqp_condense (flags MPCQP_TV);
+ * xlo/xhi (N*nx, stride strideXb, 0 = shared; both NULL = no state box,
+ * one NULL = unbounded on that side); lb/ub (N*nu) as in mpcqp_solve_box.
+ * Outputs: z (N*nu), y (optional, N*nx: state-row multipliers, > 0 at xhi),
+ * X (optional, N*nx: x_1..x_N of z, the IPOPT "g" rows), status.
+ * Pipeline: mpcqp_condense -> rows -> (fp32, N(nu+nx) > 64) MFMA sweep ->
+ * product-form active set -> iterative refinement whose KKT residual is
+ * computed from the DYNAMICS in fp64 (forward rollout + adjoint), so the
+ * fp32 path converges to the solution of the QP its inputs define rather
+ * than to that of the fp32-rounded condensed matrices; fp64 or small QPs:
+ * the workgroup QP kernel.  Limits: nx, nu <= 16, N*(nu + nx) (state box) or
+ * N*nu <= mpcqp_max_qp_size(dtype).  workspace: mpcqp_mpc_qp_workspace()
+ * bytes of device scratch (state_box = 1 when xlo or xhi is given).
+ */
+size_t mpcqp_mpc_qp_workspace(int dtype, int batch, int nx, int nu, int N, int state_box);
+int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
+                 const void* A, int64_t strideA, const void* Bm, int64_t strideB,
+                 const void* Q, int64_t strideQ, const void* R, int64_t strideR,
+                 const void* Qf, int64_t strideQf, const void* c, int64_t strideC,
+                 const void* x0, int64_t strideX0,
+                 const void* xlo, const void* xhi, int64_t strideXb,
+                 const void* lb, int64_t strideLb, const void* ub, int64_t strideUb,
+                 void* z, void* y, void* X, int32_t* status, int max_iter, double tol,
+                 void* ws, size_t ws_bytes, void* stream);
 
 /*
  * Batched finite-horizon Riccati recursion, FHC.py:51-61:

@@ -60,6 +60,11 @@ SIGNATURES = {
                                _vp]),
     "mpcqp_solve_box_ws": (_i, [_i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                                 _vp, _vp, _i, _d, _vp, ctypes.c_size_t, _vp]),
+    "mpcqp_mpc_qp_workspace": (ctypes.c_size_t, [_i, _i, _i, _i, _i, _i]),
+    "mpcqp_mpc_qp": (_i, [_i, _i, _i, _i, _i, _i,
+                          _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
+                          _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
+                          _vp, _vp, _vp, _vp, _i, _d, _vp, ctypes.c_size_t, _vp]),
     "mpcqp_riccati": (_i, [_i, _i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                            _vp, _i64, _vp, _vp, _vp]),
     "mpcqp_bicycle_rti": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _i64, _vp, _i64,

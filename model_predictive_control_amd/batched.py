@@ -24,7 +24,7 @@ import torch
 from . import _native as nat
 
 __all__ = [
-    "condense", "solve_box", "mpc_box", "solve_poly", "solve_qp", "sweep", "riccati", "gemv",
+    "condense", "solve_box", "mpc_box", "mpc_qp", "solve_poly", "solve_qp", "sweep", "riccati", "gemv",
     "rollout",
     "pack_lower", "unpack_lower", "status_code", "status_iters", "workspace_bytes",
 ]
@@ -227,6 +227,85 @@ def mpc_box(A, B, Q, R, Qf, N: int, x0, lb=None, ub=None, c=None, *, tv: bool = 
         float(tol), _stream())
     nat.check(rc, "mpcqp_mpc_box")
     return z, status
+
+
+# --------------------------------------- fused condense + state/input box
+def mpc_qp_workspace_bytes(dtype: torch.dtype, batch: int, nx: int, nu: int, N: int,
+                           state_box: bool = True) -> int:
+    """Bytes of the ``ws=`` buffer ``mpc_qp`` needs."""
+    return int(_lib().mpcqp_mpc_qp_workspace(_code(dtype), batch, nx, nu, N, int(bool(state_box))))
+
+
+def mpc_qp(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=None, *,
+           tv: bool = False, states: bool = False, max_iter: int = 0, tol: float = 0.0,
+           out: tuple | None = None, ws: torch.Tensor | None = None):
+    """One MPC step with input box and state box, end to end (include/mpcqp.h
+    ``mpcqp_mpc_qp``): condense + QP, fp32 refined against the dynamics.
+
+    Plant conventions as ``condense``; xlo/xhi: state bounds on x_1..x_N,
+    (nx,) repeated over the horizon, (N*nx,) shared or (b, N*nx); lb/ub as
+    ``mpc_box``.  Returns (z (b, N*nu), y (b, N*nx) or None, status[, X
+    (b, N, nx) when ``states``]); y are the state-row multipliers (> 0 at xhi).
+    """
+    dt = A.dtype if isinstance(A, torch.Tensor) else torch.float64
+    dev = A.device if isinstance(A, torch.Tensor) else torch.device("cuda")
+    A, B, Q, R, Qf = (_dev(v, dt, dev) for v in (A, B, Q, R, Qf))
+    x0, c = _dev(x0, dt, dev), _dev(c, dt, dev)
+    nx, nu = int(B.shape[-2]), int(B.shape[-1])
+    if R.ndim == 1:
+        R = R.expand(nu, nu).contiguous()
+    n, m = N * nu, N * nx
+    base = 3 if tv else 2
+    sA, bA = _inst(A, base, "A")
+    sB, bB = _inst(B, base, "B")
+    sQ, bQ = _inst(Q, 2, "Q")
+    sR, bR = _inst(R, 2, "R")
+    sQf, bQf = _inst(Qf, 2, "Qf")
+    sC, bC = _inst(c, 2, "c")
+    sX, bX = _inst(x0, 1, "x0")
+
+    def sbound(v):
+        if v is None:
+            return None, 0, None
+        t = _dev(v, dt, dev)
+        if t.ndim == 1 and t.shape[0] == nx and nx != m:
+            t = t.repeat(N)
+        s, bb = _inst(t, 1, "state bound")
+        if t.shape[-1] != m:
+            raise ValueError(f"state bounds need {m} (= N*nx) entries, got {tuple(t.shape)}")
+        return t, s, bb
+
+    xlo_t, sxl, bxl = sbound(xlo)
+    xhi_t, sxh, bxh = sbound(xhi)
+    if xlo_t is not None and xhi_t is not None and sxl != sxh:
+        raise ValueError("xlo and xhi must both be shared or both per instance")
+    sXb = max(sxl, sxh)
+    lbt, slb = _bound(lb, n, dt, dev)
+    ubt, sub = _bound(ub, n, dt, dev)
+    batch = _batch_of((sA, bA), (sB, bB), (sQ, bQ), (sR, bR), (sQf, bQf), (sC, bC), (sX, bX),
+                      (sxl, bxl), (sxh, bxh),
+                      (slb, lbt.shape[0] if lbt is not None and lbt.ndim == 2 else None),
+                      (sub, ubt.shape[0] if ubt is not None and ubt.ndim == 2 else None))
+    sbox = xlo_t is not None or xhi_t is not None
+    if out is None:
+        z = torch.empty((batch, n), dtype=dt, device=dev)
+        y = torch.empty((batch, m), dtype=dt, device=dev) if sbox else None
+        status = torch.empty((batch,), dtype=torch.int32, device=dev)
+        X = torch.empty((batch, N, nx), dtype=dt, device=dev) if states else None
+    else:
+        z, y, status = out[:3]
+        X = out[3] if len(out) > 3 else None
+    lib = _lib()
+    wsb = int(lib.mpcqp_mpc_qp_workspace(_code(dt), batch, nx, nu, N, int(sbox)))
+    ws = _workspace(wsb, dev, ws)
+    rc = lib.mpcqp_mpc_qp(
+        _code(dt), batch, nx, nu, N, nat.TV if tv else 0,
+        _ptr(A), sA, _ptr(B), sB, _ptr(Q), sQ, _ptr(R), sR, _ptr(Qf), sQf, _ptr(c), sC,
+        _ptr(x0), sX, _ptr(xlo_t), _ptr(xhi_t), sXb, _ptr(lbt), slb, _ptr(ubt), sub,
+        _ptr(z), _ptr(y), _ptr(X), _ptr(status), int(max_iter), float(tol), _ptr(ws), wsb,
+        _stream())
+    nat.check(rc, "mpcqp_mpc_qp")
+    return (z, y, status, X) if states else (z, y, status)
 
 
 # ----------------------------------------------------------------- box QP

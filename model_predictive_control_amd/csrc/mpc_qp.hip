@@ -1,0 +1,222 @@
+// mpc_qp.hip -- one MPC step with input box AND state box, end to end:
+// the whole MPCController.solve of session_4/main.py:115-116 for the OCP of
+// main.py:41-113 with the input bounds lbx/ubx (main.py:68-69) and the state
+// bounds lbg/ubg on x_1..x_N (main.py:58-61, session4_sol.py:176-181),
+// linear(ised) dynamics.  BASELINE configs 3 (state + input box) and 5
+// (input box only, the large horizon).
+//
+//   1. mpcqp_condense (TV or shared plant)    -> H, f [, Gam, xbar]   (workspace)
+//   2. rows_kernel                            -> hl = xlo - xbar, hu = xhi - xbar
+//   3. fp32 with n + m > 64: sweep (MFMA) -> product-form active set whose
+//      iterative refinement takes its KKT residual from the DYNAMICS in fp64
+//      (solve_pf.hip, PfDyn) -> workgroup kernel for hand-offs;
+//      otherwise (fp64, small QPs): the workgroup kernel (mpcqp_solve_qp).
+//   4. optional: states_kernel -> X = x_1..x_N of the solution (fp64 rollout),
+//      the "g" rows IPOPT reports and the state_prediction of the
+//      ControllerLog (session_2/log.py:12).
+//
+// The refinement residual from the dynamics is what lets the fp32 path reach
+// the fp64 solution of the QP its inputs define: the condensed H, Gam, xbar
+// carry fp32 rounding of the recursion (cond(H) ~ 1e4 at config 3), which a
+// residual from them cannot see.
+#include <cstdlib>
+
+#include "pf.hpp"
+#include "quad_api.hpp"
+
+namespace mpcqp {
+
+template <typename T>
+__global__ void rows_kernel(int64_t total, int m, const T* xlo, const T* xhi, int64_t sXb,
+                            const T* xbar, T* hl, T* hu) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int64_t b = e / m;
+  const int j = (int)(e - b * m);
+  const T xb = xbar[e];
+  const T inf = Lim<T>::inf();
+  hl[e] = (xlo ? xlo[b * sXb + j] : -inf) - xb;
+  hu[e] = (xhi ? xhi[b * sXb + j] : inf) - xb;
+}
+
+// X = [x_1; ..; x_N] of z, one instance per lane, fp64 accumulation.
+template <typename T, int NX>
+__global__ void states_kernel(int batch, int nx, int nu, int N, int tv, const T* A, int64_t sA,
+                              const T* Bm, int64_t sB, const T* c, int64_t sC, const T* x0,
+                              int64_t sX0, const T* z, T* X) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  double x[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) x[i] = i < nx ? (double)x0[(int64_t)b * sX0 + i] : 0.0;
+  const T* Ab = A + (int64_t)b * sA;
+  const T* Bb = Bm + (int64_t)b * sB;
+  const T* cb = c ? c + (int64_t)b * sC : nullptr;
+  const T* zb = z + (int64_t)b * N * nu;
+  T* Xb = X + (int64_t)b * N * nx;
+  for (int s = 0; s < N; ++s) {
+    const T* As = Ab + (tv ? (int64_t)s * nx * nx : 0);
+    const T* Bs = Bb + (tv ? (int64_t)s * nx * nu : 0);
+    double xn[NX];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      double acc = (cb && i < nx) ? (double)cb[s * nx + i] : 0.0;
+#pragma unroll
+      for (int j = 0; j < NX; ++j)
+        if (i < nx && j < nx) acc = fma((double)As[i * nx + j], x[j], acc);
+      for (int a = 0; a < nu; ++a)
+        if (i < nx) acc = fma((double)Bs[i * nu + a], (double)zb[s * nu + a], acc);
+      xn[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      x[i] = xn[i];
+      if (i < nx) Xb[s * nx + i] = (T)xn[i];
+    }
+  }
+}
+
+static size_t al256(size_t v) { return (v + 255) / 256 * 256; }
+
+struct MpcWs {
+  size_t H, f, Gam, xbar, hl, hu, qp, total;
+};
+
+static MpcWs mpc_ws_layout(int dtype, int batch, int nx, int nu, int N, int sbox) {
+  const size_t es = dtype_size(dtype), B = (size_t)batch;
+  const size_t n = (size_t)N * nu, m = sbox ? (size_t)N * nx : 0;
+  MpcWs w{};
+  size_t o = 0;
+  w.H = o; o += al256(B * n * (n + 1) / 2 * es);
+  w.f = o; o += al256(B * n * es);
+  w.Gam = o; o += al256(B * m * n * es);
+  w.xbar = o; o += al256(B * m * es);
+  w.hl = o; o += al256(B * m * es);
+  w.hu = o; o += al256(B * m * es);
+  w.qp = o; o += al256(qp_ws_bytes(dtype, batch, (int)n, (int)m));
+  w.total = o;
+  return w;
+}
+
+// refinement steps with the dynamics residual (MPCQP_MPC_REFINE overrides)
+static int mpc_refine() {
+  const char* v = getenv("MPCQP_MPC_REFINE");
+  return v ? atoi(v) : 2;
+}
+
+template <typename T>
+static int launch_states(int batch, int nx, int nu, int N, int tv, const void* A, int64_t sA,
+                         const void* Bm, int64_t sB, const void* c, int64_t sC, const void* x0,
+                         int64_t sX0, const void* z, void* X, hipStream_t st) {
+  const dim3 grid((batch + 255) / 256), blk(256);
+#define MPCQP_STATES(NXT)                                                                     \
+  hipLaunchKernelGGL((states_kernel<T, NXT>), grid, blk, 0, st, batch, nx, nu, N, tv,         \
+                     (const T*)A, sA, (const T*)Bm, sB, (const T*)c, sC, (const T*)x0, sX0,   \
+                     (const T*)z, (T*)X)
+  if (nx <= 4) MPCQP_STATES(4);
+  else if (nx <= 8) MPCQP_STATES(8);
+  else if (nx <= 12) MPCQP_STATES(12);
+  else MPCQP_STATES(16);
+#undef MPCQP_STATES
+  MPCQP_CHECK_LAUNCH("states_kernel");
+  return MPCQP_OK;
+}
+
+}  // namespace mpcqp
+
+extern "C" size_t mpcqp_mpc_qp_workspace(int dtype, int batch, int nx, int nu, int N,
+                                         int state_box) {
+  if ((dtype != MPCQP_F64 && dtype != MPCQP_F32) || batch <= 0 || nx < 1 || nu < 1 || N < 1)
+    return 0;
+  return mpcqp::mpc_ws_layout(dtype, batch, nx, nu, N, state_box ? 1 : 0).total;
+}
+
+extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
+                            const void* A, int64_t strideA, const void* Bm, int64_t strideB,
+                            const void* Q, int64_t strideQ, const void* R, int64_t strideR,
+                            const void* Qf, int64_t strideQf, const void* c, int64_t strideC,
+                            const void* x0, int64_t strideX0, const void* xlo, const void* xhi,
+                            int64_t strideXb, const void* lb, int64_t strideLb, const void* ub,
+                            int64_t strideUb, void* z, void* y, void* X, int32_t* status,
+                            int max_iter, double tol, void* ws, size_t ws_bytes, void* stream) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64 || dtype == MPCQP_F32, "mpcqp_mpc_qp: bad dtype %d", dtype);
+  MPCQP_CHECK_ARG(batch >= 0, "mpcqp_mpc_qp: batch < 0");
+  MPCQP_CHECK_ARG(nx >= 1 && nx <= 16 && nu >= 1 && nu <= 16 && N >= 1,
+                  "mpcqp_mpc_qp: nx=%d nu=%d N=%d outside nx, nu in [1,16], N >= 1", nx, nu, N);
+  MPCQP_CHECK_ARG(A && Bm && Q && R && Qf && x0 && z && status,
+                  "mpcqp_mpc_qp: A, B, Q, R, Qf, x0, z, status are required");
+  MPCQP_CHECK_ARG(strideA >= 0 && strideB >= 0 && strideQ >= 0 && strideR >= 0 && strideQf >= 0 &&
+                      strideC >= 0 && strideX0 >= 0 && strideXb >= 0 && strideLb >= 0 &&
+                      strideUb >= 0,
+                  "mpcqp_mpc_qp: negative stride");
+  const int sbox = (xlo || xhi) ? 1 : 0;
+  const int n = N * nu, m = sbox ? N * nx : 0;
+  MPCQP_CHECK_ARG(n + m <= max_qp_size_dtype(dtype),
+                  "mpcqp_mpc_qp: N*(nu%s) = %d exceeds the QP size limit %d", sbox ? "+nx" : "",
+                  n + m, max_qp_size_dtype(dtype));
+  if (batch == 0) return MPCQP_OK;
+  const MpcWs L = mpc_ws_layout(dtype, batch, nx, nu, N, sbox);
+  MPCQP_CHECK_ARG(ws && ws_bytes >= L.total, "mpcqp_mpc_qp: workspace %zu bytes < %zu", ws_bytes,
+                  L.total);
+  hipStream_t st = (hipStream_t)stream;
+  char* w = (char*)ws;
+  const int tv = (flags & MPCQP_TV) ? 1 : 0;
+  void* Hw = w + L.H;
+  void* fw = w + L.f;
+  void* Gw = sbox ? w + L.Gam : nullptr;
+  void* xbw = sbox ? w + L.xbar : nullptr;
+  int rc = mpcqp_condense(dtype, batch, nx, nu, N, flags, A, strideA, Bm, strideB, Q, strideQ, R,
+                          strideR, Qf, strideQf, c, strideC, x0, strideX0, Hw, nullptr, fw, Gw,
+                          nullptr, xbw, stream);
+  if (rc != MPCQP_OK) return rc;
+  void* hl = sbox ? w + L.hl : nullptr;
+  void* hu = sbox ? w + L.hu : nullptr;
+  if (sbox) {
+    const int64_t total = (int64_t)batch * m;
+    const dim3 grid((unsigned)((total + 255) / 256)), blk(256);
+    if (dtype == MPCQP_F64)
+      hipLaunchKernelGGL((rows_kernel<double>), grid, blk, 0, st, total, m, (const double*)xlo,
+                         (const double*)xhi, strideXb, (const double*)xbw, (double*)hl,
+                         (double*)hu);
+    else
+      hipLaunchKernelGGL((rows_kernel<float>), grid, blk, 0, st, total, m, (const float*)xlo,
+                         (const float*)xhi, strideXb, (const float*)xbw, (float*)hl, (float*)hu);
+    MPCQP_CHECK_LAUNCH("rows_kernel");
+  }
+  const size_t qpb = qp_ws_bytes(dtype, batch, n, m);
+  const int64_t sH = (int64_t)n * (n + 1) / 2, sG = (int64_t)m * n;
+  if (qpb > 0) {
+    PfDyn d{};
+    const bool dyn_ok = dyn_nxp(nx, nu) > 0 &&
+                        dyn_chunk_stages(nx, nu, N, dyn_nxp(nx, nu) >= 12 ? 8 : 16) >= 1;
+    if (dyn_ok) {
+      d.nx = nx; d.nu = nu; d.N = N; d.tv = tv;
+      d.A = (const float*)A; d.sA = strideA;
+      d.B = (const float*)Bm; d.sB = strideB;
+      d.c = (const float*)c; d.sC = strideC;
+      d.x0 = (const float*)x0; d.sX0 = strideX0;
+      d.Q = (const float*)Q; d.sQ = strideQ;
+      d.R = (const float*)R; d.sR = strideR;
+      d.Qf = (const float*)Qf; d.sQf = strideQf;
+      d.xlo = (const float*)xlo; d.xhi = (const float*)xhi; d.sXb = strideXb;
+    }
+    // a missing side of the state box has no finite bound: no row can be
+    // active on it, so the residual never reads it
+    rc = solve_two_kernel(batch, n, m, Hw, sH, fw, n, Gw, sG, hl, hu, m, lb, strideLb, ub,
+                          strideUb, z, y, status, max_iter, tol, w + L.qp, st,
+                          dyn_ok ? &d : nullptr, dyn_ok ? mpc_refine() : -1);
+  } else {
+    rc = mpcqp_solve_qp(dtype, batch, n, m, Hw, sH, fw, n, Gw, sG, hl, hu, m, lb, strideLb, ub,
+                        strideUb, z, y, status, max_iter, tol, stream);
+  }
+  if (rc != MPCQP_OK) return rc;
+  if (X) {
+    rc = dtype == MPCQP_F64
+             ? launch_states<double>(batch, nx, nu, N, tv, A, strideA, Bm, strideB, c, strideC,
+                                     x0, strideX0, z, X, st)
+             : launch_states<float>(batch, nx, nu, N, tv, A, strideA, Bm, strideB, c, strideC,
+                                    x0, strideX0, z, X, st);
+  }
+  return rc;
+}

@@ -1,0 +1,57 @@
+// pf.hpp -- interface between the product-form active-set kernel
+// (solve_pf.hip) and its callers (solve_qp.hip, mpc_qp.hip).
+#pragma once
+#include "common.hpp"
+
+namespace mpcqp {
+
+constexpr int kSlots = 64;
+constexpr int kKChunk = 1536;  // floats of K rows per refinement chunk (6 KB of LDS)
+constexpr int kStatusRetry = 0x7f;  // internal: hand the instance to qp_wg_kernel
+// refinement scratch (doubles): K-pass = red (8*64) + rsum (3*64) + kbuf
+constexpr int kPool = 8 * kWave + 3 * kWave + kKChunk / 2;
+// DYN layout inside the pool (doubles): xd (3*64: u, then mu of the state
+// rows; g overwrites u) | lam (2 x 16) | X ((N+1) nx) | Q, Qf, R (floats) |
+// stage chunk (floats): [A_s | B_s | c_s] for a run of stages
+constexpr int kDynXd = 0, kDynLam = 3 * kWave, kDynX = kDynLam + 32;
+
+// Dynamics of the condensed QP (mpcqp_mpc_qp): z = [u_0..u_{N-1}], rows (m =
+// N nx, or 0) = the state box on x_1..x_N with the ORIGINAL bounds xlo/xhi.
+struct PfDyn {
+  int nx, nu, N, tv;
+  const float* A; int64_t sA;   // nx*nx (or N*nx*nx with tv) per instance
+  const float* B; int64_t sB;   // nx*nu (or N*nx*nu)
+  const float* c; int64_t sC;   // N*nx, optional
+  const float* x0; int64_t sX0; // nx
+  const float* Q; int64_t sQ;
+  const float* R; int64_t sR;
+  const float* Qf; int64_t sQf;
+  const float* xlo; const float* xhi; int64_t sXb;  // N*nx (m > 0)
+};
+
+// stages per run of the DYN stage stream: what fits both the pool and one
+// prefetch batch of `pre` registers per lane (pre * 64 floats: 16 registers,
+// 8 for the widest kernel); 0 = the DYN path does not apply
+__host__ __device__ inline int dyn_chunk_stages(int nx, int nu, int N, int pre = 16) {
+  const int qr = (2 * nx * nx + nu * nu + 1) / 2;
+  const int free_d = kPool - kDynX - (N + 1) * nx - qr;
+  const int sf = nx * nx + nx * nu + nx;
+  const int cap = free_d <= 0 ? 0 : (2 * free_d) / sf;
+  const int rcap = pre * 64 / sf;
+  return cap < rcap ? cap : rcap;
+}
+
+// compiled DYN widths (padded max(nx, nu)); 0 = none
+__host__ __device__ inline int dyn_nxp(int nx, int nu) {
+  const int w = nx > nu ? nx : nu;
+  return w <= 4 ? 4 : (w <= 8 ? 8 : (w <= 12 ? 12 : (w <= 16 ? 16 : 0)));
+}
+
+int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
+              const float* G, int64_t sG, const float* hl, const float* hu, int64_t sh,
+              const float* lb, int64_t sLb, const float* ub, int64_t sUb, const float* M0,
+              const float* s0, float* z, float* y, int32_t* status, int* retry_count,
+              int* retry_list, int max_iter, int refine, float tol, hipStream_t st,
+              const PfDyn* dyn = nullptr);
+
+}  // namespace mpcqp

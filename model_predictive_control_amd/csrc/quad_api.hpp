@@ -61,10 +61,12 @@ int solve_box_wg(int dtype, int batch, int n, const void* H, int64_t sH, const v
                  const void* Ms = nullptr);
 int max_qp_size_dtype(int dtype);
 size_t qp_ws_bytes(int dtype, int batch, int n, int m);
+struct PfDyn;
+// dyn != NULL: refine from the dynamics (pf.hpp); refine < 0: default steps
 int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const void* f,
                      int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
                      int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
                      void* z, void* y, int32_t* status, int max_iter, double tol, void* ws,
-                     hipStream_t st);
+                     hipStream_t st, const PfDyn* dyn = nullptr, int refine = -1);
 
 }  // namespace mpcqp

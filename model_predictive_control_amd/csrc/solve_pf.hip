@@ -24,15 +24,20 @@
 // which holds row j of S^-1 in 64 registers (unused slots are zero rows and
 // columns), the index a_j and its bound.  More than 64 active constraints
 // (n > 64 only) hands the instance to the workgroup kernel (kStatusRetry).
-// The refinement (iterative refinement of the final active set against the
-// ORIGINAL H, G with fp64 accumulation) follows gi_mixed.
-#include "common.hpp"
+// The refinement (iterative refinement of the final active set with an fp64
+// KKT residual) follows gi_mixed.  The residual comes from one of:
+//   * the ORIGINAL H, G (fp32 data, fp64 accumulation): K x streamed through
+//     LDS -- the generic QP of mpcqp_solve_qp_ws;
+//   * the DYNAMICS (DYN = true, mpcqp_mpc_qp): H z + f + G'lam and G z - h
+//     from an fp64 forward rollout x_{k+1} = A_k x_k + B_k u_k + c_k and the
+//     adjoint lam_k = Qhat x_k + mu_k + A_k' lam_{k+1}, g_k = R u_k +
+//     B_k' lam_{k+1}.  This is the residual of the QP the fp32 inputs define
+//     exactly (no fp32 rounding of the condensed H, Gam, xbar), so refinement
+//     converges past the fp32 condensing floor, and it costs O(N nx (nx+nu))
+//     instead of O((n+m)^2) reads.
+#include "pf.hpp"
 
 namespace mpcqp {
-
-constexpr int kSlots = 64;
-constexpr int kKChunk = 1536;  // floats of K rows per refinement chunk (6 KB of LDS)
-constexpr int kStatusRetry = 0x7f;  // internal: hand the instance to qp_wg_kernel
 
 struct PfArgs {
   int batch, n, m;
@@ -48,7 +53,29 @@ struct PfArgs {
   int* retry_count; int* retry_list;
   int max_iter, refine;
   float tol;
+  PfDyn d;                     // DYN kernels only
 };
+
+// cnt floats from up to three contiguous global segments into LDS, every
+// load of a 1024-float group issued before its first LDS store
+__device__ __forceinline__ void lds_copy3(float* dst, const float* s1, int n1, const float* s2,
+                                          int n2, const float* s3, int n3, int l) {
+  const int cnt = n1 + n2 + n3;
+  for (int e0 = 0; e0 < cnt; e0 += 16 * kWave) {
+    float t[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = e0 + l + kWave * k;
+      const float* p = e < n1 ? s1 + e : (e < n1 + n2 ? s2 + (e - n1) : s3 + (e - n1 - n2));
+      t[k] = e < cnt ? *p : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = e0 + l + kWave * k;
+      if (e < cnt) dst[e] = t[k];
+    }
+  }
+}
 
 __device__ __forceinline__ float bperm(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(lane << 2, __float_as_int(v)));
@@ -76,17 +103,245 @@ __device__ __forceinline__ V pick(const V (&x)[NR], int i) {
   return v;
 }
 
-template <int NR>
-__global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffffll), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Sum over groups of P lanes (P = 2 or 4, wave-uniform), result in every lane.
+__device__ __forceinline__ double group_sum(double v, int P) {
+  v += dppd<0xB1>(v);             // quad_perm [1,0,3,2]
+  if (P == 4) v += dppd<0x4E>(v);  // quad_perm [2,3,0,1]
+  return v;
+}
+
+// KKT residual of the condensed QP from the dynamics, in fp64 (DYN pf
+// kernels).  x: z (i < n) and the signed row multipliers (rows i >= n, the
+// state box on x_1..x_N in stage-major order).  Out: w_i = (H z + f + G'mu)_i
+// on free z, (G z - h)_i = x_k(z)_c - xlo/xhi on active rows, 0 elsewhere.
+//   forward   x_{s+1} = A_s x_s + B_s u_s + c_s
+//   backward  lam_N = Qf x_N + mu_N,  g_s = R u_s + B_s' lam_{s+1},
+//             lam_s = Q x_s + mu_s + A_s' lam_{s+1}
+// Every matrix-vector row is a dot product over 4 lanes (row r = lane / 4)
+// whose NXP/2 terms per lane are unrolled at compile time (NXP >= nx, nu,
+// the padded terms are masked), so a stage costs one LDS round trip.
+// Stage data (A_s, B_s, c_s) streams through the pool in runs of `cap`
+// stages (<= 1024 floats, one 16-register batch), visited forward 0..K-1
+// then backward K-1..0; the next run's loads are issued before the current
+// run is computed and land in LDS after it (`loaded` = resident run).
+template <int NR, int NXP>
+__device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m, int l,
+                                             const float (&x)[NR], const int (&st)[NR],
+                                             double* pool, int& loaded, float (&w)[NR]) {
+  static_assert(NXP % 4 == 0 && NXP <= 16, "4 lanes per row, at most 16 rows");
+  constexpr int TT = NXP / 2;  // terms per lane: 2*NXP padded terms over 4 lanes
+  constexpr int PRE = NXP >= 12 ? 8 : 16;  // prefetch registers (register budget)
+  const int nx = d.nx, nu = d.nu, N = d.N, tv = d.tv;
+  double* xd = pool + kDynXd;
+  double* lam = pool + kDynLam;
+  double* X = pool + kDynX;
+  float* Qs = reinterpret_cast<float*>(X + (N + 1) * nx);
+  float* Qfs = Qs + nx * nx;
+  float* Rs = Qfs + nx * nx;
+  float* ch = reinterpret_cast<float*>(X + (N + 1) * nx + (2 * nx * nx + nu * nu + 1) / 2);
+  const int cap = dyn_chunk_stages(nx, nu, N, PRE);
+  const int K = (N + cap - 1) / cap;
+  const int sfA = nx * nx, sfB = nx * nu;
+  const float* Ab = d.A + (int64_t)b * d.sA;
+  const float* Bb = d.B + (int64_t)b * d.sB;
+  const float* cb = d.c ? d.c + (int64_t)b * d.sC : nullptr;
+  const int i4 = l >> 2, q = l & 3;
+
+  // run r: stages [r cap, r cap + S); LDS image A_c (S or 1) | B_c | c_c (S)
+  auto run_len = [&](int r) { return N - r * cap < cap ? N - r * cap : cap; };
+  auto chA = [&](int S, int t) { return ch + (tv ? t * sfA : 0); };
+  auto chB = [&](int S, int t) { return ch + (tv ? S * sfA : sfA) + (tv ? t * sfB : 0); };
+  auto chC = [&](int S, int t) { return ch + (tv ? S * (sfA + sfB) : sfA + sfB) + t * nx; };
+  float pre[PRE];
+  int pre_cnt = 0, pre_run = -1;
+  auto issue = [&](int r) __attribute__((always_inline)) {
+    const int s0 = r * cap, S = run_len(r);
+    const int nA = tv ? S * sfA : sfA, nB = tv ? S * sfB : sfB, nC = cb ? S * nx : 0;
+    const float* pA = Ab + (tv ? (int64_t)s0 * sfA : 0);
+    const float* pB = Bb + (tv ? (int64_t)s0 * sfB : 0);
+    const float* pC = cb ? cb + (int64_t)s0 * nx : nullptr;
+    pre_cnt = nA + nB + nC;
+#pragma unroll
+    for (int k = 0; k < PRE; ++k) {
+      const int e = l + kWave * k;
+      const float* p = e < nA ? pA + e : (e < nA + nB ? pB + (e - nA) : pC + (e - nA - nB));
+      pre[k] = e < pre_cnt ? *p : 0.f;
+    }
+    pre_run = r;
+  };
+  auto commit = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < PRE; ++k) {
+      const int e = l + kWave * k;
+      if (e < pre_cnt) ch[e] = pre[k];
+    }
+    loaded = pre_run;
+  };
+  if (loaded < 0)
+    lds_copy3(Qs, d.Q + (int64_t)b * d.sQ, sfA, d.Qf + (int64_t)b * d.sQf, sfA,
+              d.R + (int64_t)b * d.sR, nu * nu, l);
+
+  // x0, u and the row multipliers into LDS
+  if (l < nx) X[l] = (double)d.x0[(int64_t)b * d.sX0 + l];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) xd[l + kWave * r] = (double)x[r];
+
+  auto fwd_run = [&](int r) __attribute__((always_inline)) {
+    const int s0 = r * cap, S = run_len(r);
+    const bool row = i4 < nx;
+    for (int t = 0; t < S; ++t) {
+      const int s = s0 + t;
+      const float* As = chA(S, t);
+      const float* Bs = chB(S, t);
+      const float cs = (cb && row) ? chC(S, t)[i4] : 0.f;
+      double acc = 0.0;
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt) {
+        const int k = q + 4 * tt;
+        bool ok;
+        float cf;
+        double v;
+        if (4 * tt < NXP) {  // A_s row i4 . x_s
+          ok = row && k < nx;
+          cf = As[ok ? i4 * nx + k : 0];
+          v = X[s * nx + (ok ? k : 0)];
+        } else {             // B_s row i4 . u_s
+          const int k2 = k - NXP;
+          ok = row && k2 < nu;
+          cf = Bs[ok ? i4 * nu + k2 : 0];
+          v = xd[s * nu + (ok ? k2 : 0)];
+        }
+        acc = fma(ok ? (double)cf : 0.0, v, acc);
+      }
+      acc = group_sum(acc, 4);
+      if (row && q == 0) X[(s + 1) * nx + i4] = acc + (double)cs;
+      wave_lds_sync();
+    }
+  };
+  // one backward sub-step for rows of one kind: g rows (a = row) or lam rows
+  auto bwd_rows = [&](int s, int S, int t, const double* ln, bool isg, bool isl, int rr)
+      __attribute__((always_inline)) {
+    const float* As = chA(S, t);
+    const float* Bs = chB(S, t);
+    double acc = 0.0;
+#pragma unroll
+    for (int tt = 0; tt < TT; ++tt) {
+      const int k = q + 4 * tt;
+      bool ok;
+      float cf;
+      double v;
+      if (4 * tt < NXP) {  // A_s col / B_s col . lam_{s+1}
+        ok = (isl || isg) && k < nx;
+        cf = isl ? As[ok ? k * nx + rr : 0] : Bs[ok ? k * nu + rr : 0];
+        v = ln[ok ? k : 0];
+      } else {             // Q x_s / R u_s
+        const int k2 = k - NXP;
+        ok = isl ? k2 < nx : (isg && k2 < nu);
+        cf = isl ? Qs[ok ? rr * nx + k2 : 0] : Rs[ok ? rr * nu + k2 : 0];
+        v = isl ? X[s * nx + (ok ? k2 : 0)] : xd[s * nu + (ok ? k2 : 0)];
+      }
+      acc = fma(ok ? (double)cf : 0.0, v, acc);
+    }
+    return group_sum(acc, 4);
+  };
+  auto bwd_run = [&](int r) __attribute__((always_inline)) {
+    const int s0 = r * cap, S = run_len(r);
+    const bool one = nx + nu <= 16;  // lam and g rows side by side
+    for (int t = S - 1; t >= 0; --t) {
+      const int s = s0 + t;
+      const double* ln = lam + ((s + 1) & 1) * 16;  // lam_{s+1}
+      if (one) {
+        const bool isl = i4 < nx && s >= 1, isg = i4 >= nx && i4 < nx + nu;
+        const int rr = isl || i4 < nx ? i4 : i4 - nx;
+        const double acc = bwd_rows(s, S, t, ln, isg, isl, rr);
+        if (q == 0) {
+          if (isl) lam[(s & 1) * 16 + rr] = acc + (m ? xd[n + (s - 1) * nx + rr] : 0.0);
+          if (isg) xd[s * nu + rr] = acc;
+        }
+      } else {
+        const bool isg = i4 < nu, isl = i4 < nx && s >= 1;
+        const double ag = bwd_rows(s, S, t, ln, isg, false, i4);
+        const double al = bwd_rows(s, S, t, ln, false, isl, i4);
+        if (q == 0) {
+          if (isl) lam[(s & 1) * 16 + i4] = al + (m ? xd[n + (s - 1) * nx + i4] : 0.0);
+          if (isg) xd[s * nu + i4] = ag;
+        }
+      }
+      wave_lds_sync();
+    }
+  };
+
+  for (int p = 0; p < 2 * K; ++p) {
+    const bool fw = p < K;
+    const int r = fw ? p : 2 * K - 1 - p;
+    const int rn = p + 1 < 2 * K ? (p + 1 < K ? p + 1 : 2 * K - 2 - p) : -1;
+    if (loaded != r) {  // first use only: blocking load
+      issue(r);
+      commit();
+    }
+    const bool pf = rn >= 0 && rn != r;
+    if (pf) issue(rn);
+    wave_lds_sync();
+    if (p == K) {  // lam_N = Qf x_N + mu_N
+      double acc = 0.0;
+#pragma unroll
+      for (int tt = 0; tt < NXP / 4; ++tt) {
+        const int k = q + 4 * tt;
+        const bool ok = i4 < nx && k < nx;
+        acc = fma(ok ? (double)Qfs[ok ? i4 * nx + k : 0] : 0.0, X[N * nx + (ok ? k : 0)], acc);
+      }
+      acc = group_sum(acc, 4);
+      if (i4 < nx && q == 0) lam[(N & 1) * 16 + i4] = acc + (m ? xd[n + (N - 1) * nx + i4] : 0.0);
+      wave_lds_sync();
+    }
+    if (fw) fwd_run(r);
+    else bwd_run(r);
+    if (pf) {
+      wave_lds_sync();
+      commit();
+    }
+  }
+  // ---- residual on the working set
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int i = l + kWave * r;
+    const bool isz = i < n;
+    const bool act = st[r] == 1 || st[r] == 2;
+    double e = 0.0;
+    if (isz) {
+      e = xd[i];
+    } else if (act && i < n + m) {
+      const int j = i - n;
+      const float* bp = (st[r] == 1) ? d.xlo : d.xhi;
+      e = X[nx + j] - (double)bp[(int64_t)b * d.sXb + j];
+    }
+    const bool inS = isz ? (st[r] == 0) : act;
+    w[r] = (inS && i < n + m) ? (float)e : 0.f;
+  }
+  wave_lds_sync();
+}
+
+template <int NR, int NXP>
+__global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
   __shared__ float xb[NR * kWave];
   // per-index bounds and scales live in LDS (read by the scan and the
   // output only): keeps them out of the register budget
   __shared__ float s_lo[NR * kWave], s_hi[NR * kWave], s_sl[NR * kWave], s_su[NR * kWave],
       s_scl[NR * kWave];
   __shared__ __attribute__((aligned(16))) float sx[kSlots];  // slot-vector broadcast
-  __shared__ double red[8 * kWave];
-  __shared__ double rsum[NR * kWave];
-  __shared__ float kbuf[kKChunk];  // refinement: rows of K staged per chunk
+  __shared__ double pool[kPool];   // refinement scratch (K-pass or DYN layout)
+  double* red = pool;
+  double* rsum = pool + 8 * kWave;
+  float* kbuf = reinterpret_cast<float*>(pool + 11 * kWave);  // rows of K staged per chunk
+  static_assert(NR <= 3, "rsum holds 3 * 64 doubles");
   static_assert(kKChunk >= 8 * NR * kWave, "8 rows of K (<= NR*64 floats each) must fit one chunk");
   static_assert(kKChunk % kWave == 0, "chunk is whole wave loads");
   const int b = blockIdx.x, l = threadIdx.x;
@@ -526,6 +781,9 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
     // ------------------------------------------- iterative refinement
     const float* Hb = a.H + (int64_t)b * a.sH;
     const float* Gb = m ? a.G + (int64_t)b * a.sG : nullptr;
+    // DYN: the horizon's stage data stays in LDS across refinement steps
+    // when it fits one chunk
+    int dyn_loaded = -1;
     for (int it = 0; it < a.refine; ++it) {
       float x[NR];
 #pragma unroll
@@ -536,6 +794,11 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
         const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
         x[r] = (st[r] == 3) ? 0.f : (isz ? val[r] : (act ? sside * mu[r] : 0.f));
       }
+      float w[NR];
+      if constexpr (NXP > 0) {
+        dyn_residual<NR, NXP>(a.d, b, n, m, l, x, st, pool, dyn_loaded, w);
+        MPCQP_PHASE(0);  // phase timing: the residual is charged with the setup
+      } else {
       // yk = K x in fp64, K = [[H, G'], [G, 0]]: row sweeps over packed H
       // and over G; the row-direction sums reduce 8 rows at a time in LDS
       double yk[NR];
@@ -614,7 +877,6 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
       wave_lds_sync();
       kpass(Hb, 0, n, true);
       if (m) kpass(Gb, n, nt, false);
-      float w[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         const int i = l + kWave * r;
@@ -625,6 +887,7 @@ __global__ __launch_bounds__(64) void qp_pf_kernel(PfArgs a) {
         const bool inS = isz ? (st[r] == 0) : act;
         const double e = isz ? yi + (double)fz[r] : yi - bnd;
         w[r] = (inS && i < nt) ? (float)e : 0.f;
+      }
       }
       wave_lds_sync();
       // sv = M w (w on free z and active rows): y2 = M0[:, free z] w
@@ -677,13 +940,23 @@ int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* 
               const float* G, int64_t sG, const float* hl, const float* hu, int64_t sh,
               const float* lb, int64_t sLb, const float* ub, int64_t sUb, const float* M0,
               const float* s0, float* z, float* y, int32_t* status, int* retry_count,
-              int* retry_list, int max_iter, int refine, float tol, hipStream_t st) {
+              int* retry_list, int max_iter, int refine, float tol, hipStream_t st,
+              const PfDyn* dyn) {
   PfArgs a{batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, M0, s0, z, y, status,
-           retry_count, retry_list, max_iter, refine, tol};
-  if (n + m <= 2 * kWave)
-    hipLaunchKernelGGL((qp_pf_kernel<2>), dim3(batch), dim3(kWave), 0, st, a);
-  else
-    hipLaunchKernelGGL((qp_pf_kernel<3>), dim3(batch), dim3(kWave), 0, st, a);
+           retry_count, retry_list, max_iter, refine, tol, PfDyn{}};
+  if (dyn) a.d = *dyn;
+  const bool two = n + m <= 2 * kWave;
+  const int nxp = dyn ? dyn_nxp(dyn->nx, dyn->nu) : 0;
+#define MPCQP_PF(NRV, NXPV) \
+  hipLaunchKernelGGL((qp_pf_kernel<NRV, NXPV>), dim3(batch), dim3(kWave), 0, st, a)
+  switch (nxp) {
+    case 4: if (two) MPCQP_PF(2, 4); else MPCQP_PF(3, 4); break;
+    case 8: if (two) MPCQP_PF(2, 8); else MPCQP_PF(3, 8); break;
+    case 12: if (two) MPCQP_PF(2, 12); else MPCQP_PF(3, 12); break;
+    case 16: if (two) MPCQP_PF(2, 16); else MPCQP_PF(3, 16); break;
+    default: if (two) MPCQP_PF(2, 0); else MPCQP_PF(3, 0); break;
+  }
+#undef MPCQP_PF
   MPCQP_CHECK_LAUNCH("qp_pf_kernel");
   return MPCQP_OK;
 }

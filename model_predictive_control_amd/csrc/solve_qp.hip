@@ -15,6 +15,8 @@
 #include <cstdlib>
 
 #include "wg.hpp"
+#include "pf.hpp"
+#include "quad_api.hpp"
 
 namespace mpcqp {
 
@@ -304,11 +306,6 @@ size_t qp_ws_bytes(int dtype, int batch, int n, int m) {
   return ws_m0_bytes(batch, n, m) + ws_s0_bytes(batch, n, m) + 256 + (size_t)batch * sizeof(int);
 }
 
-int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
-              const float* G, int64_t sG, const float* hl, const float* hu, int64_t sh,
-              const float* lb, int64_t sLb, const float* ub, int64_t sUb, const float* M0,
-              const float* s0, float* z, float* y, int32_t* status, int* retry_count,
-              int* retry_list, int max_iter, int refine, float tol, hipStream_t st);
 
 // refinement steps of the product-form kernel (MPCQP_PF_REFINE overrides;
 // a tuning knob, default 1: the fp64 residual against the original data
@@ -325,7 +322,7 @@ int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const v
                      int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
                      int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
                      void* z, void* y, int32_t* status, int max_iter, double tol, void* ws,
-                     hipStream_t st) {
+                     hipStream_t st, const PfDyn* dyn, int refine) {
   char* w = (char*)ws;
   float* M0 = (float*)w;
   float* s0 = (float*)(w + ws_m0_bytes(batch, n, m));
@@ -339,7 +336,8 @@ int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const v
   const float tl = tol > 0 ? (float)tol : 1e-6f;
   rc = launch_pf(batch, n, m, (const float*)H, sH, (const float*)f, sf, (const float*)G, sG,
                  (const float*)hl, (const float*)hu, sh, (const float*)lb, sLb, (const float*)ub,
-                 sUb, M0, s0, (float*)z, (float*)y, status, cnt, list, mi, pf_refine(), tl, st);
+                 sUb, M0, s0, (float*)z, (float*)y, status, cnt, list, mi,
+                 refine >= 0 ? refine : pf_refine(), tl, st, dyn);
   if (rc != MPCQP_OK) return rc;
   return solve_qp_t<float>(batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, z, y,
                            status, max_iter, tol, st, M0, cnt, list);

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CS = os.path.join(ROOT, "model_predictive_control_amd", "csrc")
 LIB = os.path.join(ROOT, "model_predictive_control_amd", "lib", "libmpcqp_timing.so")
 SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.hip", "quad_box.hip",
-        "solve_qp.hip", "sweep.hip", "solve_pf.hip", "bicycle.hip", "misc.hip"]
+        "solve_qp.hip", "sweep.hip", "solve_pf.hip", "mpc_qp.hip", "bicycle.hip", "misc.hip"]
 PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/recheck", "GI: scan+argmax", "GI: pivot col+ratio", "GI: sweep"]
 
 if "--build" in sys.argv:
@@ -58,26 +58,35 @@ elif cfg == 55:
     PHASES = ["backward W/What", "fw: loads+What", "fw: MFMA tiles", "fw: Gam/H epilogue", "fw: E tile", "", "", ""]
     a = A(); a.batch = 32768; a.slots = 1; a.horizon = 0; a.reps = 1
     w = bench.CONFIGS[5](a, torch.device("cuda"), 0)
-    run = lambda: w._condense(0)  # noqa: E731
+    run = lambda: batched.condense(w.A[0], w.B[0], w.Q_t, w.R_t, w.Q_t, w.N, x0=w.X0_t[0],  # noqa: E731
+                                   tv=True, outputs=("H", "f"))
     waves = a.batch * R
 elif pf:
     # qp_pf_kernel of config 3 / 5 (one wave per instance)
     reader = lib.mpcqp_debug_phase_cycles_pf
     reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    PHASES = ["setup + s0", "refresh", "scan + col load", "gather + S^-1 u", "M0[:,P] v",
-              "ratio + update", "S^-1 update", "refinement"]
-    a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1
+    # (mpcqp_mpc_qp: the DYN kernel; its refinement residual is charged to
+    # phase 0 and the M0 correction to phase 7)
+    PHASES = ["setup + s0 (+DYN residual)", "refresh", "scan + col load", "gather + S^-1 u",
+              "M0[:,P] v", "ratio + update", "S^-1 update", "refinement (correction)"]
+    a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1; a.check = 0
     w = bench.CONFIGS[cfg](a, torch.device("cuda"), 0)
-    w._condense(0)
-    run = lambda: w._solve(0)  # noqa: E731
+    run = lambda: w.step(0)  # noqa: E731
     waves = a.batch * R
 else:
     # qp_wg_kernel of config 3 / 5 (phases 0..3: K load, z sweep-in, GI, refinement)
     PHASES = ["load K", "sweep-in z", "active set", "refinement", "", "", "", ""]
     a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1
+    a.check = 0
     w = bench.CONFIGS[cfg](a, torch.device("cuda"), 0)
-    w._condense(0)
-    run = lambda: w._solve(0)  # noqa: E731
+    if cfg == 3:
+        d = batched.condense(w.A[0], w.B[0], w.Q_t, w.R_t, w.QN_t, w.N, x0=w.X0_t[0], c=w.c[0],
+                             tv=True, outputs=("H", "f", "Gam", "xbar"))
+        run = lambda: batched.solve_qp(d["H"], d["f"], d["Gam"], w.xmin_t - d["xbar"],  # noqa: E731
+                                       w.xmax_t - d["xbar"], w.lbz, w.ubz, presweep=False)
+    else:
+        d = batched.condense(w.A[0], w.B[0], w.Q_t, w.R_t, w.Q_t, w.N, x0=w.X0_t[0], tv=True)
+        run = lambda: batched.solve_box(d["H"], d["f"], w.lb_t, w.ub_t, presweep=False)  # noqa: E731
     waves = a.batch * 8 * R  # 512-thread workgroups
 run()
 torch.cuda.synchronize()
