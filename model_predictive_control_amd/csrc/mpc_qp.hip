@@ -10,7 +10,8 @@
 //   3. fp32 with n + m > 64: sweep (MFMA) -> product-form active set whose
 //      iterative refinement takes its KKT residual from the DYNAMICS in fp64
 //      (solve_pf.hip, PfDyn) -> workgroup kernel for hand-offs;
-//      otherwise (fp64, small QPs): the workgroup kernel (mpcqp_solve_qp).
+//      otherwise (fp64, small QPs): mpcqp_solve_box (input box only) or the
+//      workgroup kernel (mpcqp_solve_qp).
 //   4. optional: states_kernel -> X = x_1..x_N of the solution (fp64 rollout),
 //      the "g" rows IPOPT reports and the state_prediction of the
 //      ControllerLog (session_2/log.py:12).
@@ -98,10 +99,17 @@ static MpcWs mpc_ws_layout(int dtype, int batch, int nx, int nu, int N, int sbox
   return w;
 }
 
-// refinement steps with the dynamics residual (MPCQP_MPC_REFINE overrides)
+// most refinement steps with the dynamics residual (MPCQP_MPC_REFINE
+// overrides); each instance stops once its correction is below kDynStop
 static int mpc_refine() {
   const char* v = getenv("MPCQP_MPC_REFINE");
-  return v ? atoi(v) : 2;
+  return v ? atoi(v) : 4;
+}
+
+// MPCQP_MPC_DYN=0 refines against the condensed matrices instead (A/B checks)
+static bool mpc_dyn() {
+  const char* v = getenv("MPCQP_MPC_DYN");
+  return v ? atoi(v) != 0 : true;
 }
 
 template <typename T>
@@ -188,8 +196,7 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
   const int64_t sH = (int64_t)n * (n + 1) / 2, sG = (int64_t)m * n;
   if (qpb > 0) {
     PfDyn d{};
-    const bool dyn_ok = dyn_nxp(nx, nu) > 0 &&
-                        dyn_chunk_stages(nx, nu, N, dyn_nxp(nx, nu) >= 12 ? 8 : 16) >= 1;
+    const bool dyn_ok = mpc_dyn() && dyn_nxp(nx, nu) > 0 && dyn_chunk_stages(nx, nu, N) >= 1;
     if (dyn_ok) {
       d.nx = nx; d.nu = nu; d.N = N; d.tv = tv;
       d.A = (const float*)A; d.sA = strideA;
@@ -206,6 +213,9 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
     rc = solve_two_kernel(batch, n, m, Hw, sH, fw, n, Gw, sG, hl, hu, m, lb, strideLb, ub,
                           strideUb, z, y, status, max_iter, tol, w + L.qp, st,
                           dyn_ok ? &d : nullptr, dyn_ok ? mpc_refine() : -1);
+  } else if (m == 0) {  // input box only: the wavefront box kernels
+    rc = mpcqp_solve_box(dtype, batch, n, Hw, sH, fw, n, lb, strideLb, ub, strideUb, z, status,
+                         max_iter, tol, stream);
   } else {
     rc = mpcqp_solve_qp(dtype, batch, n, m, Hw, sH, fw, n, Gw, sG, hl, hu, m, lb, strideLb, ub,
                         strideUb, z, y, status, max_iter, tol, stream);

@@ -14,6 +14,10 @@ constexpr int kPool = 8 * kWave + 3 * kWave + kKChunk / 2;
 // rows; g overwrites u) | lam (2 x 16) | X ((N+1) nx) | Q, Qf, R (floats) |
 // stage chunk (floats): [A_s | B_s | c_s] for a run of stages
 constexpr int kDynXd = 0, kDynLam = 3 * kWave, kDynX = kDynLam + 32;
+// DYN refinement stops once a correction is below this (relative to 1+|z|)
+constexpr float kDynStop = 1e-4f;
+// ... and re-scans the refined point with this relative feasibility tolerance
+constexpr float kDynTol = 1e-7f;
 
 // Dynamics of the condensed QP (mpcqp_mpc_qp): z = [u_0..u_{N-1}], rows (m =
 // N nx, or 0) = the state box on x_1..x_N with the ORIGINAL bounds xlo/xhi.
@@ -29,16 +33,13 @@ struct PfDyn {
   const float* xlo; const float* xhi; int64_t sXb;  // N*nx (m > 0)
 };
 
-// stages per run of the DYN stage stream: what fits both the pool and one
-// prefetch batch of `pre` registers per lane (pre * 64 floats: 16 registers,
-// 8 for the widest kernel); 0 = the DYN path does not apply
-__host__ __device__ inline int dyn_chunk_stages(int nx, int nu, int N, int pre = 16) {
+// stages per run of the DYN stage stream (what fits the pool); 0 = the DYN
+// path does not apply
+__host__ __device__ inline int dyn_chunk_stages(int nx, int nu, int N) {
   const int qr = (2 * nx * nx + nu * nu + 1) / 2;
   const int free_d = kPool - kDynX - (N + 1) * nx - qr;
   const int sf = nx * nx + nx * nu + nx;
-  const int cap = free_d <= 0 ? 0 : (2 * free_d) / sf;
-  const int rcap = pre * 64 / sf;
-  return cap < rcap ? cap : rcap;
+  return free_d <= 0 ? 0 : (2 * free_d) / sf;
 }
 
 // compiled DYN widths (padded max(nx, nu)); 0 = none

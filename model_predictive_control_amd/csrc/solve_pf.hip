@@ -37,6 +37,20 @@
 //     instead of O((n+m)^2) reads.
 #include "pf.hpp"
 
+// tools/phase_timing.py dyn3|dyn5 builds with MPCQP_PHASE_DYN: the phase
+// clock then times the DYN refinement (PHASE_D) instead of the active set
+#ifdef MPCQP_PHASE_DYN
+#define MPCQP_PHASE_K(i) \
+  do {               \
+  } while (0)
+#define MPCQP_PHASE_D(i) MPCQP_PHASE(i)
+#else
+#define MPCQP_PHASE_K(i) MPCQP_PHASE(i)
+#define MPCQP_PHASE_D(i) \
+  do {               \
+  } while (0)
+#endif
+
 namespace mpcqp {
 
 struct PfArgs {
@@ -58,19 +72,20 @@ struct PfArgs {
 
 // cnt floats from up to three contiguous global segments into LDS, every
 // load of a 1024-float group issued before its first LDS store
+template <int BATCH = 16>
 __device__ __forceinline__ void lds_copy3(float* dst, const float* s1, int n1, const float* s2,
                                           int n2, const float* s3, int n3, int l) {
   const int cnt = n1 + n2 + n3;
-  for (int e0 = 0; e0 < cnt; e0 += 16 * kWave) {
-    float t[16];
+  for (int e0 = 0; e0 < cnt; e0 += BATCH * kWave) {
+    float t[BATCH];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < BATCH; ++k) {
       const int e = e0 + l + kWave * k;
       const float* p = e < n1 ? s1 + e : (e < n1 + n2 ? s2 + (e - n1) : s3 + (e - n1 - n2));
       t[k] = e < cnt ? *p : 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < BATCH; ++k) {
       const int e = e0 + l + kWave * k;
       if (e < cnt) dst[e] = t[k];
     }
@@ -129,16 +144,17 @@ __device__ __forceinline__ double group_sum(double v, int P) {
 // whose NXP/2 terms per lane are unrolled at compile time (NXP >= nx, nu,
 // the padded terms are masked), so a stage costs one LDS round trip.
 // Stage data (A_s, B_s, c_s) streams through the pool in runs of `cap`
-// stages (<= 1024 floats, one 16-register batch), visited forward 0..K-1
-// then backward K-1..0; the next run's loads are issued before the current
-// run is computed and land in LDS after it (`loaded` = resident run).
+// stages, visited forward 0..K-1 then backward K-1..0 (`loaded` = the
+// resident run; a horizon that fits one run is loaded once per kernel).
+// Measured: register prefetching of the next run (8-16 VGPRs) cost more in
+// spills and short runs than the round trips it hid.
 template <int NR, int NXP>
 __device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m, int l,
                                              const float (&x)[NR], const int (&st)[NR],
-                                             double* pool, int& loaded, float (&w)[NR]) {
+                                             double* pool, int& loaded,
+                                             float (&w)[NR] MPCQP_CLK_PARAM) {
   static_assert(NXP % 4 == 0 && NXP <= 16, "4 lanes per row, at most 16 rows");
   constexpr int TT = NXP / 2;  // terms per lane: 2*NXP padded terms over 4 lanes
-  constexpr int PRE = NXP >= 12 ? 8 : 16;  // prefetch registers (register budget)
   const int nx = d.nx, nu = d.nu, N = d.N, tv = d.tv;
   double* xd = pool + kDynXd;
   double* lam = pool + kDynLam;
@@ -147,7 +163,7 @@ __device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m
   float* Qfs = Qs + nx * nx;
   float* Rs = Qfs + nx * nx;
   float* ch = reinterpret_cast<float*>(X + (N + 1) * nx + (2 * nx * nx + nu * nu + 1) / 2);
-  const int cap = dyn_chunk_stages(nx, nu, N, PRE);
+  const int cap = dyn_chunk_stages(nx, nu, N);
   const int K = (N + cap - 1) / cap;
   const int sfA = nx * nx, sfB = nx * nu;
   const float* Ab = d.A + (int64_t)b * d.sA;
@@ -160,30 +176,14 @@ __device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m
   auto chA = [&](int S, int t) { return ch + (tv ? t * sfA : 0); };
   auto chB = [&](int S, int t) { return ch + (tv ? S * sfA : sfA) + (tv ? t * sfB : 0); };
   auto chC = [&](int S, int t) { return ch + (tv ? S * (sfA + sfB) : sfA + sfB) + t * nx; };
-  float pre[PRE];
-  int pre_cnt = 0, pre_run = -1;
-  auto issue = [&](int r) __attribute__((always_inline)) {
+  // run r into LDS: every load of a 16-register batch issued before its
+  // first LDS store
+  auto load_run = [&](int r) __attribute__((always_inline)) {
     const int s0 = r * cap, S = run_len(r);
-    const int nA = tv ? S * sfA : sfA, nB = tv ? S * sfB : sfB, nC = cb ? S * nx : 0;
-    const float* pA = Ab + (tv ? (int64_t)s0 * sfA : 0);
-    const float* pB = Bb + (tv ? (int64_t)s0 * sfB : 0);
-    const float* pC = cb ? cb + (int64_t)s0 * nx : nullptr;
-    pre_cnt = nA + nB + nC;
-#pragma unroll
-    for (int k = 0; k < PRE; ++k) {
-      const int e = l + kWave * k;
-      const float* p = e < nA ? pA + e : (e < nA + nB ? pB + (e - nA) : pC + (e - nA - nB));
-      pre[k] = e < pre_cnt ? *p : 0.f;
-    }
-    pre_run = r;
-  };
-  auto commit = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < PRE; ++k) {
-      const int e = l + kWave * k;
-      if (e < pre_cnt) ch[e] = pre[k];
-    }
-    loaded = pre_run;
+    lds_copy3<NXP >= 8 ? 8 : 16>(ch, Ab + (tv ? (int64_t)s0 * sfA : 0), tv ? S * sfA : sfA,
+              Bb + (tv ? (int64_t)s0 * sfB : 0), tv ? S * sfB : sfB,
+              cb ? cb + (int64_t)s0 * nx : nullptr, cb ? S * nx : 0, l);
+    loaded = r;
   };
   if (loaded < 0)
     lds_copy3(Qs, d.Q + (int64_t)b * d.sQ, sfA, d.Qf + (int64_t)b * d.sQf, sfA,
@@ -282,14 +282,12 @@ __device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m
   for (int p = 0; p < 2 * K; ++p) {
     const bool fw = p < K;
     const int r = fw ? p : 2 * K - 1 - p;
-    const int rn = p + 1 < 2 * K ? (p + 1 < K ? p + 1 : 2 * K - 2 - p) : -1;
-    if (loaded != r) {  // first use only: blocking load
-      issue(r);
-      commit();
+    if (loaded != r) {
+      wave_lds_sync();  // the previous run's readers are done
+      load_run(r);
     }
-    const bool pf = rn >= 0 && rn != r;
-    if (pf) issue(rn);
     wave_lds_sync();
+    MPCQP_PHASE_D(1);
     if (p == K) {  // lam_N = Qf x_N + mu_N
       double acc = 0.0;
 #pragma unroll
@@ -302,11 +300,12 @@ __device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m
       if (i4 < nx && q == 0) lam[(N & 1) * 16 + i4] = acc + (m ? xd[n + (N - 1) * nx + i4] : 0.0);
       wave_lds_sync();
     }
-    if (fw) fwd_run(r);
-    else bwd_run(r);
-    if (pf) {
-      wave_lds_sync();
-      commit();
+    if (fw) {
+      fwd_run(r);
+      MPCQP_PHASE_D(2);
+    } else {
+      bwd_run(r);
+      MPCQP_PHASE_D(3);
     }
   }
   // ---- residual on the working set
@@ -327,6 +326,7 @@ __device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m
     w[r] = (inS && i < n + m) ? (float)e : 0.f;
   }
   wave_lds_sync();
+  MPCQP_PHASE_D(4);
 }
 
 template <int NR, int NXP>
@@ -479,6 +479,65 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
         axpy_rows(row, c, out);
       }
     };
+    // out += M0[:, F] w_F over the FREE z only (w is zero on fixed z, whose
+    // rows are skipped); kZB rows per memory round trip, the next batch in
+    // flight while the current one is accumulated
+    auto zcols_free = [&](const float (&wv)[NR], float (&out)[NR]) {
+      uint64_t mk0 = __builtin_amdgcn_ballot_w64(st[0] == 0 && l < n);
+      uint64_t mk1 = NR > 1 ? __builtin_amdgcn_ballot_w64(st[NR > 1 ? 1 : 0] == 0 && l + kWave < n) : 0;
+      uint64_t mk2 = NR > 2 ? __builtin_amdgcn_ballot_w64(st[NR > 2 ? 2 : 0] == 0 && l + 2 * kWave < n) : 0;
+      auto take = [&](int& j, float& c) __attribute__((always_inline)) {
+        j = -1;
+        c = 0.f;
+        if (mk0) {
+          const int bit = __builtin_ctzll(mk0);
+          mk0 &= mk0 - 1;
+          j = bit;
+          c = readlane(wv[0], bit);
+        } else if (mk1) {
+          const int bit = __builtin_ctzll(mk1);
+          mk1 &= mk1 - 1;
+          j = kWave + bit;
+          c = readlane(wv[NR > 1 ? 1 : 0], bit);
+        } else if (mk2) {
+          const int bit = __builtin_ctzll(mk2);
+          mk2 &= mk2 - 1;
+          j = 2 * kWave + bit;
+          c = readlane(wv[NR > 2 ? 2 : 0], bit);
+        }
+      };
+      auto load = [&](float (&v)[kZB][NR], float (&c)[kZB]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < kZB; ++t) {
+          int j;
+          take(j, c[t]);
+          const float* rp = M0 + (int64_t)(j < 0 ? 0 : j) * nt;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            v[t][r] = (j >= 0 && i < nt) ? rp[i] : 0.f;  // exhausted slots load nothing
+          }
+        }
+      };
+      float v[kZB][NR], c[kZB];
+      load(v, c);
+      while (true) {
+        const bool more = (mk0 | mk1 | mk2) != 0;
+        float vn[kZB][NR], cn[kZB];
+        if (more) load(vn, cn);
+#pragma unroll
+        for (int t = 0; t < kZB; ++t)
+#pragma unroll
+          for (int r = 0; r < NR; ++r) out[r] = fmaf(c[t], v[t][r], out[r]);
+        if (!more) break;
+#pragma unroll
+        for (int t = 0; t < kZB; ++t) {
+          c[t] = cn[t];
+#pragma unroll
+          for (int r = 0; r < NR; ++r) v[t][r] = vn[t][r];
+        }
+      }
+    };
     // out += M0[:, z] c_z with c_z = coef(j) for j < n; the next batch's
     // rows are in flight while the current one is accumulated
     auto zcols = [&](auto&& coef, float (&out)[NR]) {
@@ -599,16 +658,22 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
       }
     };
 
-    MPCQP_PHASE(0);
+    MPCQP_PHASE_K(0);
     refresh();
-    MPCQP_PHASE(1);
+    MPCQP_PHASE_K(1);
+    // DYN: after the refinement, the exact values are re-scanned with a tight
+    // tolerance; a bound the fp32 active set left within a.tol of violation
+    // (invisible to it, but amplified by ill-conditioning) re-enters the
+    // active set, and the refinement runs again
+    float tolc = a.tol;
+    for (int round = 0; round < (NXP > 0 ? 3 : 1); ++round) {
     bool active = true;
     for (int pass = 0; pass < 3 && active; ++pass) {
       while (true) {
         float viol;
         int p;
         scan(viol, p);
-        if (!(viol > a.tol)) break;
+        if (!(viol > tolc)) break;
         const float valp0 = pick<NR>(val, p);
         float valp = valp0;
         const float lop = s_lo[p], hip = s_hi[p];
@@ -656,10 +721,10 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
               }
             }
           }
-          MPCQP_PHASE(2);
+          MPCQP_PHASE_K(2);
           const float u = gather(col);
           const float v = smul(u);
-          MPCQP_PHASE(3);
+          MPCQP_PHASE_K(3);
 #pragma unroll
           for (int t = 0; t < kB; ++t) {
             const float c = j0[t] >= 0 ? readlane(v, j0[t]) : 0.f;
@@ -667,7 +732,7 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
             for (int r = 0; r < NR; ++r) col[r] = fmaf(c, v0[t][r], col[r]);
           }
           pcols(v, col, 1.f, false, mrest);
-          MPCQP_PHASE(4);
+          MPCQP_PHASE_K(4);
 #pragma unroll
           for (int r = 0; r < NR; ++r) {
             const int i = l + kWave * r;
@@ -713,7 +778,7 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
             mu[r] = fmaf(s_eff, dmu, mu[r]);
           }
           tau = fmaf(s_eff, dtds, tau);
-          MPCQP_PHASE(5);
+          MPCQP_PHASE_K(5);
           if (partial) {
             // k leaves the active set
             if (!dep) valp = fmaf(sgn, s_eff, valp);
@@ -762,21 +827,21 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
             }
           }
           added = !partial;
-          MPCQP_PHASE(6);
+          MPCQP_PHASE_K(6);
         }
       }
-      MPCQP_PHASE(2);
+      MPCQP_PHASE_K(2);
       refresh();
-      MPCQP_PHASE(1);
+      MPCQP_PHASE_K(1);
       {
         float viol;
         int p;
         scan(viol, p);
-        active = viol > a.tol;
+        active = viol > tolc;
       }
     }
     if (active) code = MPCQP_STATUS_MAXITER;
-    MPCQP_PHASE(2);
+    MPCQP_PHASE_K(2);
 
     // ------------------------------------------- iterative refinement
     const float* Hb = a.H + (int64_t)b * a.sH;
@@ -785,6 +850,7 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
     // when it fits one chunk
     int dyn_loaded = -1;
     for (int it = 0; it < a.refine; ++it) {
+      MPCQP_PHASE_D(0);
       float x[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
@@ -795,9 +861,10 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
         x[r] = (st[r] == 3) ? 0.f : (isz ? val[r] : (act ? sside * mu[r] : 0.f));
       }
       float w[NR];
+      float dmax = 0.f;
       if constexpr (NXP > 0) {
-        dyn_residual<NR, NXP>(a.d, b, n, m, l, x, st, pool, dyn_loaded, w);
-        MPCQP_PHASE(0);  // phase timing: the residual is charged with the setup
+        dyn_residual<NR, NXP>(a.d, b, n, m, l, x, st, pool, dyn_loaded, w MPCQP_CLK_ARG);
+        MPCQP_PHASE_K(0);  // phase timing: the residual is charged with the setup
       } else {
       // yk = K x in fp64, K = [[H, G'], [G, 0]]: row sweeps over packed H
       // and over G; the row-direction sums reduce 8 rows at a time in LDS
@@ -894,7 +961,12 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
       float y2[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) y2[r] = 0.f;
-      zcols([&](int j) __attribute__((always_inline)) { return pick<NR>(w, j); }, y2);
+      // (measured: skipping the fixed z rows pays in the DYN kernels, the
+      // plain sweep over every z row is faster in the others)
+      if constexpr (NXP > 0)
+        zcols_free(w, y2);
+      else
+        zcols([&](int j) __attribute__((always_inline)) { return pick<NR>(w, j); }, y2);
       const float ys = gather(y2);
       const float wsl = gather(w);
       const float q = smul(aidx >= 0 ? ys - wsl : 0.f);
@@ -908,12 +980,33 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
         const float sv = act ? -qi : y2[r];
         const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
         val[r] = (isz && st[r] == 0) ? val[r] + sv : val[r];
+        val[r] = (!isz && st[r] == 0) ? val[r] - sv : val[r];  // row values G z
         mu[r] = (!isz && act) ? mu[r] + sside * sv : mu[r];
+        dmax = (isz && st[r] == 0) ? fmaxf(dmax, fabsf(sv) / (1.f + fabsf(val[r]))) : dmax;
       }
+      // DYN: the residual is exact, so a small correction means converged
+      // (the next step would shrink it by the contraction of the fp32 M0,
+      // ~1e-2); a large one (ill-conditioned instance) takes another step
+      MPCQP_PHASE_D(5);
+      if constexpr (NXP > 0) {
+        if (!(wave_max(dmax) > kDynStop)) break;
+      }
+    }
+    if constexpr (NXP > 0) {
+      float viol;
+      int p;
+      scan(viol, p);
+      MPCQP_PHASE_D(6);
+      if (!(viol > kDynTol) || code != MPCQP_STATUS_OPTIMAL) break;
+      tolc = kDynTol;
+    } else {
+      break;
+    }
     }
   }
 out:
-  MPCQP_PHASE(7);
+  MPCQP_PHASE_K(7);
+  MPCQP_PHASE_D(7);
   {
     const bool ok = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
 #pragma unroll

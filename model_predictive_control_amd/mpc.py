@@ -10,16 +10,16 @@ device:
   1.+2. nominal rollout of the forward-Euler model from x0 with the warm-
      started input sequence (previous solution shifted one stage) and the
      per-stage linearisation (A_k, B_k, c_k)    (libmpcqp ``mpcqp_bicycle_rti``),
-  3. time-varying condensing  -> H, f        (libmpcqp ``mpcqp_condense``, TV),
-  4. input-box QP                            (libmpcqp ``mpcqp_solve_box``),
+  3.+4. time-varying condensing and the QP, with the predicted states, in
+     one call                                (libmpcqp ``mpcqp_mpc_qp``),
 
 repeated ``sqp_iters`` times.  Any number of initial states is solved in one
 batch (``solve`` accepts x of shape (nx,) or (batch, nx)).
 
 With ``state_box=True`` (default) the state box of main.py:58-61 on x_1..x_N
-is enforced as well: step 3 also returns Gam and the free response xbar, and
-step 4 becomes ``mpcqp_solve_qp`` with rows  x_min - xbar <= Gam z <= x_max -
-xbar  (one QP per workgroup; needs N*(nx+nu) <= 192, i.e. N <= 32).  The
+is enforced as well (rows  x_min - xbar <= Gam z <= x_max - xbar  of the
+condensed QP; needs N*(nx+nu) <= 192, i.e. N <= 32); without it the QP has
+the input box only.  The
 collision rows of main.py:95-104 are non-convex and out of scope.
 """
 from __future__ import annotations
@@ -97,25 +97,19 @@ class MPCController:
             U = self._warm
         else:
             U = torch.zeros((b, N, nu), dtype=self.dtype, device=self.device)
-        z = status = None
+        z = status = X = None
         for _ in range(self.sqp_iters):
             # FE rollout from x0 under U + per-stage (A_k, B_k, c_k): one launch
             A, B, c = batched.bicycle_rti(X0, U, self.params, self.ts)
-            if self.state_box:
-                d = batched.condense(A.contiguous(), B.contiguous(), self.Q, self.R, self.QN, N,
-                                     x0=X0, c=c.contiguous(), tv=True,
-                                     outputs=("H", "f", "Gam", "xbar"))
-                z, lam, status = batched.solve_qp(d["H"], d["f"], d["Gam"], self.xmin - d["xbar"],
-                                                  self.xmax - d["xbar"], self.lbz, self.ubz)
-                self.last_lam_g = lam
-            else:
-                d = batched.condense(A.contiguous(), B.contiguous(), self.Q, self.R, self.QN, N,
-                                     x0=X0, c=c.contiguous(), tv=True, outputs=("H", "f", "Gam", "xbar"))
-                z, status = batched.solve_box(d["H"], d["f"], self.lbz, self.ubz)
+            # condense + QP (+ predicted states) in one libmpcqp call
+            box = dict(xlo=self.xmin, xhi=self.xmax) if self.state_box else {}
+            z, lam, status, X = batched.mpc_qp(A, B, self.Q, self.R, self.QN, N, X0, c=c,
+                                               lb=self.lbz, ub=self.ubz, tv=True, states=True,
+                                               **box)
+            self.last_lam_g = lam
             U = z.view(b, N, nu)
         # predicted states x_1..x_N of the last linearisation (IPOPT's "g" rows)
-        self.last_prediction = (d["xbar"] + torch.bmm(d["Gam"], z.unsqueeze(-1)).squeeze(-1)
-                                ).view(b, N, self.nx)
+        self.last_prediction = X
         self._warm = torch.cat([U[:, 1:], U[:, -1:]], 1).contiguous()
         self.last_status = status
         return z, status

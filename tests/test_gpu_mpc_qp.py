@@ -201,3 +201,25 @@ def test_mpc_qp_errors(dev):
     from model_predictive_control_amd._native import MpcqpError
     with pytest.raises(MpcqpError):  # N*(nu+nx) beyond the QP size limit
         batched.mpc_qp(A, B, Q, R, Q, 400, x0, xlo=-torch.ones(2, dtype=torch.float64, device=dev))
+
+
+@pytest.mark.parametrize("dt,tol", [(torch.float64, 1e-10)])
+def test_mpc_qp_input_box_small_matches_mpc_box(dev, dt, tol):
+    """Input box only, n <= 64 (the box-kernel branch of mpcqp_mpc_qp): the
+    same z as the fused mpcqp_mpc_box on the config-2 plant (fp64, the
+    config's dtype; its Hessian, cond ~6e3, is not an fp32 problem)."""
+    rng = np.random.default_rng(5)
+    N, b = 20, 64
+    A = np.array([[1.0, 0.5], [0.0, 1.0]])
+    B = np.array([[0.0], [-0.5]])
+    C = np.array([[1.0], [-2.0 / 3.0]])
+    Q = C @ C.T + 1e-3 * np.eye(2)
+    R = np.array([[0.1]])
+    t = lambda a: torch.as_tensor(a, dtype=dt, device=dev)  # noqa: E731
+    X0 = t(rng.uniform(-10, 10, (b, 2)))
+    z1, y, st1 = batched.mpc_qp(t(A), t(B), t(Q), t(R), t(Q), N, X0, lb=-1.0, ub=1.0)
+    z2, st2 = batched.mpc_box(t(A), t(B), t(Q), t(R), t(Q), N, X0, -1.0, 1.0)
+    torch.cuda.synchronize()
+    assert y is None
+    assert (batched.status_code(st1) == 0).all() and (batched.status_code(st2) == 0).all()
+    assert float((z1 - z2).abs().max()) < tol

@@ -13,12 +13,17 @@ SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.h
         "solve_qp.hip", "sweep.hip", "solve_pf.hip", "mpc_qp.hip", "bicycle.hip", "misc.hip"]
 PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/recheck", "GI: scan+argmax", "GI: pivot col+ratio", "GI: sweep"]
 
+DYN = "--dyn" in sys.argv or (len(sys.argv) > 1 and sys.argv[1].startswith("dyn"))
+if DYN:  # a separate library whose pf kernel clock times the DYN refinement
+    LIB = LIB.replace("_timing.so", "_timing_dyn.so")
+
 if "--build" in sys.argv:
     objs = []
     for s in SRCS:
         o = f"/tmp/timing_{s}.o"
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
-                        "-DMPCQP_PHASE_TIMING", "-I", os.path.join(ROOT, "include"), "-c"]
+                        "-DMPCQP_PHASE_TIMING"] + (["-DMPCQP_PHASE_DYN"] if DYN else []) + [
+                        "-I", os.path.join(ROOT, "include"), "-c"]
                        + (["-mllvm", "-pragma-unroll-threshold=1000000"] if s == "sweep.hip" else []) + [
                         os.path.join(CS, s), "-o", o], check=True)
         objs.append(o)
@@ -34,8 +39,8 @@ from model_predictive_control_amd import _native, batched  # noqa: E402
 
 lib = _native.load()
 arg = sys.argv[1] if len(sys.argv) > 1 else "2"
-pf = arg.startswith("pf")
-cfg = int(arg[2:] if pf else arg)
+pf = arg.startswith("pf") or arg.startswith("dyn")
+cfg = int(arg[3:] if arg.startswith("dyn") else (arg[2:] if pf else arg))
 reader = lib.mpcqp_debug_phase_cycles if cfg == 2 else lib.mpcqp_debug_phase_cycles_qp
 reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = (ctypes.c_ulonglong * 8)()
@@ -69,6 +74,9 @@ elif pf:
     # phase 0 and the M0 correction to phase 7)
     PHASES = ["setup + s0 (+DYN residual)", "refresh", "scan + col load", "gather + S^-1 u",
               "M0[:,P] v", "ratio + update", "S^-1 update", "refinement (correction)"]
+    if DYN:
+        PHASES = ["active set (all)", "DYN: stage loads", "DYN: forward", "DYN: backward",
+                  "DYN: residual tail", "correction (M0)", "re-scan", "output"]
     a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1; a.check = 0
     w = bench.CONFIGS[cfg](a, torch.device("cuda"), 0)
     run = lambda: w.step(0)  # noqa: E731
