@@ -70,6 +70,9 @@ __device__ __forceinline__ T quad_sum(T v) {
 template <typename T, int BS>
 struct QSym {
   static constexpr int NMAX = 4 * BS;
+  static constexpr int NV = NMAX;  // row-indexed vectors
+  static constexpr int NC = BS;    // columns per lane
+  static constexpr int RPL = BS;   // rows per lane
   static constexpr int CBUF = NMAX * BS;  // column-publish tile (per group)
   static constexpr int BUF = CBUF + NMAX;  // + mat-vec vector
   T m[BS][BS];
@@ -186,16 +189,20 @@ struct QSym {
   }
 };
 
-// Per-group LDS block for the box active set: [CBUF+NMAX | f | lb | ub].
-template <typename T, int BS>
-struct QBoxLds {
-  static constexpr int NMAX = 4 * BS;
+// Per-group LDS block for the box active set: [Mat::BUF | f | lb | ub], the
+// vectors indexed by (padded) row.
+template <class Mat>
+struct GBoxLds {
+  static constexpr int NMAX = Mat::NMAX;
+  static constexpr int NV = Mat::NV;
   static constexpr int oBuf = 0;
-  static constexpr int oF = QSym<T, BS>::BUF;
-  static constexpr int oLb = oF + NMAX;
-  static constexpr int oUb = oLb + NMAX;
-  static constexpr int size = oUb + NMAX;
+  static constexpr int oF = Mat::BUF;
+  static constexpr int oLb = oF + NV;
+  static constexpr int oUb = oLb + NV;
+  static constexpr int size = oUb + NV;
 };
+template <typename T, int BS>
+using QBoxLds = GBoxLds<QSym<T, BS>>;
 
 // Relative-violation scale of a bound: 1/(1+|b|) for a finite bound, NaN for
 // an infinite one (a NaN violation never wins the arg-max and fmax skips it),
@@ -337,7 +344,8 @@ __device__ __forceinline__ int gi_box(Mat& M, T* gb, const T* fs, const T* lbs,
         active = false;
         stepping = false;
       }
-      T c[BS], cc[BS];
+      constexpr int NC = Mat::NC;  // columns per lane
+      T c[BS], cc[NC];
       const T mpp = M.column(p, gb, c, cc);  // c[r] = M_ip, M_pp < 0
       const T rm = fast_rcp(mpp);
       const T sgn = (tgt > zp) ? T(1) : T(-1);
@@ -372,16 +380,15 @@ __device__ __forceinline__ int gi_box(Mat& M, T* gb, const T* fs, const T* lbs,
       const T sigma = partial ? T(1) : T(-1);
       // full steps sweep on p, whose column is still in registers: publish
       // again only when some group of the wave drops a bound
-      T kr[BS], kcol[BS];
+      T kr[BS], kcol[NC];
       T d = mpp;
       if (__any(stepping && partial)) {
         d = M.column(idx, gb, kr, kcol);
       } else {
 #pragma unroll
-        for (int r = 0; r < BS; ++r) {
-          kr[r] = c[r];
-          kcol[r] = cc[r];
-        }
+        for (int r = 0; r < BS; ++r) kr[r] = c[r];
+#pragma unroll
+        for (int r = 0; r < NC; ++r) kcol[r] = cc[r];
       }
       const bool bad = stepping && (partial ? !(d > T(0)) : !(d < T(0)));
       if (stepping && !bad) {

@@ -103,12 +103,12 @@ __global__ __launch_bounds__(64, (QuadOcc<T, BS>::w)) void box_quad_kernel(BoxAr
 }
 
 // ----------------------------------------------------------- fused kernel
-template <typename T, int NX, int NU, int BS>
+template <typename T, int NX, int NU, class Mat>
 struct QMpcLds {
   int oA, oB, oQ, oQf, oR, oC, oX0, oK, oSi, oAcl, oX, oKf, oMinv, total, ld;
   __host__ __device__ QMpcLds(int N, int n, int tv) {
     const int S = tv ? N : 1;
-    oA = QBoxLds<T, BS>::size;
+    oA = GBoxLds<Mat>::size;
     oB = oA + S * NX * NX;
     oQ = oB + S * NX * NU;
     oQf = oQ + NX * NX;
@@ -139,18 +139,27 @@ struct QMpcOcc {
   static constexpr int w = NX <= 2 ? QuadOcc<T, BS>::w : (QuadOcc<T, BS>::w < 2 ? 1 : 2);
 };
 
-template <typename T, int NX, int NU, int BS>
-__global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(MpcArgsQ<T> a) {
-  using BL = QBoxLds<T, BS>;
-  constexpr int NMAX = BL::NMAX;
+// GL lanes per QP (16 with QSym: four QPs per wave); OCC: minimum waves per
+// SIMD the register allocation must allow.  Measured and rejected: two QPs
+// per wave (32-lane groups, 3 x 5 blocks at n = 20, row-block reductions
+// through v_permlane16_swap): 73.1 vs 70.6 us at config 2 -- the per-wave
+// fixed work (Riccati, x-bar/adjoint chains, reductions) doubles per QP, so
+// VALU instructions per QP rose 47 % (PMC SQ_INSTS_VALU) while the two waves
+// per SIMD hid only part of it.
+template <typename T, int NX, int NU, class Mat, int GL, int OCC>
+__global__ __launch_bounds__(64, OCC) void mpc_group_kernel(MpcArgsQ<T> a) {
+  using BL = GBoxLds<Mat>;
+  constexpr int NV = BL::NV;
+  constexpr int RPL = Mat::RPL;
+  constexpr int GPW = kWave / GL;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  const int lane = threadIdx.x, g = lane >> 4, q = lane & 15;
-  const int b = blockIdx.x * 4 + g;
+  const int lane = threadIdx.x, g = lane / GL, q = lane % GL;
+  const int b = blockIdx.x * GPW + g;
   const bool live = b < a.batch;
   const int bl = live ? b : 0;
   const int nx = a.nx, nu = a.nu, N = a.N, n = N * nu, tv = a.tv;
   const int S = tv ? N : 1;
-  const QMpcLds<T, NX, NU, BS> L(N, n, tv);
+  const QMpcLds<T, NX, NU, Mat> L(N, n, tv);
   T* sm = reinterpret_cast<T*>(smem_raw) + g * L.total;
   T* gb = sm + BL::oBuf;
   T* fs = sm + BL::oF;
@@ -178,37 +187,37 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
   bool nonfinite = false, badbox = false;
   {
     const T* Ab = a.A + (int64_t)bl * a.sA;
-    for (int e = q; e < S * NX * NX; e += 16) {
+    for (int e = q; e < S * NX * NX; e += GL) {
       const int s = e / (NX * NX), r = (e / NX) % NX, cc = e % NX;
       const T v = (r < nx && cc < nx) ? Ab[(int64_t)s * nx * nx + r * nx + cc] : T(0);
       As[e] = v;
       nonfinite |= !finite(v);
     }
     const T* Bb = a.B + (int64_t)bl * a.sB;
-    for (int e = q; e < S * NX * NU; e += 16) {
+    for (int e = q; e < S * NX * NU; e += GL) {
       const int s = e / (NX * NU), r = (e / NU) % NX, cc = e % NU;
       const T v = (r < nx && cc < nu) ? Bb[(int64_t)s * nx * nu + r * nu + cc] : T(0);
       Bs[e] = v;
       nonfinite |= !finite(v);
     }
-    for (int e = q; e < NX * NX; e += 16) {
+    for (int e = q; e < NX * NX; e += GL) {
       const int r = e / NX, cc = e % NX;
       const bool in = live && r < nx && cc < nx;
       Qs[e] = in ? a.Q[(int64_t)b * a.sQ + r * nx + cc] : T(0);
       Qfs[e] = in ? a.Qf[(int64_t)b * a.sQf + r * nx + cc] : T(0);
     }
-    for (int e = q; e < NU * NU; e += 16) {
+    for (int e = q; e < NU * NU; e += GL) {
       const int r = e / NU, cc = e % NU;
       // padded inputs get R = I so that S_k stays invertible (their B cols are 0)
       Rs[e] = (live && r < nu && cc < nu) ? a.R[(int64_t)b * a.sR + r * nu + cc] : (r == cc ? T(1) : T(0));
     }
     const T* Cb = (live && a.c) ? a.c + (int64_t)b * a.sC : nullptr;
-    for (int e = q; e < N * NX; e += 16) {
+    for (int e = q; e < N * NX; e += GL) {
       const int k = e / NX, cc = e % NX;
       Cs[e] = (Cb && cc < nx) ? Cb[k * nx + cc] : T(0);
     }
     if (q < NX) X0s[q] = (live && a.x0 && q < nx) ? a.x0[(int64_t)b * a.sX0 + q] : T(0);
-    for (int i = q; i < NMAX; i += 16) {
+    for (int i = q; i < NV; i += GL) {
       const bool v = live && i < n;
       const T li = (v && a.lb) ? a.lb[(int64_t)b * a.slb + i] : -Lim<T>::inf();
       const T ui = (v && a.ub) ? a.ub[(int64_t)b * a.sub + i] : Lim<T>::inf();
@@ -410,7 +419,7 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
 
   MPCQP_PHASE(2);
   // ------------------------------ columns of -H^{-1}, one lane per column
-  for (int c = q; c < n; c += 16) {
+  for (int c = q; c < n; c += GL) {
     const int jj = c / nu, bb = c - jj * nu;
     T s[NX], kf[NU];
     // k = jj: kff = S^{-1} e_b, s = -K' e_b
@@ -483,17 +492,17 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
 
   MPCQP_PHASE(3);
   // ------------------------------------------------ box QP on M = -H^{-1}
-  QSym<T, BS> M;
+  Mat M;
   M.init(lane);
   M.load_dense_sym(Mv, ld, n);
-  for (int i = q; i < n; i += 16) nonfinite |= !finite(fs[i]);
-  const unsigned long long gmask = 0xFFFFull << (16 * g);
+  for (int i = q; i < n; i += GL) nonfinite |= !finite(fs[i]);
+  const unsigned long long gmask = (GL == 64 ? ~0ull : ((1ull << GL) - 1)) << (GL * g);
   if ((__ballot(nonfinite) & gmask) != 0) code = MPCQP_STATUS_NONFINITE;
   else if ((__ballot(badbox) & gmask) != 0) code = MPCQP_STATUS_INFEASIBLE;
-  T zr[BS];
+  T zr[RPL];
   int iters = 0;
-  const int c2 = gi_box<T, BS>(M, gb, fs, lbs, ubs, n, a.max_iter, a.tol,
-                                    live && code == MPCQP_STATUS_OPTIMAL, zr, iters MPCQP_CLK_ARG);
+  const int c2 = gi_box<T, RPL>(M, gb, fs, lbs, ubs, n, a.max_iter, a.tol,
+                                     live && code == MPCQP_STATUS_OPTIMAL, zr, iters MPCQP_CLK_ARG);
   if (code == MPCQP_STATUS_OPTIMAL) code = c2;
   MPCQP_PHASE(4);
 #ifdef MPCQP_PHASE_TIMING
@@ -501,12 +510,12 @@ __global__ __launch_bounds__(64, (QMpcOcc<T, NX, BS>::w)) void mpc_quad_kernel(M
 #endif
   if (code != MPCQP_STATUS_OPTIMAL && code != MPCQP_STATUS_MAXITER) {
 #pragma unroll
-    for (int r = 0; r < BS; ++r) zr[r] = __builtin_nan("");
+    for (int r = 0; r < RPL; ++r) zr[r] = __builtin_nan("");
   }
   if (live && M.bj == 0) {
 #pragma unroll
-    for (int r = 0; r < BS; ++r) {
-      const int i = M.bi * BS + r;
+    for (int r = 0; r < RPL; ++r) {
+      const int i = M.bi * RPL + r;
       if (i < n) a.z[(int64_t)b * n + i] = zr[r];
     }
   }
@@ -538,24 +547,31 @@ int solve_box_quad(const BoxArgsQ<T>& a, hipStream_t st) {
   }
 }
 
-template <typename T, int NX, int NU, int BS>
-int launch_mpc_quad(const MpcArgsQ<T>& a, hipStream_t st) {
+template <typename T, int NX, int NU, class Mat, int GL, int OCC>
+int launch_mpc_group(const MpcArgsQ<T>& a, hipStream_t st) {
+  constexpr int GPW = kWave / GL;
   const int n = a.N * a.nu;
-  const QMpcLds<T, NX, NU, BS> L(a.N, n, a.tv);
-  const size_t bytes = (size_t)4 * L.total * sizeof(T);
+  const QMpcLds<T, NX, NU, Mat> L(a.N, n, a.tv);
+  const size_t bytes = (size_t)GPW * L.total * sizeof(T);
   if (bytes > 160 * 1024) {
     set_error("mpcqp_mpc_box: LDS footprint %zu B > 160 KiB", bytes);
     return MPCQP_ENOTSUP;
   }
+  auto kern = mpc_group_kernel<T, NX, NU, Mat, GL, OCC>;
   if (bytes > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)mpc_quad_kernel<T, NX, NU, BS>,
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(mpc_quad)");
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(mpc_group)");
   }
-  hipLaunchKernelGGL((mpc_quad_kernel<T, NX, NU, BS>), dim3((a.batch + 3) / 4), dim3(kWave), bytes,
-                     st, a);
-  MPCQP_CHECK_LAUNCH("mpc_quad_kernel");
+  hipLaunchKernelGGL(kern, dim3((a.batch + GPW - 1) / GPW), dim3(kWave), bytes, st, a);
+  MPCQP_CHECK_LAUNCH("mpc_group_kernel");
   return MPCQP_OK;
+}
+
+// four QPs per wave (QSym, 16 lanes each)
+template <typename T, int NX, int NU, int BS>
+int launch_mpc_quad(const MpcArgsQ<T>& a, hipStream_t st) {
+  return launch_mpc_group<T, NX, NU, QSym<T, BS>, 16, QMpcOcc<T, NX, BS>::w>(a, st);
 }
 
 template <typename T, int NX, int NU>

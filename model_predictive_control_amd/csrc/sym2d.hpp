@@ -115,6 +115,9 @@ __device__ __forceinline__ void blocks_argmin(T& v, int& idx) {
 template <typename T, int BS>
 struct Sym2D {
   static constexpr int NMAX = 8 * BS;
+  static constexpr int NV = NMAX;  // row-indexed vectors
+  static constexpr int NC = BS;    // columns per lane
+  static constexpr int RPL = BS;   // rows per lane
   // LDS scratch a kernel must provide: BUF elements
   static constexpr int BUF = NMAX * BS + NMAX;
   T m[BS][BS];
