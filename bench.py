@@ -230,7 +230,7 @@ class Config2:
                    traffic.get("solve_box"), {"bytes_per_launch": sb})
         # fused kernel: SURVEY.md 8(d) per-instance figure (22.0 kflop condense,
         # config 2) against the fp64 peak; it moves only A, B, x0 in and z out.
-        r_f = roof("mpc_quad_kernel<double,2,1,5>", "mfma", fl, t_f, FP64_PEAK_TFS, "TFLOP/s",
+        r_f = roof("mpc_group_kernel<double,2,1,QSym<double,5>,16,2>", "mfma", fl, t_f, FP64_PEAK_TFS, "TFLOP/s",
                    traffic.get("mpc_box"), {"flops_per_launch": fl,
                                             "hbm_bytes_per_launch": (nx * nx + nx * nu + nx + n) * 8 * bsz + 4 * bsz})
         # split vs fused agreement on the same slot

@@ -261,6 +261,18 @@ void sweep_mfma_kernel(SweepArgs a) {
         bst(v[i], rM, keep ? 4 * (r * nt + cc) : kOOB);
       }
     };
+    // off-diagonal tiles with 16-byte stores: a tile's transpose holds, per
+    // lane, 4 consecutive columns of one of its rows (row cs, columns 4 gs..)
+    // -- so tile (rb, cb) is stored from its transpose and the mirror tile
+    // (cb, rb) from the tile itself, one dwordx4 per lane instead of four
+    // dword stores (the epilogue is store-issue bound).  Needs n, m % 4 == 0
+    // (4-column groups never straddle the z/row or padding boundaries, rows
+    // 16-byte aligned).
+    const bool vec4 = ((n | m) & 3) == 0;
+    auto put16 = [&](const mf4& v, int rb, int cb) {
+      const int r = orig(16 * rb + cs), c0 = orig(16 * cb + 4 * gs);
+      bst4(v, rM, (r >= 0 && c0 >= 0) ? 4 * (r * nt + c0) : kOOB);
+    };
     // s0 = M F with F_j = f of z block j in every column (MFMA, from the
     // tiles and their transposes on their way out)
     const bool want_s0 = a.s0 != nullptr;
@@ -282,6 +294,9 @@ void sweep_mfma_kernel(SweepArgs a) {
         if (ti == tj) {
           put(t[tri(ti, tj)], ti, tj, 1);
           put(tt, ti, tj, 2);
+        } else if (vec4) {
+          put16(tt, ti, tj);
+          put16(t[tri(ti, tj)], tj, ti);
         } else {
           put(t[tri(ti, tj)], ti, tj, 0);
           put(tt, tj, ti, 0);
@@ -313,7 +328,9 @@ void sweep_mfma_kernel(SweepArgs a) {
 // the sweep only ever subtracts into, is formed at the end as
 //     M_GG = -G H^-1 G' = -M_Gz G'       (MFMA against G' re-read from HBM)
 // so the register file holds 42 instead of 78 tiles at config 3 (KP = 4,
-// TR = 8) and the kernel runs without spills.
+// TR = 8) and the kernel runs without spills.  G is staged in LDS once (m n
+// floats, <= 36 KB; one wave per SIMD): the M_GG products read each G tile
+// (jr, k) once per row tile ir >= jr, which from HBM was ~5x the bytes of G.
 template <int KP>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
 void sweep_rows_kernel(SweepArgs a) {
@@ -329,6 +346,25 @@ void sweep_rows_kernel(SweepArgs a) {
   const rsrc_t rG = mk_rsrc(Gb, (int64_t)m * n * 4);
   mf4 Z[NZ], Gt[TRM][KP];
   bool nonfin = false;
+  // G into LDS: every load of a 16-register batch issued before its stores
+  extern __shared__ float Gs[];
+  {
+    const int cnt = m * n;
+    for (int e0 = 0; e0 < cnt; e0 += 16 * kWave) {
+      float t[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int e = e0 + l + kWave * k;
+        t[k] = bld(rG, e < cnt ? 4 * e : kOOB);
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int e = e0 + l + kWave * k;
+        if (e < cnt) Gs[e] = t[k];
+      }
+    }
+    __syncthreads();
+  }
   // zz: packed H, mirrored on the diagonal tiles, unit pad pivots
 #pragma unroll
   for (int ti = 0; ti < KP; ++ti)
@@ -353,7 +389,7 @@ void sweep_rows_kernel(SweepArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int rho = 16 * ir + 4 * g + i, z = 16 * k + c;
-        const float v = bld(rG, (rho < m && z < n) ? 4 * (rho * n + z) : kOOB);
+        const float v = (rho < m && z < n) ? Gs[rho * n + z] : 0.f;
         nonfin |= !finite(v);
         Gt[ir][k][i] = v;
       }
@@ -428,6 +464,15 @@ void sweep_rows_kernel(SweepArgs a) {
       bst(v[i], rM, keep ? 4 * (r * nt + cc) : kOOB);
     }
   };
+  // 16-byte stores of off-diagonal tiles (see the generic kernel): v holds
+  // row cs of tile (rb, cb), columns 4 gs .. 4 gs + 3
+  const bool vec4 = ((n | m) & 3) == 0;
+  auto put16 = [&](const mf4& v, int rb, bool rrow, int cb, bool crow) {
+    const int r0 = 16 * rb + cs, c0 = 16 * cb + 4 * gs;
+    const int r = rrow ? (r0 < m ? n + r0 : -1) : (r0 < n ? r0 : -1);
+    const int cc = crow ? (c0 < m ? n + c0 : -1) : (c0 < n ? c0 : -1);
+    bst4(v, rM, (r >= 0 && cc >= 0) ? 4 * (r * nt + cc) : kOOB);
+  };
   const bool want_s0 = a.s0 != nullptr;
   mf4 F[KP];
 #pragma unroll
@@ -450,6 +495,9 @@ void sweep_rows_kernel(SweepArgs a) {
         if (ti == tj) {
           put(Z[tri(ti, tj)], ti, false, tj, false, 1);
           put(tt, ti, false, tj, false, 2);
+        } else if (vec4) {
+          put16(tt, ti, false, tj, false);
+          put16(Z[tri(ti, tj)], tj, false, ti, false);
         } else {
           put(Z[tri(ti, tj)], ti, false, tj, false, 0);
           put(tt, tj, false, ti, false, 0);
@@ -480,8 +528,13 @@ void sweep_rows_kernel(SweepArgs a) {
 #pragma unroll
       for (int k = 0; k < KP; ++k) {
         tts[k] = mm(Gt[ir][k], eye, zero);
-        put(Gt[ir][k], ir, true, k, false, 0);
-        put(tts[k], k, false, ir, true, 0);
+        if (vec4) {
+          put16(tts[k], ir, true, k, false);
+          put16(Gt[ir][k], k, false, ir, true);
+        } else {
+          put(Gt[ir][k], ir, true, k, false, 0);
+          put(tts[k], k, false, ir, true, 0);
+        }
         if (want_s0) acc = mm(tts[k], F[k], acc);
       }
       if (want_s0 && cs == 0) {
@@ -500,7 +553,7 @@ void sweep_rows_kernel(SweepArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int rho = 16 * jr + cs, z = 16 * k + 4 * gs + e;
-            gt[e] = bld(rG, (rho < m && z < n) ? 4 * (rho * n + z) : kOOB);
+            gt[e] = (rho < m && z < n) ? Gs[rho * n + z] : 0.f;
           }
           gg = mm(tts[k], gt, gg);  // M_Gz(ir, k) G(jr, k)'
         }
@@ -509,6 +562,9 @@ void sweep_rows_kernel(SweepArgs a) {
         if (jr == ir) {
           put(gg, ir, true, jr, true, 1);
           put(ggt, ir, true, jr, true, 2);
+        } else if (vec4) {
+          put16(ggt, ir, true, jr, true);
+          put16(gg, jr, true, ir, true);
         } else {
           put(gg, ir, true, jr, true, 0);
           put(ggt, jr, true, ir, true, 0);
@@ -522,7 +578,8 @@ void sweep_rows_kernel(SweepArgs a) {
 
 template <int KP>
 static int launch_sweep_rows(const SweepArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((sweep_rows_kernel<KP>), dim3(a.batch), dim3(64), 0, st, a);
+  const size_t lds = (size_t)a.m * a.n * sizeof(float);  // G staged per wave
+  hipLaunchKernelGGL((sweep_rows_kernel<KP>), dim3(a.batch), dim3(64), lds, st, a);
   MPCQP_CHECK_LAUNCH("sweep_rows_kernel");
   return MPCQP_OK;
 }
