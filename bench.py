@@ -372,7 +372,7 @@ class Config3:
                    traffic.get("condense"), {"bytes_per_launch": cb})
         r_w = roof("sweep_rows_kernel<4>", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
                    traffic.get("sweep"), {"flops_per_launch": wf})
-        r_p = roof("qp_pf_kernel<3,true>", "hbm", pb, t_p, HBM_PEAK_GBS, "GB/s",
+        r_p = roof("qp_pf_kernel<3,4> (DYN refinement)", "hbm", pb, t_p, HBM_PEAK_GBS, "GB/s",
                    traffic.get("solve_pf"), {"bytes_per_launch": pb,
                                              "note": "time = mpc_qp - condense - sweep "
                                                      "(includes the rows kernel)"})
@@ -602,7 +602,7 @@ class Config5:
                    traffic.get("sweep"), {"flops_per_launch": wf})
         # pf reads M0, s0 and the dynamics (A_k, B_k, x0) for the refinement
         pb = (n * n + n + N * (nx * nx + nx * nu) + nx + n) * 4 * bsz
-        r_p = roof("qp_pf_kernel<3,true>", "hbm", pb, t_p, HBM_PEAK_GBS, "GB/s",
+        r_p = roof("qp_pf_kernel<3,12> (DYN refinement)", "hbm", pb, t_p, HBM_PEAK_GBS, "GB/s",
                    traffic.get("solve_pf"), {"bytes_per_launch": pb,
                                              "note": "time = mpc_qp - condense - sweep"})
         extra = {"kernel_us": {"condense": round(t_c * 1e3, 2), "sweep": round(t_w * 1e3, 2),

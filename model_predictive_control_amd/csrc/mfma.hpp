@@ -47,13 +47,5 @@ __device__ __forceinline__ float bld(rsrc_t r, int off) {
 __device__ __forceinline__ void bst(float v, rsrc_t r, int off) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
-// 16-byte store of a lane's four C-layout values (an offset past the range
-// drops all four)
-__device__ __forceinline__ void bst4(const mf4& v, rsrc_t r, int off) {
-  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-  const u4 w = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                __float_as_uint(v[3])};
-  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
-}
 
 }  // namespace mpcqp

@@ -261,18 +261,6 @@ void sweep_mfma_kernel(SweepArgs a) {
         bst(v[i], rM, keep ? 4 * (r * nt + cc) : kOOB);
       }
     };
-    // off-diagonal tiles with 16-byte stores: a tile's transpose holds, per
-    // lane, 4 consecutive columns of one of its rows (row cs, columns 4 gs..)
-    // -- so tile (rb, cb) is stored from its transpose and the mirror tile
-    // (cb, rb) from the tile itself, one dwordx4 per lane instead of four
-    // dword stores (the epilogue is store-issue bound).  Needs n, m % 4 == 0
-    // (4-column groups never straddle the z/row or padding boundaries, rows
-    // 16-byte aligned).
-    const bool vec4 = ((n | m) & 3) == 0;
-    auto put16 = [&](const mf4& v, int rb, int cb) {
-      const int r = orig(16 * rb + cs), c0 = orig(16 * cb + 4 * gs);
-      bst4(v, rM, (r >= 0 && c0 >= 0) ? 4 * (r * nt + c0) : kOOB);
-    };
     // s0 = M F with F_j = f of z block j in every column (MFMA, from the
     // tiles and their transposes on their way out)
     const bool want_s0 = a.s0 != nullptr;
@@ -294,9 +282,6 @@ void sweep_mfma_kernel(SweepArgs a) {
         if (ti == tj) {
           put(t[tri(ti, tj)], ti, tj, 1);
           put(tt, ti, tj, 2);
-        } else if (vec4) {
-          put16(tt, ti, tj);
-          put16(t[tri(ti, tj)], tj, ti);
         } else {
           put(t[tri(ti, tj)], ti, tj, 0);
           put(tt, tj, ti, 0);
@@ -464,15 +449,6 @@ void sweep_rows_kernel(SweepArgs a) {
       bst(v[i], rM, keep ? 4 * (r * nt + cc) : kOOB);
     }
   };
-  // 16-byte stores of off-diagonal tiles (see the generic kernel): v holds
-  // row cs of tile (rb, cb), columns 4 gs .. 4 gs + 3
-  const bool vec4 = ((n | m) & 3) == 0;
-  auto put16 = [&](const mf4& v, int rb, bool rrow, int cb, bool crow) {
-    const int r0 = 16 * rb + cs, c0 = 16 * cb + 4 * gs;
-    const int r = rrow ? (r0 < m ? n + r0 : -1) : (r0 < n ? r0 : -1);
-    const int cc = crow ? (c0 < m ? n + c0 : -1) : (c0 < n ? c0 : -1);
-    bst4(v, rM, (r >= 0 && cc >= 0) ? 4 * (r * nt + cc) : kOOB);
-  };
   const bool want_s0 = a.s0 != nullptr;
   mf4 F[KP];
 #pragma unroll
@@ -495,9 +471,6 @@ void sweep_rows_kernel(SweepArgs a) {
         if (ti == tj) {
           put(Z[tri(ti, tj)], ti, false, tj, false, 1);
           put(tt, ti, false, tj, false, 2);
-        } else if (vec4) {
-          put16(tt, ti, false, tj, false);
-          put16(Z[tri(ti, tj)], tj, false, ti, false);
         } else {
           put(Z[tri(ti, tj)], ti, false, tj, false, 0);
           put(tt, tj, false, ti, false, 0);
@@ -528,13 +501,8 @@ void sweep_rows_kernel(SweepArgs a) {
 #pragma unroll
       for (int k = 0; k < KP; ++k) {
         tts[k] = mm(Gt[ir][k], eye, zero);
-        if (vec4) {
-          put16(tts[k], ir, true, k, false);
-          put16(Gt[ir][k], k, false, ir, true);
-        } else {
-          put(Gt[ir][k], ir, true, k, false, 0);
-          put(tts[k], k, false, ir, true, 0);
-        }
+        put(Gt[ir][k], ir, true, k, false, 0);
+        put(tts[k], k, false, ir, true, 0);
         if (want_s0) acc = mm(tts[k], F[k], acc);
       }
       if (want_s0 && cs == 0) {
@@ -562,9 +530,6 @@ void sweep_rows_kernel(SweepArgs a) {
         if (jr == ir) {
           put(gg, ir, true, jr, true, 1);
           put(ggt, ir, true, jr, true, 2);
-        } else if (vec4) {
-          put16(ggt, ir, true, jr, true);
-          put16(gg, jr, true, ir, true);
         } else {
           put(gg, ir, true, jr, true, 0);
           put(ggt, jr, true, ir, true, 0);
