@@ -672,12 +672,19 @@ def main():
     args.slots = args.slots or C.default_slots
 
     rank, world, local = mdist.env_rank_world()
+    # rehearsal knobs (one-GPU box): MPCQP_BENCH_DEVICE pins every rank to one
+    # device, MPCQP_DIST_BACKEND=gloo replaces RCCL (which needs one GPU per rank)
+    local = int(os.environ.get("MPCQP_BENCH_DEVICE", local))
+    backend = os.environ.get("MPCQP_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     wl = C(args, dev, rank)
     S = args.slots
@@ -718,7 +725,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
-    elapsed = mdist.max_over_ranks(elapsed, dev)
+    elapsed = mdist.max_over_ranks(elapsed, dev if backend == "nccl" else torch.device("cpu"))
     value = world * args.batch * args.steps / elapsed
 
     # ---- correctness of what was timed: statuses + oracle spot check (rank 0)
