@@ -93,40 +93,120 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   T* Cs = sm + L.oC;
   T* X0s = sm + L.oX0;
   const bool need_aff = (a.f != nullptr) || (a.xbar != nullptr);
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
 
   // ---------------------------------------------------------------- stage in
+  // A, B, c of one instance are dense runs in HBM.  All loads of a chunk
+  // (UA + UB + UC per lane, clamped addresses, no branches) are issued before
+  // its LDS stores, so a chunk costs one HBM round trip; config 3 (N = 30,
+  // nx = 4) is one chunk.  Padding (nx < NX) is zeroed first and the data
+  // scattered over it (LDS ops of one wave complete in order).
   {
     const T* Ab = a.A + (int64_t)b * a.sA;
-    for (int e = lane; e < S * NX * NX; e += kWave) {
-      const int s = e / (NX * NX), r = (e / NX) % NX, q = e % NX;
-      As[e] = (r < nx && q < nx) ? Ab[(int64_t)s * nx * nx + r * nx + q] : T(0);
-    }
     const T* Bb = a.B + (int64_t)b * a.sB;
-    for (int e = lane; e < S * NX * nu; e += kWave) {
-      const int s = e / (NX * nu), rem = e - s * NX * nu, r = rem / nu, q = rem - r * nu;
-      Bs[e] = (r < nx) ? Bb[(int64_t)s * nx * nu + r * nu + q] : T(0);
-    }
+    const T* Cb = (need_aff && a.c) ? a.c + (int64_t)b * a.sC : nullptr;
     const T* Qb = a.Q + (int64_t)b * a.sQ;
     const T* Qfb = a.Qf + (int64_t)b * a.sQf;
-    for (int e = lane; e < NX * NX; e += kWave) {
-      const int r = e / NX, q = e % NX;
-      const bool in = r < nx && q < nx;
-      Qs[e] = in ? Qb[r * nx + q] : T(0);
-      Qfs[e] = in ? Qfb[r * nx + q] : T(0);
-    }
     const T* Rb = a.R + (int64_t)b * a.sR;
-    for (int e = lane; e < nu * nu; e += kWave) Rs[e] = Rb[e];
-    if (need_aff) {
-      const T* Cb = a.c ? a.c + (int64_t)b * a.sC : nullptr;
-      for (int e = lane; e < N * NX; e += kWave) {
-        const int k = e / NX, q = e % NX;
-        Cs[e] = (Cb && q < nx) ? Cb[k * nx + q] : T(0);
-      }
-      const T* X0b = a.x0 ? a.x0 + (int64_t)b * a.sX0 : nullptr;
-      if (lane < NX) X0s[lane] = (X0b && lane < nx) ? X0b[lane] : T(0);
+    const T* X0b = (need_aff && a.x0) ? a.x0 + (int64_t)b * a.sX0 : nullptr;
+    const int cA = S * nx * nx, cB = S * nx * nu, cC = Cb ? N * nx : 0, cR = nu * nu;
+    // small operands: Q, Qf (QK padded entries per lane), R (<= 4 per lane), x0
+    constexpr int QK = (NX * NX + kWave - 1) / kWave;
+    T qv[QK], qfv[QK];
+    bool qin[QK];
+#pragma unroll
+    for (int k = 0; k < QK; ++k) {
+      const int e = k * kWave + lane, qr = e / NX, qq = e % NX;
+      qin[k] = e < NX * NX && qr < nx && qq < nx;
+      const int qo = qin[k] ? qr * nx + qq : 0;
+      qv[k] = Qb[qo];
+      qfv[k] = Qfb[qo];
     }
+    T rv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = k * kWave + lane;
+      rv[k] = Rb[e < cR ? e : 0];
+    }
+    const T x0v = X0b ? X0b[lane < nx ? lane : 0] : T(0);
+    const bool pad = nx < NX;
+    if (pad) {
+      for (int e = lane; e < S * NX * NX; e += kWave) As[e] = T(0);
+      for (int e = lane; e < S * NX * nu; e += kWave) Bs[e] = T(0);
+    }
+    if (need_aff && (pad || !Cb))
+      for (int e = lane; e < N * NX; e += kWave) Cs[e] = T(0);
+    // e / d for e < 2^24 from a float estimate, corrected to exact
+    auto qdiv = [](int e, int d, float rd) {
+      int s = (int)((float)e * rd);
+      s -= (s * d > e) ? 1 : 0;
+      s += ((s + 1) * d <= e) ? 1 : 0;
+      return s;
+    };
+    const float rA = 1.f / (float)(nx * nx), rB = 1.f / (float)(nx * nu), rN = 1.f / (float)nx;
+    constexpr int UA = 8, UB = 4, UC = 2;
+    auto chunk = [&](int c) {
+      T va[UA], vb[UB], vc[UC];
+#pragma unroll
+      for (int k = 0; k < UA; ++k) {
+        const int e = (c * UA + k) * kWave + lane;
+        va[k] = Ab[e < cA ? e : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < UB; ++k) {
+        const int e = (c * UB + k) * kWave + lane;
+        vb[k] = Bb[e < cB ? e : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < UC; ++k) {
+        const int e = (c * UC + k) * kWave + lane;
+        vc[k] = (e < cC) ? Cb[e] : T(0);
+      }
+#pragma unroll
+      for (int k = 0; k < UA; ++k) {
+        const int e = (c * UA + k) * kWave + lane;
+        if (e < cA) {
+          int o = e;
+          if (pad) {
+            const int s = qdiv(e, nx * nx, rA), rem = e - s * nx * nx;
+            const int r = qdiv(rem, nx, rN);
+            o = s * NX * NX + r * NX + (rem - r * nx);
+          }
+          As[o] = va[k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < UB; ++k) {
+        const int e = (c * UB + k) * kWave + lane;
+        if (e < cB) Bs[pad ? e + qdiv(e, nx * nu, rB) * (NX - nx) * nu : e] = vb[k];
+      }
+#pragma unroll
+      for (int k = 0; k < UC; ++k) {
+        const int e = (c * UC + k) * kWave + lane;
+        if (e < cC) Cs[pad ? e + qdiv(e, nx, rN) * (NX - nx) : e] = vc[k];
+      }
+    };
+    // chunk 0 outside the loop: its loads share the round trip of the small
+    // operands above (a loop header would wait for those first)
+    chunk(0);
+    for (int c = 1; c * kWave * UA < cA || c * kWave * UB < cB || c * kWave * UC < cC; ++c) chunk(c);
+#pragma unroll
+    for (int k = 0; k < QK; ++k) {
+      const int e = k * kWave + lane;
+      if (e < NX * NX) {
+        Qs[e] = qin[k] ? qv[k] : T(0);
+        Qfs[e] = qin[k] ? qfv[k] : T(0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k * kWave + lane < cR) Rs[k * kWave + lane] = rv[k];
+    if (need_aff && lane < NX) X0s[lane] = lane < nx ? x0v : T(0);
   }
   __syncthreads();
+  MPCQP_PHASE(0);
 
   // ------------------------------------------------------------ recursions
   if constexpr (NX <= MPCQP_CONDENSE_REG_NX) {
@@ -252,6 +332,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
     }
   }
   __syncthreads();
+  MPCQP_PHASE(1);
   // adjoint y_N = Qf xbar_N, y_k = Q xbar_k + A_k' y_{k+1}  (f = B_k' y_{k+1}).
   // Summing f along the columns instead (f_col = sum_k s_k' Q xbar_k) removes
   // this chain but loses ~10x accuracy in fp32 (cancellation), so it stays.
@@ -276,6 +357,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
       __syncthreads();
     }
   }
+  MPCQP_PHASE(2);
 
   // ------------------------------------------------------- column sweep
   // z columns (H, Gam), then -- only when F or Phi is requested -- the x0
@@ -351,6 +433,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
     }
   }
 
+  MPCQP_PHASE(3);
   // ------------------------------------------------- linear term and xbar
   if (a.f) {
     T* fb = a.f + (int64_t)b * n;
@@ -370,6 +453,10 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
       xb[e] = Xs[(k + 1) * NX + q];
     }
   }
+  MPCQP_PHASE(4);
+#ifdef MPCQP_PHASE_TIMING
+  mpcqp_clk.flush();
+#endif
 }
 
 template <typename T, int NX>
