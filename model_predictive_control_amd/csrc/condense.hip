@@ -47,28 +47,59 @@ struct CondenseArgs {
   const T* c; int64_t sC;
   const T* x0; int64_t sX0;
   T* H; T* F; T* f; T* Gam; T* Phi; T* xbar;
+  int rh, rg;  // output rings (elements, powers of two) of the streamed sweep; rh = 0: direct stores
 };
 
 struct CLayout {
-  int oA, oB, oQ, oQf, oR, oW, oT, oX, oY, oC, oX0, total;
+  int oA, oB, oQ, oQf, oR, oW, oT, oX, oY, oC, oX0, oWh, oRH, oRG, total;
 };
 
-__host__ __device__ inline CLayout clayout(int NX, int nu, int N, int tv) {
+// Streamed sweep (rh > 0): A, R and What_k = B_k' W_{k+1} persist; everything
+// else is dead once What, f and xbar are out, and the two output rings
+// overlay it.
+__host__ __device__ inline CLayout clayout(int NX, int nu, int N, int tv, int rh, int rg) {
   CLayout L;
   const int S = tv ? N : 1;
+  auto al4 = [](int o) { return (o + 3) & ~3; };  // 16-byte ring / vector alignment
   L.oA = 0;
-  L.oB = L.oA + S * NX * NX;
+  int o = S * NX * NX;
+  L.oWh = L.oRH = L.oRG = 0;
+  if (rh) {
+    L.oR = o;
+    o = al4(o + nu * nu);
+    L.oWh = o;                         // What_k, k = 0..N-1 (nu x NX each)
+    o = al4(o + N * nu * NX);
+  }
+  const int u = o;
+  L.oB = o;
   L.oQ = L.oB + S * NX * nu;
   L.oQf = L.oQ + NX * NX;
-  L.oR = L.oQf + NX * NX;
-  L.oW = L.oR + nu * nu;               // W_k, k = 0..N  ((N+1) slots; slot 0 unused)
+  o = L.oQf + NX * NX;
+  if (!rh) {
+    L.oR = o;
+    o += nu * nu;
+  }
+  L.oW = o;                            // W_k, k = 0..N  ((N+1) slots; slot 0 unused)
   L.oT = L.oW + (N + 1) * NX * NX;     // scratch NX x NX
   L.oX = L.oT + NX * NX;               // xbar_k, k = 0..N
   L.oY = L.oX + (N + 1) * NX;          // y_k, k = 0..N
   L.oC = L.oY + (N + 1) * NX;          // drift c_k, k = 0..N-1
   L.oX0 = L.oC + N * NX;               // x0
   L.total = L.oX0 + NX;
+  if (rh) {
+    L.oRH = u;
+    L.oRG = u + rh;
+    if (u + rh + rg > L.total) L.total = u + rh + rg;
+  }
   return L;
+}
+
+// e / d for 0 <= e < 2^24 from a float estimate, corrected to exact
+__device__ __forceinline__ int qdiv(int e, int d, float rd) {
+  int s = (int)((float)e * rd);
+  s -= (s * d > e) ? 1 : 0;
+  s += ((s + 1) * d <= e) ? 1 : 0;
+  return s;
 }
 
 template <typename T, int NX>
@@ -80,7 +111,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   const int nx = a.nx, nu = a.nu, N = a.N, n = N * nu;
   const int tv = a.tv;
   const int S = tv ? N : 1;
-  const CLayout L = clayout(NX, nu, N, tv);
+  const CLayout L = clayout(NX, nu, N, tv, a.rh, a.rg);
   T* As = sm + L.oA;
   T* Bs = sm + L.oB;
   T* Qs = sm + L.oQ;
@@ -138,13 +169,6 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
     }
     if (need_aff && (pad || !Cb))
       for (int e = lane; e < N * NX; e += kWave) Cs[e] = T(0);
-    // e / d for e < 2^24 from a float estimate, corrected to exact
-    auto qdiv = [](int e, int d, float rd) {
-      int s = (int)((float)e * rd);
-      s -= (s * d > e) ? 1 : 0;
-      s += ((s + 1) * d <= e) ? 1 : 0;
-      return s;
-    };
     const float rA = 1.f / (float)(nx * nx), rB = 1.f / (float)(nx * nu), rN = 1.f / (float)nx;
     constexpr int UA = 8, UB = 4, UC = 2;
     auto chunk = [&](int c) {
@@ -359,6 +383,29 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   }
   MPCQP_PHASE(2);
 
+  // ------------------------------------------------- linear term and xbar
+  if (a.f) {
+    T* fb = a.f + (int64_t)b * n;
+    const float rNu = 1.f / (float)nu;
+    for (int r = lane; r < n; r += kWave) {
+      const int i = qdiv(r, nu, rNu), aa = r - i * nu;
+      const T* Bi = Bs + (tv ? i : 0) * NX * nu;
+      T acc = T(0);
+#pragma unroll
+      for (int q = 0; q < NX; ++q) acc = fma(Bi[q * nu + aa], Ys[(i + 1) * NX + q], acc);
+      fb[r] = acc;
+    }
+  }
+  if (a.xbar) {
+    T* xb = a.xbar + (int64_t)b * N * nx;
+    const float rN = 1.f / (float)nx;
+    for (int e = lane; e < N * nx; e += kWave) {
+      const int k = qdiv(e, nx, rN), q = e - k * nx;
+      xb[e] = Xs[(k + 1) * NX + q];
+    }
+  }
+  MPCQP_PHASE(3);
+
   // ------------------------------------------------------- column sweep
   // z columns (H, Gam), then -- only when F or Phi is requested -- the x0
   // columns
@@ -367,7 +414,117 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   T* Fb = a.F ? a.F + (int64_t)b * n * nx : nullptr;
   T* Gb = a.Gam ? a.Gam + (int64_t)b * ((int64_t)N * nx * n) : nullptr;
   T* Pb = a.Phi ? a.Phi + (int64_t)b * ((int64_t)N * nx * nx) : nullptr;
-  for (int col0 = 0; col0 < ncol; col0 += kWave) {
+  if (a.rh) {
+    // Streamed sweep (ncol <= 64, one column per lane).  H row block i is
+    // What_i s_{i+1} (nu x NX FMAs instead of W s then B' v), and both H
+    // (packed rows, in order) and Gamma (block row i = rows i*nx..) are one
+    // contiguous stream per instance in stage order: lanes scatter their
+    // entries into an LDS ring, and every complete CH-element window leaves as
+    // one 16-byte-per-lane store (a quarter of the store instructions of
+    // per-row 4-byte stores, which bound the direct sweep).
+    T* Whs = sm + L.oWh;
+    {
+      const int cnt = N * nu * NX;
+      const float rW = 1.f / (float)(nu * NX);
+      for (int e = lane; e < cnt; e += kWave) {
+        const int k = qdiv(e, nu * NX, rW), rem = e - k * nu * NX;
+        const int aa = rem / NX, q = rem % NX;
+        const T* Bk = Bs + (tv ? k : 0) * NX * nu;
+        const T* W1 = Ws + (k + 1) * NX * NX;
+        T acc = T(0);
+#pragma unroll
+        for (int p = 0; p < NX; ++p) acc = fma(Bk[p * nu + aa], W1[p * NX + q], acc);
+        Whs[e] = acc;
+      }
+    }
+    const int col = lane;
+    const bool act = col < ncol;
+    const bool isz = col < n;
+    const int j = isz ? col / nu : -1;
+    const int bc = isz ? col - j * nu : col - n;
+    T bcol[NX];  // B_j e_bc, injected at stage j
+#pragma unroll
+    for (int q = 0; q < NX; ++q) bcol[q] = isz ? Bs[(tv ? j : 0) * NX * nu + q * nu + bc] : T(0);
+    __syncthreads();  // What visible; B, W, X, Y dead: the rings take over
+    constexpr int VEC = 16 / (int)sizeof(T);
+    constexpr int CH = kWave * VEC;
+    typedef T VT __attribute__((ext_vector_type(VEC)));
+    T* RH = sm + L.oRH;
+    T* RG = sm + L.oRG;
+    const int RHM = a.rh - 1, RGM = a.rg - 1;
+    // ring position p <-> element g0 + p, g0 = VEC-aligned, d = offset of the stream
+    const int dh = (int)(((uintptr_t)Hb / sizeof(T)) % VEC);
+    const int dg = Gb ? (int)(((uintptr_t)Gb / sizeof(T)) % VEC) : 0;
+    T* Hal = Hb - dh;
+    T* Gal = Gb ? Gb - dg : nullptr;
+    const int hiH = dh + n * (n + 1) / 2, hiG = dg + N * nx * n;
+    auto flush = [&](const T* ring, int rmask, T* gal, int w, int lo, int hi) {
+      const int p0 = w + lane * VEC;
+      if (p0 < hi && p0 + VEC > lo) {
+        const VT v = *reinterpret_cast<const VT*>(ring + (p0 & rmask));
+        if (p0 >= lo && p0 + VEC <= hi) {
+          __builtin_nontemporal_store(v, reinterpret_cast<VT*>(gal + p0));
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e)
+            if (p0 + e >= lo && p0 + e < hi) gal[p0 + e] = v[e];
+        }
+      }
+    };
+    T s[NX];
+#pragma unroll
+    for (int q = 0; q < NX; ++q) s[q] = (!isz && q == bc) ? T(1) : T(0);
+    int fh = 0, fg = 0;  // flushed ring positions (multiples of CH)
+    for (int i = 0; i < N; ++i) {
+      const T* Ai = As + (tv ? i : 0) * NX * NX;
+      const T* Wh = Whs + i * nu * NX;
+      const bool inj = isz && (i == j);
+      T t[NX];
+#pragma unroll
+      for (int r = 0; r < NX; ++r) {
+        T acc = T(0);
+#pragma unroll
+        for (int q = 0; q < NX; ++q) acc = fma(Ai[r * NX + q], s[q], acc);
+        t[r] = acc;
+      }
+#pragma unroll
+      for (int q = 0; q < NX; ++q) s[q] = inj ? bcol[q] : t[q];
+      if (Gb && isz) {
+#pragma unroll
+        for (int q = 0; q < NX; ++q)
+          if (q < nx) RG[(dg + (i * nx + q) * n + col) & RGM] = s[q];
+      }
+      if (act && !isz && Pb) {
+#pragma unroll
+        for (int q = 0; q < NX; ++q)
+          if (q < nx) Pb[(i * nx + q) * nx + bc] = s[q];
+      }
+      for (int aa = 0; aa < nu; ++aa) {
+        T o = inj ? Rs[aa * nu + bc] : T(0);
+#pragma unroll
+        for (int q = 0; q < NX; ++q) o = fma(Wh[aa * NX + q], s[q], o);
+        const int r = i * nu + aa;
+        if (isz) {
+          if (col <= r) RH[(dh + r * (r + 1) / 2 + col) & RHM] = o;
+        } else if (act && Fb) {
+          Fb[r * nx + bc] = o;
+        }
+      }
+      const int rr = (i + 1) * nu;
+      const int ph = dh + rr * (rr + 1) / 2, pg = Gb ? dg + (i + 1) * nx * n : 0;
+      if (ph - fh >= CH || pg - fg >= CH) {
+        __syncthreads();
+        for (; ph - fh >= CH; fh += CH) flush(RH, RHM, Hal, fh, dh, hiH);
+        for (; pg - fg >= CH; fg += CH) flush(RG, RGM, Gal, fg, dg, hiG);
+        asm volatile("" ::: "memory");
+      }
+    }
+    __syncthreads();
+    for (; fh < hiH; fh += CH) flush(RH, RHM, Hal, fh, dh, hiH);
+    if (Gb)
+      for (; fg < hiG; fg += CH) flush(RG, RGM, Gal, fg, dg, hiG);
+  }
+  for (int col0 = 0; col0 < (a.rh ? 0 : ncol); col0 += kWave) {
     const int col = col0 + lane;
     const bool act = col < ncol;
     const bool isz = col < n;
@@ -432,27 +589,6 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
       }
     }
   }
-
-  MPCQP_PHASE(3);
-  // ------------------------------------------------- linear term and xbar
-  if (a.f) {
-    T* fb = a.f + (int64_t)b * n;
-    for (int r = lane; r < n; r += kWave) {
-      const int i = r / nu, aa = r - i * nu;
-      const T* Bi = Bs + (tv ? i : 0) * NX * nu;
-      T acc = T(0);
-#pragma unroll
-      for (int q = 0; q < NX; ++q) acc = fma(Bi[q * nu + aa], Ys[(i + 1) * NX + q], acc);
-      fb[r] = acc;
-    }
-  }
-  if (a.xbar) {
-    T* xb = a.xbar + (int64_t)b * N * nx;
-    for (int e = lane; e < N * nx; e += kWave) {
-      const int k = e / nx, q = e - k * nx;
-      xb[e] = Xs[(k + 1) * NX + q];
-    }
-  }
   MPCQP_PHASE(4);
 #ifdef MPCQP_PHASE_TIMING
   mpcqp_clk.flush();
@@ -460,8 +596,26 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
 }
 
 template <typename T, int NX>
-static int launch_condense(const CondenseArgs<T>& a, hipStream_t st) {
-  const CLayout L = clayout(NX, a.nu, a.N, a.tv);
+static int launch_condense(CondenseArgs<T> a, hipStream_t st) {
+  // streamed sweep when every column fits one wavefront (MPCQP_CONDENSE_RING=0: direct stores)
+  static const int ring_on = [] {
+    const char* e = getenv("MPCQP_CONDENSE_RING");
+    return e ? atoi(e) : 1;
+  }();
+  const int n = a.N * a.nu, ncol = n + ((a.F || a.Phi) ? a.nx : 0);
+  a.rh = a.rg = 0;
+  if (ring_on && ncol <= kWave) {
+    constexpr int VEC = 16 / (int)sizeof(T), CH = kWave * VEC;
+    auto pow2 = [](int v) {
+      int p = 1;
+      while (p < v) p <<= 1;
+      return p;
+    };
+    a.rh = pow2(CH + a.nu * n + VEC);
+    a.rg = a.Gam ? pow2(CH + a.nx * n + VEC) : 0;
+    if ((size_t)clayout(NX, a.nu, a.N, a.tv, a.rh, a.rg).total * sizeof(T) > 160 * 1024) a.rh = a.rg = 0;
+  }
+  const CLayout L = clayout(NX, a.nu, a.N, a.tv, a.rh, a.rg);
   const size_t bytes = (size_t)L.total * sizeof(T);
   if (bytes > 160 * 1024) {
     set_error("mpcqp_condense: per-instance LDS footprint %zu B exceeds 160 KiB (N too large)", bytes);

@@ -157,3 +157,36 @@ def test_condense_fp32_mfma_all_outputs(dev, nx, nu, N, tv):
            for b in range(batch)]
     out = {k: v.double() for k, v in out.items()}
     _check(out, ref, N * nu, 2e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("off", [1, 2, 3])
+def test_condense_streamed_outputs_misaligned(dev, dt, off):
+    """The streamed sweep (n <= 64) writes H and Gamma as 16-byte vectors from an LDS ring,
+    with the stream start aligned down; outputs placed `off` elements past a 16-byte boundary
+    must come out identical to aligned ones, and nothing outside them may be written."""
+    rng = np.random.default_rng(31 + off)
+    nx, nu, N, batch = 4, 2, 30, 7
+    A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, True, batch)
+    x0 = rng.normal(size=(batch, nx))
+    c = rng.normal(size=(batch, N, nx))
+    args = (_t(A, dev, dt), _t(B, dev, dt), _t(Q, dev, dt), _t(R, dev, dt), _t(Qf, dev, dt), N)
+    kw = dict(x0=_t(x0, dev, dt), c=_t(c, dev, dt), tv=True, outputs=("H", "f", "Gam", "xbar"))
+    ref = batched.condense(*args, **kw)
+    n = N * nu
+    shapes = {"H": (batch, n * (n + 1) // 2), "f": (batch, n), "Gam": (batch, N * nx, n),
+              "xbar": (batch, N, nx)}
+    bufs, out = {}, {}
+    for k, shp in shapes.items():
+        numel = int(np.prod(shp))
+        bufs[k] = torch.full((numel + off + 8,), 7.0, dtype=dt, device=dev)
+        out[k] = bufs[k][off:off + numel].view(shp)
+    got = batched.condense(*args, **kw, out=out)
+    torch.cuda.synchronize()
+    for k in shapes:
+        assert torch.equal(got[k].reshape(-1), ref[k].reshape(-1)), k
+        assert bool((bufs[k][:off] == 7.0).all()) and bool((bufs[k][off + got[k].numel():] == 7.0).all()), k
+    o = oc.condense(A[0], B[0], Q, R, Qf, N, x0=x0[0], c=c[0])
+    Hd = batched.unpack_lower(got["H"].double(), n).cpu().numpy()[0]
+    tol = 1e-10 if dt == torch.float64 else 2e-5
+    assert np.abs(Hd - o["H"]).max() <= tol * max(1.0, np.abs(o["H"]).max())

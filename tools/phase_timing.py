@@ -70,7 +70,7 @@ elif cfg == 33:
     # condense_kernel<float, 4> of config 3 (all four outputs of mpc_qp)
     reader = lib.mpcqp_debug_phase_cycles_condense
     reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    PHASES = ["stage-in", "W + xbar recursion", "adjoint y", "column sweep (H, Gam)", "f, xbar", "", "", ""]
+    PHASES = ["stage-in", "W + xbar recursion", "adjoint y", "f, xbar out", "What + column sweep", "", "", ""]
     a = A(); a.batch = 65536; a.slots = 1; a.horizon = 0; a.reps = 1; a.check = 0
     w = bench.Config3(a, torch.device("cuda"), 0)
     run = lambda: batched.condense(w.A[0], w.B[0], w.Q_t, w.R_t, w.QN_t, w.N, x0=w.X0_t[0],  # noqa: E731
