@@ -321,6 +321,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
 void sweep_rows_kernel(SweepArgs a) {
   constexpr int TRM = 12 - KP;  // row tiles held at most (np + m <= 192)
   constexpr int NZ = KP * (KP + 1) / 2;
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
   const int b = blockIdx.x;
   const int l = threadIdx.x, g = l >> 4, c = l & 15;
   const int n = a.n, m = a.m, np = a.np, nt = n + m;
@@ -331,66 +334,68 @@ void sweep_rows_kernel(SweepArgs a) {
   const rsrc_t rG = mk_rsrc(Gb, (int64_t)m * n * 4);
   mf4 Z[NZ], Gt[TRM][KP];
   bool nonfin = false;
-  // G into LDS: every load of a 16-register batch issued before its stores
+  // The zz tiles (packed H, mirrored on the diagonal tiles, unit pad pivots)
+  // and the G z tiles (G[rho][z], rho = 16 ir + 4g + i, z = 16 k + c) come
+  // straight from HBM, every load issued before the first use (one round
+  // trip); G is then kept in LDS (zero-padded to 16 tr x ldg, ldg = 16 KP +
+  // 4 so that the float4 reads of the M_GG phase are bank-conflict free) for
+  // the G' operands at the end.
   extern __shared__ float Gs[];
-  {
-    const int cnt = m * n;
-    for (int e0 = 0; e0 < cnt; e0 += 16 * kWave) {
-      float t[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int e = e0 + l + kWave * k;
-        t[k] = bld(rG, e < cnt ? 4 * e : kOOB);
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int e = e0 + l + kWave * k;
-        if (e < cnt) Gs[e] = t[k];
-      }
-    }
-    __syncthreads();
-  }
-  // zz: packed H, mirrored on the diagonal tiles, unit pad pivots
+  const int ldg = 16 * KP + 4;
 #pragma unroll
   for (int ti = 0; ti < KP; ++ti)
 #pragma unroll
-    for (int tj = 0; tj <= ti; ++tj) {
+    for (int tj = 0; tj <= ti; ++tj)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 16 * ti + 4 * g + i, cc = 16 * tj + c;
         const int hi = r > cc ? r : cc, lo = r > cc ? cc : r;
-        const float v = bld(rH, hi < n ? 4 * (hi * (hi + 1) / 2 + lo) : kOOB) +
-                        ((r == cc && r >= n) ? 1.f : 0.f);
-        nonfin |= !finite(v);
-        Z[tri(ti, tj)][i] = v;
+        Z[tri(ti, tj)][i] = bld(rH, hi < n ? 4 * (hi * (hi + 1) / 2 + lo) : kOOB);
       }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  // G z: G[rho][z], rho = 16 ir + 4g + i, z = 16 k + c
 #pragma unroll
   for (int ir = 0; ir < TRM; ++ir)
 #pragma unroll
-    for (int k = 0; k < KP; ++k) {
+    for (int k = 0; k < KP; ++k)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int rho = 16 * ir + 4 * g + i, z = 16 * k + c;
-        const float v = (rho < m && z < n) ? Gs[rho * n + z] : 0.f;
-        nonfin |= !finite(v);
-        Gt[ir][k][i] = v;
+        Gt[ir][k][i] = bld(rG, (ir < tr && rho < m && z < n) ? 4 * (rho * n + z) : kOOB);
       }
-      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int ti = 0; ti < KP; ++ti)
+#pragma unroll
+    for (int tj = 0; tj <= ti; ++tj)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * ti + 4 * g + i, cc = 16 * tj + c;
+        nonfin |= !finite(Z[tri(ti, tj)][i]);
+        Z[tri(ti, tj)][i] += (r == cc && r >= n) ? 1.f : 0.f;
+      }
+#pragma unroll
+  for (int ir = 0; ir < TRM; ++ir) {
+    if (ir < tr) {  // uniform
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          nonfin |= !finite(Gt[ir][k][i]);
+          Gs[(16 * ir + 4 * g + i) * ldg + 16 * k + c] = Gt[ir][k][i];
+        }
     }
+  }
   bool bad = false;
   mf4 eye;
 #pragma unroll
   for (int i = 0; i < 4; ++i) eye[i] = (4 * g + i == c) ? 1.f : 0.f;
   const mf4 zero = {0.f, 0.f, 0.f, 0.f};
+  MPCQP_PHASE(0);
 
 #pragma unroll
   for (int k = 0; k < KP; ++k) {
     mf4 li = eye;
     chol_inv16(Z[tri(k, k)], li, g, c, bad);  // L^-1
     __builtin_amdgcn_sched_barrier(0);
+    MPCQP_PHASE(1);
     const mf4 lit = mm(li, eye, zero);
     mf4 Wz[KP];
 #pragma unroll
@@ -409,6 +414,7 @@ void sweep_rows_kernel(SweepArgs a) {
         if (i != k) Z[tri(i, j)] = mm(Wz[i], wn, Z[tri(i, j)]);
     }
     __builtin_amdgcn_sched_barrier(0);
+    MPCQP_PHASE(2);
     // row tiles, one W at a time: M_rho,j -= W_rho' W_j, M_rho,k = W_rho' L^-1
 #pragma unroll
     for (int ir = 0; ir < TRM; ++ir) {
@@ -421,12 +427,15 @@ void sweep_rows_kernel(SweepArgs a) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    MPCQP_PHASE(3);
 #pragma unroll
     for (int i = 0; i < KP; ++i) {
       if (i < k) Z[tri(k, i)] = mm(li, Wz[i], zero);
       else if (i > k) Z[tri(i, k)] = mm(Wz[i], li, zero);
     }
     Z[tri(k, k)] = mm(li, -li, zero);
+    __builtin_amdgcn_sched_barrier(0);
+    MPCQP_PHASE(4);
   }
 
   const bool fin_bad = __builtin_amdgcn_ballot_w64(nonfin) != 0;
@@ -491,6 +500,7 @@ void sweep_rows_kernel(SweepArgs a) {
         }
     }
   }
+  MPCQP_PHASE(5);
   // G z tiles (and their transposes, the z-row block), the row part of s0,
   // then the row-row block -M_Gz G'
 #pragma unroll
@@ -513,18 +523,13 @@ void sweep_rows_kernel(SweepArgs a) {
         }
       }
       __builtin_amdgcn_sched_barrier(0);
-      for (int jr = 0; jr <= ir; ++jr) {
-        mf4 gg = zero;
-#pragma unroll
-        for (int k = 0; k < KP; ++k) {
-          mf4 gt;  // G(jr, k)' in C layout: lane (g, c) holds G[16 jr + c][16 k + 4g + e]
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int rho = 16 * jr + cs, z = 16 * k + 4 * gs + e;
-            gt[e] = (rho < m && z < n) ? Gs[rho * n + z] : 0.f;
-          }
-          gg = mm(tts[k], gt, gg);  // M_Gz(ir, k) G(jr, k)'
-        }
+      // G(jr, k)' in C layout: lane (g, c) holds G[16 jr + c][16 k + 4g + e],
+      // one float4 of the padded LDS copy (zero outside m x n)
+      auto gtile = [&](int jr, int k) __attribute__((always_inline)) {
+        const float4 v = *reinterpret_cast<const float4*>(&Gs[(16 * jr + cs) * ldg + 16 * k + 4 * gs]);
+        return mf4{v.x, v.y, v.z, v.w};
+      };
+      auto emit = [&](mf4 gg, int jr) __attribute__((always_inline)) {
         gg = -gg;
         const mf4 ggt = mm(gg, eye, zero);
         if (jr == ir) {
@@ -534,16 +539,39 @@ void sweep_rows_kernel(SweepArgs a) {
           put(gg, ir, true, jr, true, 0);
           put(ggt, jr, true, ir, true, 0);
         }
+      };
+      // two independent accumulation chains at a time (MFMA dependent
+      // latency, one wave per SIMD)
+      int jr = 0;
+      for (; jr + 1 <= ir; jr += 2) {
+        mf4 g0 = zero, g1 = zero;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+          g0 = mm(tts[k], gtile(jr, k), g0);  // M_Gz(ir, k) G(jr, k)'
+          g1 = mm(tts[k], gtile(jr + 1, k), g1);
+        }
+        emit(g0, jr);
+        emit(g1, jr + 1);
+      }
+      if (jr <= ir) {
+        mf4 g0 = zero;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) g0 = mm(tts[k], gtile(jr, k), g0);
+        emit(g0, jr);
       }
     }
   }
   if (l == 0)
     a.status[b] = fin_bad ? MPCQP_STATUS_NONFINITE : (piv_bad ? MPCQP_STATUS_NOT_CONVEX : 0);
+  MPCQP_PHASE(6);
+#ifdef MPCQP_PHASE_TIMING
+  mpcqp_clk.flush();
+#endif
 }
 
 template <int KP>
 static int launch_sweep_rows(const SweepArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)a.m * a.n * sizeof(float);  // G staged per wave
+  const size_t lds = (size_t)((a.m + 15) / 16 * 16) * (16 * KP + 4) * sizeof(float);  // G staged per wave
   hipLaunchKernelGGL((sweep_rows_kernel<KP>), dim3(a.batch), dim3(64), lds, st, a);
   MPCQP_CHECK_LAUNCH("sweep_rows_kernel");
   return MPCQP_OK;
@@ -618,3 +646,7 @@ extern "C" int mpcqp_sweep(int dtype, int batch, int n, int m, const void* H, in
   return sweep_launch(batch, n, m, H, strideH, G, strideG, M, full, status, (hipStream_t)stream,
                       nullptr, 0, nullptr);
 }
+
+#ifdef MPCQP_PHASE_TIMING
+MPCQP_DEBUG_PHASE_READER(mpcqp_debug_phase_cycles_sweep)
+#endif

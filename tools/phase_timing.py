@@ -66,6 +66,17 @@ elif cfg == 55:
     run = lambda: batched.condense(w.A[0], w.B[0], w.Q_t, w.R_t, w.Q_t, w.N, x0=w.X0_t[0],  # noqa: E731
                                    tv=True, outputs=("H", "f"))
     waves = a.batch * R
+elif cfg in (35, 36):
+    # sweep_rows_kernel of config 3 (35: one mpc_qp step; the sweep's clock only)
+    reader = lib.mpcqp_debug_phase_cycles_sweep
+    reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    PHASES = ["loads", "chol_inv16", "W + zz update", "row tiles", "M_kz, M_kk", "out: zz + s0",
+              "out: rows + M_GG", ""]
+    a = A(); a.batch = int(os.environ.get("PT_BATCH", 65536)); a.slots = 1; a.horizon = 0; a.reps = 1
+    a.check = 0
+    w = bench.CONFIGS[3](a, torch.device("cuda"), 0)
+    run = lambda: w.step(0)  # noqa: E731
+    waves = a.batch * R
 elif cfg == 33:
     # condense_kernel<float, 4> of config 3 (all four outputs of mpc_qp)
     reader = lib.mpcqp_debug_phase_cycles_condense
@@ -87,7 +98,8 @@ elif pf:
     if DYN:
         PHASES = ["active set (all)", "DYN: stage loads", "DYN: forward", "DYN: backward",
                   "DYN: residual tail", "correction (M0)", "re-scan", "output"]
-    a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1; a.check = 0
+    a = A(); a.batch = int(os.environ.get("PT_BATCH", 4096)); a.slots = 1; a.horizon = 0; a.reps = 1
+    a.check = 0
     w = bench.CONFIGS[cfg](a, torch.device("cuda"), 0)
     run = lambda: w.step(0)  # noqa: E731
     waves = a.batch * R
