@@ -35,6 +35,7 @@
 //     exactly (no fp32 rounding of the condensed H, Gam, xbar), so refinement
 //     converges past the fp32 condensing floor, and it costs O(N nx (nx+nu))
 //     instead of O((n+m)^2) reads.
+#include "mfma.hpp"
 #include "pf.hpp"
 
 // tools/phase_timing.py dyn3|dyn5 builds with MPCQP_PHASE_DYN: the phase
@@ -347,6 +348,9 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
   const int b = blockIdx.x, l = threadIdx.x;
   const int n = a.n, m = a.m, nt = n + m;
   const float* M0 = a.M0 + (int64_t)b * nt * nt;
+  // M0 rows through a range-checked descriptor: a masked lane (past nt, or an
+  // empty slot) loads 0 with no exec-mask branch around the load
+  const rsrc_t rM0 = mk_rsrc(M0, (int64_t)nt * nt * 4);
   const float* fb = a.f + (int64_t)b * a.sf;
   const float inf = Lim<float>::inf();
   const int pre = a.status[b];  // sweep status
@@ -446,11 +450,10 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
       float v[kB][NR];
 #pragma unroll
       for (int t = 0; t < kB; ++t) {
-        const float* rp = M0 + (int64_t)(row[t] < 0 ? 0 : row[t]) * nt;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
           const int i = l + kWave * r;
-          v[t][r] = (row[t] >= 0 && i < nt) ? rp[i] : 0.f;  // row -1: empty entry, no load
+          v[t][r] = bld(rM0, (row[t] >= 0 && i < nt) ? 4 * (row[t] * nt + i) : kOOB);  // row -1: empty
         }
       }
 #pragma unroll
@@ -511,11 +514,10 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
         for (int t = 0; t < kZB; ++t) {
           int j;
           take(j, c[t]);
-          const float* rp = M0 + (int64_t)(j < 0 ? 0 : j) * nt;
 #pragma unroll
           for (int r = 0; r < NR; ++r) {
             const int i = l + kWave * r;
-            v[t][r] = (j >= 0 && i < nt) ? rp[i] : 0.f;  // exhausted slots load nothing
+            v[t][r] = bld(rM0, (j >= 0 && i < nt) ? 4 * (j * nt + i) : kOOB);  // exhausted slots: 0
           }
         }
       };
@@ -546,11 +548,10 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
         for (int t = 0; t < kZB; ++t) {
           const int j = j0 + t < n ? j0 + t : 0;
           c[t] = j0 + t < n ? coef(j0 + t) : 0.f;
-          const float* rp = M0 + (int64_t)j * nt;
 #pragma unroll
           for (int r = 0; r < NR; ++r) {
             const int i = l + kWave * r;
-            v[t][r] = i < nt ? rp[i] : 0.f;
+            v[t][r] = bld(rM0, i < nt ? 4 * (j * nt + i) : kOOB);
           }
         }
       };
@@ -698,11 +699,10 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
           int j0[kB];
           uint64_t mrest = used;
           {
-            const float* row = M0 + (int64_t)p * nt;
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
               const int i = l + kWave * r;
-              col[r] = i < nt ? row[i] : 0.f;
+              col[r] = bld(rM0, i < nt ? 4 * (p * nt + i) : kOOB);
             }
 #pragma unroll
             for (int t = 0; t < kB; ++t) {
@@ -713,11 +713,10 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
                 mrest &= mrest - 1;
                 aj = readlane(aidx, j0[t]);
               }
-              const float* rp = M0 + (int64_t)aj * nt;
 #pragma unroll
               for (int r = 0; r < NR; ++r) {
                 const int i = l + kWave * r;
-                v0[t][r] = (j0[t] >= 0 && i < nt) ? rp[i] : 0.f;  // empty slots load nothing
+                v0[t][r] = bld(rM0, (j0[t] >= 0 && i < nt) ? 4 * (aj * nt + i) : kOOB);  // empty: 0
               }
             }
           }
