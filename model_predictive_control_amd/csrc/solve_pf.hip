@@ -394,6 +394,17 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
 #pragma unroll
   for (int j = 0; j < kSlots; ++j) S[j] = 0.f;
   uint64_t used = 0;
+  // Row cache: during the active set the refinement pool is free, and holds
+  // the M0 rows of the first ncache slots (written when a constraint joins,
+  // from the raw column p already in registers), so the per-iteration
+  // M0[:, P] v reads those from LDS instead of HBM.  cmask = cached slots;
+  // the refinement's residual reuses the pool and clears it.
+  // (measured: pays at config 3; with the wide-state DYN residual (NXP >= 8,
+  // config 5) the extra registers spill and it costs more than it saves)
+  constexpr bool kCache = NXP <= 4;
+  float* cache = reinterpret_cast<float*>(pool);
+  const int ncache = !kCache ? 0 : ((2 * kPool) / nt < 16 ? (2 * kPool) / nt : 16);
+  uint64_t cmask = 0;
 
   int code = MPCQP_STATUS_OPTIMAL, iters = 0;
   if (pre) {
@@ -463,7 +474,27 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
     };
     // out += sign * M0[:, P] q  (rows a_j of the symmetric M0); fixed_z_f:
     // coefficient -f_a on the fixed z instead (rows contribute nothing)
+    // cached slots: the row from LDS, no memory round trip
+    auto ccols = [&](float q, float (&out)[NR], float sign, bool fixed_z_f, uint64_t mm) {
+      if constexpr (!kCache) return;
+      while (mm) {
+        const int j = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        const int aj = readlane(aidx, j);
+        const float c = fixed_z_f ? (aj < n ? -fb[aj] : 0.f) : sign * readlane(q, j);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int i = l + kWave * r;
+          const float v = cache[j * nt + (i < nt ? i : 0)];
+          out[r] = fmaf(c, i < nt ? v : 0.f, out[r]);
+        }
+      }
+    };
     auto pcols = [&](float q, float (&out)[NR], float sign, bool fixed_z_f, uint64_t mm) {
+      if constexpr (kCache) {
+        ccols(q, out, sign, fixed_z_f, mm & cmask);
+        mm &= ~cmask;
+      }
       while (mm) {
         int row[kB];
         float c[kB];
@@ -695,14 +726,15 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
           // column p of the current M.  The first kB active rows of M0 are
           // loaded in the same memory round trip as column p (their indices
           // are known; only their coefficients v wait for the column)
-          float col[NR], v0[kB][NR];
+          float col[NR], v0[kB][NR], rawc[NR];
           int j0[kB];
-          uint64_t mrest = used;
+          uint64_t mrest = kCache ? used & ~cmask : used;
           {
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
               const int i = l + kWave * r;
               col[r] = bld(rM0, i < nt ? 4 * (p * nt + i) : kOOB);
+              if constexpr (kCache) rawc[r] = col[r];
             }
 #pragma unroll
             for (int t = 0; t < kB; ++t) {
@@ -730,6 +762,7 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
 #pragma unroll
             for (int r = 0; r < NR; ++r) col[r] = fmaf(c, v0[t][r], col[r]);
           }
+          if constexpr (kCache) ccols(v, col, 1.f, false, used & cmask);
           pcols(v, col, 1.f, false, mrest);
           MPCQP_PHASE_K(4);
 #pragma unroll
@@ -790,6 +823,7 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
             }
             s_drop(q, d);
             used &= ~(1ull << q);
+            cmask &= ~(1ull << q);
             if (l == q) aidx = -1;
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
@@ -811,6 +845,14 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
             const int snew = __builtin_ctzll(~used);
             s_add(v, snew, -mpp);
             used |= 1ull << snew;
+            if (kCache && snew < ncache) {
+#pragma unroll
+              for (int r = 0; r < NR; ++r) {
+                const int i = l + kWave * r;
+                if (i < nt) cache[snew * nt + i] = rawc[r];
+              }
+              cmask |= 1ull << snew;
+            }
             if (l == snew) {
               aidx = p;
               sbnd = tgt;
@@ -848,6 +890,7 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
     // DYN: the horizon's stage data stays in LDS across refinement steps
     // when it fits one chunk
     int dyn_loaded = -1;
+    cmask = 0;  // the residual below reuses the pool
     for (int it = 0; it < a.refine; ++it) {
       MPCQP_PHASE_D(0);
       float x[NR];
