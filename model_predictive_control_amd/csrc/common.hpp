@@ -96,36 +96,92 @@ __device__ __forceinline__ int readlane(int v, int lane) {
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ------------------------------------------------------ wave reductions
+// Cross-lane steps without LDS: quad_perm DPP (lane ^ 1, ^ 2), row_ror:4 and
+// row_ror:8 DPP (within a 16-lane row: after the quad steps every quad holds
+// its best, so rotating by 4 then 8 combines all four quads), and
+// v_permlane16_swap / v_permlane32_swap (lane ^ 16, ^ 32).  Every step is a
+// VALU op (ds_bpermute, what __shfl_xor compiles to, is an LDS round trip per
+// step); the result of a commutative reduction is the same in every lane.
+__device__ __forceinline__ unsigned lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+template <int X>
+__device__ __forceinline__ int lane_step(int v) {
+  if constexpr (X == 1) {
+    return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);
+  } else if constexpr (X == 2) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);
+  } else if constexpr (X == 4) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);
+  } else if constexpr (X == 8) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);
+  } else if constexpr (X == 16) {
+    const auto s = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)((lane_id() & 16) ? s[0] : s[1]);
+  } else {
+    static_assert(X == 32, "lane_step: 1, 2, 4, 8, 16 or 32");
+    const auto s = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)((lane_id() & 32) ? s[0] : s[1]);
+  }
+}
+template <int X>
+__device__ __forceinline__ float lane_step(float v) {
+  return __int_as_float(lane_step<X>(__float_as_int(v)));
+}
+template <int X>
+__device__ __forceinline__ double lane_step(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = lane_step<X>((int)(b & 0xffffffffll));
+  const int hi = lane_step<X>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // Arg-max over the wave: returns the largest value; ties resolve to the
 // smallest lane index.  Lanes that should not compete pass -inf.
+template <int X, typename T>
+__device__ __forceinline__ void argmax_step(T& v, int& idx) {
+  const T ov = lane_step<X>(v);
+  const int oi = lane_step<X>(idx);
+  const bool take = (ov > v) || (ov == v && oi < idx);
+  v = take ? ov : v;
+  idx = take ? oi : idx;
+}
+template <int X, typename T>
+__device__ __forceinline__ void argmin_step(T& v, int& idx) {
+  const T ov = lane_step<X>(v);
+  const int oi = lane_step<X>(idx);
+  const bool take = (ov < v) || (ov == v && oi < idx);
+  v = take ? ov : v;
+  idx = take ? oi : idx;
+}
 template <typename T>
 __device__ __forceinline__ void wave_argmax(T& v, int& idx) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const T ov = __shfl_xor(v, off, kWave);
-    const int oi = __shfl_xor(idx, off, kWave);
-    const bool take = (ov > v) || (ov == v && oi < idx);
-    v = take ? ov : v;
-    idx = take ? oi : idx;
-  }
+  argmax_step<1>(v, idx);
+  argmax_step<2>(v, idx);
+  argmax_step<4>(v, idx);
+  argmax_step<8>(v, idx);
+  argmax_step<16>(v, idx);
+  argmax_step<32>(v, idx);
 }
 
 template <typename T>
 __device__ __forceinline__ void wave_argmin(T& v, int& idx) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const T ov = __shfl_xor(v, off, kWave);
-    const int oi = __shfl_xor(idx, off, kWave);
-    const bool take = (ov < v) || (ov == v && oi < idx);
-    v = take ? ov : v;
-    idx = take ? oi : idx;
-  }
+  argmin_step<1>(v, idx);
+  argmin_step<2>(v, idx);
+  argmin_step<4>(v, idx);
+  argmin_step<8>(v, idx);
+  argmin_step<16>(v, idx);
+  argmin_step<32>(v, idx);
 }
 
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));
+  v = fmax(v, lane_step<1>(v));
+  v = fmax(v, lane_step<2>(v));
+  v = fmax(v, lane_step<4>(v));
+  v = fmax(v, lane_step<8>(v));
+  v = fmax(v, lane_step<16>(v));
+  v = fmax(v, lane_step<32>(v));
   return v;
 }
 
