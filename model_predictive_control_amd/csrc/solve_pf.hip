@@ -969,9 +969,9 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
               double sm = 0.0;
 #pragma unroll
               for (int t = 0; t < 8; ++t) sm += red[rr * kWave + qq * 8 + t];
-              sm += __shfl_xor(sm, 8, kWave);
-              sm += __shfl_xor(sm, 16, kWave);
-              sm += __shfl_xor(sm, 32, kWave);
+              sm += lane_step<8>(sm);  // row_ror:8 = lane ^ 8 inside a 16-lane row
+              sm += lane_step<16>(sm);
+              sm += lane_step<32>(sm);
               if (qq == 0 && g + rr < j1) rsum[g + rr] += sm;
             }
             wave_lds_sync();

@@ -11,6 +11,8 @@
 #pragma once
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace mpcqp {
 
 // ---------------------------------------------------------------- DPP
@@ -55,14 +57,8 @@ __device__ __forceinline__ void blocks_argmax(T& v, int& idx) {
     v = take ? ov : v;
     idx = take ? oi : idx;
   }
-#pragma unroll
-  for (int off = 16; off <= 32; off <<= 1) {
-    const T ov = __shfl_xor(v, off, kWave);
-    const int oi = __shfl_xor(idx, off, kWave);
-    const bool take = (ov > v) || (ov == v && oi < idx);
-    v = take ? ov : v;
-    idx = take ? oi : idx;
-  }
+  argmax_step<16>(v, idx);
+  argmax_step<32>(v, idx);
 }
 
 // Same with a payload value carried along with the winner.
@@ -77,16 +73,18 @@ __device__ __forceinline__ void blocks_argmax(T& v, int& idx, T& pay) {
     idx = take ? oi : idx;
     pay = take ? op : pay;
   }
-#pragma unroll
-  for (int off = 16; off <= 32; off <<= 1) {
-    const T ov = __shfl_xor(v, off, kWave);
-    const int oi = __shfl_xor(idx, off, kWave);
-    const T op = __shfl_xor(pay, off, kWave);
+  auto step = [&](auto x) __attribute__((always_inline)) {
+    constexpr int X = decltype(x)::value;
+    const T ov = lane_step<X>(v);
+    const int oi = lane_step<X>(idx);
+    const T op = lane_step<X>(pay);
     const bool take = (ov > v) || (ov == v && oi < idx);
     v = take ? ov : v;
     idx = take ? oi : idx;
     pay = take ? op : pay;
-  }
+  };
+  step(std::integral_constant<int, 16>{});
+  step(std::integral_constant<int, 32>{});
 }
 
 template <typename T>
@@ -98,14 +96,8 @@ __device__ __forceinline__ void blocks_argmin(T& v, int& idx) {
     v = take ? ov : v;
     idx = take ? oi : idx;
   }
-#pragma unroll
-  for (int off = 16; off <= 32; off <<= 1) {
-    const T ov = __shfl_xor(v, off, kWave);
-    const int oi = __shfl_xor(idx, off, kWave);
-    const bool take = (ov < v) || (ov == v && oi < idx);
-    v = take ? ov : v;
-    idx = take ? oi : idx;
-  }
+  argmin_step<16>(v, idx);
+  argmin_step<32>(v, idx);
 }
 
 // NOTE: no helper here indexes a register array with a runtime value --

@@ -56,9 +56,9 @@ __device__ __forceinline__ void rowg_argmax(T& v, int& idx, T& pay) {
   MPCQP_STEP(0x128)
 #undef MPCQP_STEP
   if constexpr (G == 32) {
-    const T ov = __shfl_xor(v, 16, kWave);
-    const int oi = __shfl_xor(idx, 16, kWave);
-    const T op = __shfl_xor(pay, 16, kWave);
+    const T ov = lane_step<16>(v);
+    const int oi = lane_step<16>(idx);
+    const T op = lane_step<16>(pay);
     const bool take = (ov > v) || (ov == v && oi < idx);
     v = take ? ov : v;
     idx = take ? oi : idx;
@@ -82,8 +82,8 @@ __device__ __forceinline__ void rowg_argmin(T& v, int& idx) {
   MPCQP_STEP(0x128)
 #undef MPCQP_STEP
   if constexpr (G == 32) {
-    const T ov = __shfl_xor(v, 16, kWave);
-    const int oi = __shfl_xor(idx, 16, kWave);
+    const T ov = lane_step<16>(v);
+    const int oi = lane_step<16>(idx);
     const bool take = (ov < v) || (ov == v && oi < idx);
     v = take ? ov : v;
     idx = take ? oi : idx;
