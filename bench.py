@@ -29,9 +29,10 @@ contract; they are parity/roofline cases and not the headline line:
      sweep + product-form active set, n = 160)
 
 In every config the inputs are resident in HBM before the timed region, and
-steps cycle over distinct x0 batches ("slots").  Each slot's step is captured
-once into a HIP graph (torch.cuda.CUDAGraph) and replayed; the kernels
-recompute everything on every replay.
+steps cycle over distinct x0 batches ("slots").  A round of S steps (slots
+0..S-1 in order) is captured once into a HIP graph (torch.cuda.CUDAGraph) and
+replayed K // S times, the remainder from one-step graphs (--no-chain: one
+graph launch per step); the kernels recompute everything on every replay.
 
 Per-kernel device times: HIP events around a graph of R back-to-back launches
 of that kernel alone, on the stream the graph runs on.
@@ -658,6 +659,8 @@ def main():
     ap.add_argument("--horizon", type=int, default=0, help="N (0 = config default)")
     ap.add_argument("--slots", type=int, default=0, help="distinct x0 batches cycled over")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-chain", action="store_true",
+                    help="replay one graph per step instead of one per round of slots")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--reps", type=int, default=20, help="launches per kernel-timing graph")
@@ -692,6 +695,7 @@ def main():
         wl.step(s)
     torch.cuda.synchronize()
     graphs = None
+    chain = None
     if not args.no_graph:
         try:
             graphs = []
@@ -701,10 +705,19 @@ def main():
                 with torch.cuda.graph(g, stream=cap):
                     wl.step(s)
                 graphs.append(g)
+            # one graph holding a whole round of S steps (slots 0..S-1 in
+            # order): the timed loop replays it K // S times, so consecutive
+            # steps are not separated by a graph launch each
+            if S > 1 and not args.no_chain:
+                chain = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(chain, stream=cap):
+                    for s in range(S):
+                        wl.step(s)
             torch.cuda.synchronize()
         except Exception as e:  # pragma: no cover - reported in the JSON
             print(f"graph capture failed ({e}); eager launches", file=sys.stderr)
             graphs = None
+            chain = None
 
     def run(k):
         if graphs is not None:
@@ -712,15 +725,25 @@ def main():
         else:
             wl.step(k % S)
 
-    for k in range(args.warmup):
-        run(k)
+    def run_steps(k0, count):
+        """Steps k0 .. k0+count-1 (slot k % S each), whole rounds through the chain graph."""
+        k = k0
+        end = k0 + count
+        while k < end:
+            if chain is not None and k % S == 0 and end - k >= S:
+                chain.replay()
+                k += S
+            else:
+                run(k)
+                k += 1
+
+    run_steps(0, args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        run(k)
+    run_steps(0, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -750,7 +773,8 @@ def main():
             cpu = wl.cpu_baseline(args.cpu_seconds)
         cfg = wl.workload()
         cfg.update({"batch_per_gpu": args.batch, "parallelism": f"dp{world}",
-                    "graph": graphs is not None, "config": args.config})
+                    "graph": graphs is not None, "graph_steps": S if chain is not None else 1,
+                    "config": args.config})
         out = {
             "metric": METRIC,
             "value": round(value, 1),
