@@ -231,16 +231,40 @@ __global__ __launch_bounds__(64, OCC) void mpc_group_kernel(MpcArgsQ<T> a) {
 
   int code = MPCQP_STATUS_OPTIMAL;
   MPCQP_PHASE(0);
-  // ------------------------------------- Riccati backward (all lanes, regs)
+  // -------------- Riccati backward + free response forward (all lanes, regs)
+  // The two recursions are independent serial chains; one loop runs Riccati
+  // stage N-1-t next to x-bar stage t so that their latencies overlap (at one
+  // wave per SIMD nothing else hides them).
   {
-    T P[NX][NX], Qr[NX][NX], Rr[NU][NU], Ar[NX][NX], Br[NX][NU];
+    T P[NX][NX], Qr[NX][NX], Rr[NU][NU], Ar[NX][NX], Br[NX][NU], Ax[NX][NX];
     load_sq<T, NX, NX>(Qfs, P, NX);
     load_sq<T, NX, NX>(Qs, Qr, NX);
     load_sq<T, NU, NU>(Rs, Rr, NU);
     load_sq<T, NX, NX>(As, Ar, NX);
     load_sq<T, NX, NU>(Bs, Br, NU);
+    load_sq<T, NX, NX>(As, Ax, NX);
+    T xk[NX];
+#pragma unroll
+    for (int qq = 0; qq < NX; ++qq) xk[qq] = X0s[qq];
     bool ok = true;
-    for (int k = N - 1; k >= 0; --k) {
+    for (int t = 0; t < N; ++t) {
+      {  // x-bar stage t: x_{t+1} = A_t x_t + c_t
+        if (tv) load_sq<T, NX, NX>(As + t * NX * NX, Ax, NX);
+        T xn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          T s = Cs[t * NX + i];
+#pragma unroll
+          for (int qq = 0; qq < NX; ++qq) s = fma(Ax[i][qq], xk[qq], s);
+          xn[i] = s;
+        }
+#pragma unroll
+        for (int qq = 0; qq < NX; ++qq) xk[qq] = xn[qq];
+        if (q == 0)
+#pragma unroll
+          for (int qq = 0; qq < NX; ++qq) Xs[(t + 1) * NX + qq] = xk[qq];
+      }
+      const int k = N - 1 - t;
       if (tv) {
         load_sq<T, NX, NX>(As + k * NX * NX, Ar, NX);
         load_sq<T, NX, NU>(Bs + k * NX * NU, Br, NU);
@@ -358,27 +382,8 @@ __global__ __launch_bounds__(64, OCC) void mpc_group_kernel(MpcArgsQ<T> a) {
     if (!ok) code = MPCQP_STATUS_NOT_CONVEX;
 
     MPCQP_PHASE(1);
-    // ---- free response xbar (forward) and adjoint y -> f (backward)
-    if (tv == 0) load_sq<T, NX, NX>(As, Ar, NX);
-    T xk[NX];
-#pragma unroll
-    for (int qq = 0; qq < NX; ++qq) xk[qq] = X0s[qq];
-    for (int k = 0; k < N; ++k) {
-      if (tv) load_sq<T, NX, NX>(As + k * NX * NX, Ar, NX);
-      T xn[NX];
-#pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        T s = Cs[k * NX + i];
-#pragma unroll
-        for (int qq = 0; qq < NX; ++qq) s = fma(Ar[i][qq], xk[qq], s);
-        xn[i] = s;
-      }
-#pragma unroll
-      for (int qq = 0; qq < NX; ++qq) xk[qq] = xn[qq];
-      if (q == 0)
-#pragma unroll
-        for (int qq = 0; qq < NX; ++qq) Xs[(k + 1) * NX + qq] = xk[qq];
-    }
+    // ---- adjoint y -> f (backward); x_k of the next stage is read from LDS
+    // one iteration ahead so the read overlaps this stage's FMA chain
     __syncthreads();
     T yk[NX];
 #pragma unroll
@@ -388,6 +393,9 @@ __global__ __launch_bounds__(64, OCC) void mpc_group_kernel(MpcArgsQ<T> a) {
       for (int qq = 0; qq < NX; ++qq) s = fma(Qfs[i * NX + qq], xk[qq], s);
       yk[i] = s;
     }
+    T xnext[NX];
+#pragma unroll
+    for (int qq = 0; qq < NX; ++qq) xnext[qq] = Xs[(N - 1) * NX + qq];
     for (int k = N - 1; k >= 0; --k) {
       // f_(k,u) = B_k[:,u]' y_{k+1}
       const T* Bk = Bs + (tv ? k : 0) * NX * NU;
@@ -400,13 +408,19 @@ __global__ __launch_bounds__(64, OCC) void mpc_group_kernel(MpcArgsQ<T> a) {
         }
       }
       if (k == 0) break;
+      T xc[NX];
+#pragma unroll
+      for (int qq = 0; qq < NX; ++qq) {
+        xc[qq] = xnext[qq];
+        xnext[qq] = Xs[(k > 1 ? k - 1 : 1) * NX + qq];
+      }
       if (tv) load_sq<T, NX, NX>(As + k * NX * NX, Ar, NX);
       T yn[NX];
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
         T s = T(0);
 #pragma unroll
-        for (int qq = 0; qq < NX; ++qq) s = fma(Qr[i][qq], Xs[k * NX + qq], s);
+        for (int qq = 0; qq < NX; ++qq) s = fma(Qr[i][qq], xc[qq], s);
 #pragma unroll
         for (int qq = 0; qq < NX; ++qq) s = fma(Ar[qq][i], yk[qq], s);
         yn[i] = s;

@@ -116,6 +116,14 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
     nonfinite |= v && !finite(s0[r]);
     badbox |= v && (!(li[r] <= ui[r]) || li[r] == Lim<T>::inf() || ui[r] == -Lim<T>::inf());
   }
+  // relative-violation scales 1/(1+|bound|), NaN for an infinite bound (a NaN
+  // violation never wins the arg-max): the per-iteration scan only multiplies
+  T sl[BS], su[BS];
+#pragma unroll
+  for (int r = 0; r < BS; ++r) {
+    sl[r] = finite(li[r]) ? T(1) / (T(1) + fabs(li[r])) : T(__builtin_nan(""));
+    su[r] = finite(ui[r]) ? T(1) / (T(1) + fabs(ui[r])) : T(__builtin_nan(""));
+  }
   publish<T, BS>(li, lis, W.bi, W.bj);
   publish<T, BS>(ui, uis, W.bi, W.bj);
   __syncthreads();
@@ -165,15 +173,12 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
       int p = 0;
 #pragma unroll
       for (int r = 0; r < BS; ++r) {
-        if (st[r] == 0) {
-          const T vl = finite(li[r]) ? (li[r] - si[r]) * fast_rcp(T(1) + fabs(li[r])) : -Lim<T>::inf();
-          const T vu = finite(ui[r]) ? (si[r] - ui[r]) * fast_rcp(T(1) + fabs(ui[r])) : -Lim<T>::inf();
-          const T vv = fmax(vl, vu);
-          if (vv > viol) {
-            viol = vv;
-            p = W.bi * BS + r;
-          }
-        }
+        const T vl = (li[r] - si[r]) * sl[r];
+        const T vu = (si[r] - ui[r]) * su[r];
+        const T vv = (st[r] == 0) ? fmax(vl, vu) : -Lim<T>::inf();
+        const bool take = vv > viol;
+        viol = take ? vv : viol;
+        p = take ? W.bi * BS + r : p;
       }
       blocks_argmax(viol, p);
       p = uniform(p);
@@ -203,13 +208,12 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
 #pragma unroll
         for (int r = 0; r < BS; ++r) {
           dy[r] = -c[r] * ysgn;
-          T t = Lim<T>::inf();
-          if (st[r] == 2 && dy[r] < T(0)) t = yi[r] / (-dy[r]);
-          if (st[r] == 1 && dy[r] > T(0)) t = (-yi[r]) / dy[r];
-          if (t < ti) {
-            ti = t;
-            k = W.bi * BS + r;
-          }
+          // an active row's multiplier moves toward 0: t = -y / dy (>= 0)
+          const bool cand = (st[r] == 2 && dy[r] < T(0)) || (st[r] == 1 && dy[r] > T(0));
+          const T t = cand ? -yi[r] * fast_rcp(dy[r]) : Lim<T>::inf();
+          const bool take = t < ti;
+          ti = take ? t : ti;
+          k = take ? W.bi * BS + r : k;
         }
         blocks_argmin(ti, k);
         k = uniform(k);

@@ -7,7 +7,7 @@ lane 0 of each wave adds s_memtime deltas per phase into a device array.
 """
 import ctypes, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CS = os.path.join(ROOT, "model_predictive_control_amd", "csrc")
+CS = os.environ.get("PT_CS", os.path.join(ROOT, "model_predictive_control_amd", "csrc"))
 LIB = os.path.join(ROOT, "model_predictive_control_amd", "lib", "libmpcqp_timing.so")
 SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.hip", "quad_box.hip",
         "solve_qp.hip", "sweep.hip", "solve_pf.hip", "mpc_qp.hip", "bicycle.hip", "misc.hip"]
@@ -16,17 +16,22 @@ PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/r
 DYN = "--dyn" in sys.argv or (len(sys.argv) > 1 and sys.argv[1].startswith("dyn"))
 if DYN:  # a separate library whose pf kernel clock times the DYN refinement
     LIB = LIB.replace("_timing.so", "_timing_dyn.so")
+LIB = os.environ.get("PT_LIB", LIB)  # A/B: build and time two variants side by side
 
 if "--build" in sys.argv:
-    objs = []
-    for s in SRCS:
-        o = f"/tmp/timing_{s}.o"
+    from concurrent.futures import ThreadPoolExecutor
+
+    def compile_one(s):
+        o = f"/tmp/timing_{os.path.basename(LIB)}_{s}.o"
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
                         "-DMPCQP_PHASE_TIMING"] + (["-DMPCQP_PHASE_DYN"] if DYN else []) + [
                         "-I", os.path.join(ROOT, "include"), "-c"]
                        + (["-mllvm", "-pragma-unroll-threshold=1000000"] if s == "sweep.hip" else []) + [
                         os.path.join(CS, s), "-o", o], check=True)
-        objs.append(o)
+        return o
+
+    with ThreadPoolExecutor(6) as ex:
+        objs = list(ex.map(compile_one, SRCS))
     subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "--offload-arch=gfx950", "-o", LIB] + objs, check=True)
     print("built", LIB)
     sys.exit(0)
