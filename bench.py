@@ -767,6 +767,7 @@ def main():
             with open(tpath) as fh:
                 traffic = json.load(fh)  # measured at the config's default batch
         err = wl.check()
+        e2e = host_roundtrip(wl, graphs, args)
         dom, others, extra = wl.kernels(traffic)
         cpu = None
         if not args.no_cpu and world == 1:
@@ -797,12 +798,49 @@ def main():
             "roofline": dom,
             "cpu_baseline": cpu,
         }
+        if e2e is not None:
+            out["host_roundtrip"] = e2e
         out.update(others)
         out.update(extra)
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
     return out
+
+
+def host_roundtrip(wl, graphs, args, reps=50):
+    """End-to-end rate of the receding-horizon loop with host buffers (SURVEY.md
+    8(d): reported beside, never as, `value`): per step, x0 from pinned host
+    memory to the device, the step (its graph), z back to pinned host memory,
+    and a stream synchronize -- the host needs u before the next step.  Only
+    for workloads whose step reads X0_t[s] and writes Z[s]."""
+    if not (hasattr(wl, "X0_t") and hasattr(wl, "Z")):
+        return None
+    S = args.slots
+    x0h = [wl.X0_t[s].cpu().pin_memory() for s in range(S)]
+    zh = torch.empty(wl.Z[0].shape, dtype=wl.Z.dtype).pin_memory()
+    st = torch.cuda.current_stream()
+
+    def one(k):
+        s = k % S
+        wl.X0_t[s].copy_(x0h[s], non_blocking=True)
+        if graphs is not None:
+            graphs[s].replay()
+        else:
+            wl.step(s)
+        zh.copy_(wl.Z[s], non_blocking=True)
+        st.synchronize()
+
+    for k in range(5):
+        one(k)
+    t0 = time.perf_counter()
+    for k in range(reps):
+        one(k)
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": round(args.batch / dt, 1), "unit": "solves/s", "ms_per_step": round(dt * 1e3, 4),
+            "h2d_bytes": int(x0h[0].numel() * x0h[0].element_size()),
+            "d2h_bytes": int(zh.numel() * zh.element_size()),
+            "note": "pinned host x0 -> device, one step, z -> pinned host, synchronize; per step"}
 
 
 if __name__ == "__main__":
