@@ -235,7 +235,9 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
           if (!dep) sp = sp - wpp * ysgn * ti;
           W.sweep(k, T(-1), buf);
         } else {
-          const T d = W.sweep(p, T(1), buf);
+          // column p is still in registers (W unchanged since it was read)
+          W.sweep_col(p, T(1), wpp, c, cc);
+          const T d = wpp;
           if (!(d > T(0))) {
             code = MPCQP_STATUS_NOT_CONVEX;
             goto done;
