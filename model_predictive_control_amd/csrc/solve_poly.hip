@@ -171,6 +171,7 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
     while (true) {
       T viol = -Lim<T>::inf();
       int p = 0;
+      T spv = T(0);  // the winner's row value rides along as the arg-max payload
 #pragma unroll
       for (int r = 0; r < BS; ++r) {
         const T vl = (li[r] - si[r]) * sl[r];
@@ -179,19 +180,18 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
         const bool take = vv > viol;
         viol = take ? vv : viol;
         p = take ? W.bi * BS + r : p;
+        spv = take ? si[r] : spv;
       }
-      blocks_argmax(viol, p);
+      blocks_argmax(viol, p, spv);
       p = uniform(p);
       if (!(readlane(viol, 0) > tol)) {
         code = MPCQP_STATUS_OPTIMAL;
         break;
       }
-      publish<T, BS>(si, ss, W.bi, W.bj);
-      __syncthreads();
-      const T sp0 = ss[p];
+      // lis/uis/mds are read-only after the set-up barrier: no publish needed
+      const T sp0 = readlane(spv, 0);
       const T lp = lis[p], up = uis[p];
       const T mpp = mds[p];
-      __syncthreads();
       const int side = (sp0 < lp) ? 1 : 2;
       const T tgt = (side == 1) ? lp : up;
       const T ysgn = (side == 1) ? T(-1) : T(1);
