@@ -745,9 +745,12 @@ def main():
     t0 = time.perf_counter()
     run_steps(0, args.steps)
     torch.cuda.synchronize()
+    # each rank's clock stops when its own K steps are done (the starts are
+    # aligned by the barrier above); the max over ranks below is the time until
+    # the last rank finished, without the closing barrier's own latency
+    elapsed = time.perf_counter() - t0
     if world > 1:
         torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
     elapsed = mdist.max_over_ranks(elapsed, dev if backend == "nccl" else torch.device("cpu"))
     value = world * args.batch * args.steps / elapsed
 
