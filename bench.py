@@ -696,6 +696,7 @@ def main():
     torch.cuda.synchronize()
     graphs = None
     chain = None
+    tail = None
     if not args.no_graph:
         try:
             graphs = []
@@ -713,11 +714,18 @@ def main():
                 with torch.cuda.graph(chain, stream=cap):
                     for s in range(S):
                         wl.step(s)
+                # the timed loop's last K % S steps (slots 0..K%S-1) as one graph too
+                if args.steps % S > 1:
+                    tail = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(tail, stream=cap):
+                        for s in range(args.steps % S):
+                            wl.step(s)
             torch.cuda.synchronize()
         except Exception as e:  # pragma: no cover - reported in the JSON
             print(f"graph capture failed ({e}); eager launches", file=sys.stderr)
             graphs = None
             chain = None
+            tail = None
 
     def run(k):
         if graphs is not None:
@@ -733,6 +741,9 @@ def main():
             if chain is not None and k % S == 0 and end - k >= S:
                 chain.replay()
                 k += S
+            elif tail is not None and k % S == 0 and end - k == args.steps % S:
+                tail.replay()
+                k = end
             else:
                 run(k)
                 k += 1
