@@ -213,6 +213,15 @@ __device__ __forceinline__ bool finite(T v) {
   return __builtin_isfinite(v);
 }
 
+// LDS exchange inside a single-wave workgroup (every kernel on the Sym2D /
+// QSym register layouts launches 64 threads): a wave's LDS operations execute
+// in issue order, so only the compiler must be kept from moving them across
+// the exchange -- no s_barrier and no fence
+__device__ __forceinline__ void lds_exchange() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 inline size_t dtype_size(int dtype) { return dtype == MPCQP_F64 ? 8 : 4; }
 
 }  // namespace mpcqp

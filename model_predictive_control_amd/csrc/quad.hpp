@@ -120,13 +120,13 @@ struct QSym {
 #pragma unroll
         for (int c = 0; c < BS; ++c) gb[(bi * BS + r) * BS + c] = m[r][c];
     }
-    __syncthreads();
+    lds_exchange();
 #pragma unroll
     for (int r = 0; r < BS; ++r) colr[r] = gb[(bi * BS + r) * BS + kc];
 #pragma unroll
     for (int c = 0; c < BS; ++c) colc[c] = gb[(bj * BS + c) * BS + kc];
     const T d = gb[k * BS + kc];
-    __syncthreads();
+    lds_exchange();
     return d;
   }
 
@@ -174,7 +174,7 @@ struct QSym {
 #pragma unroll
       for (int r = 0; r < BS; ++r) wb[bi * BS + r] = w[r];
     }
-    __syncthreads();
+    lds_exchange();
     T wc[BS];
 #pragma unroll
     for (int c = 0; c < BS; ++c) wc[c] = wb[bj * BS + c];
@@ -185,7 +185,7 @@ struct QSym {
       for (int c = 0; c < BS; ++c) s = fma(m[r][c], wc[c], s);
       out[r] = quad_sum(s);
     }
-    __syncthreads();
+    lds_exchange();
   }
 };
 

@@ -150,13 +150,13 @@ struct Sym2D {
 #pragma unroll
         for (int c = 0; c < BS; ++c) buf[(bi * BS + r) * BS + c] = m[r][c];
     }
-    __syncthreads();
+    lds_exchange();
 #pragma unroll
     for (int r = 0; r < BS; ++r) colr[r] = buf[(bi * BS + r) * BS + kc];
 #pragma unroll
     for (int c = 0; c < BS; ++c) colc[c] = buf[(bj * BS + c) * BS + kc];
     const T d = buf[k * BS + kc];
-    __syncthreads();
+    lds_exchange();
     return d;
   }
 
@@ -197,7 +197,7 @@ struct Sym2D {
 #pragma unroll
       for (int r = 0; r < BS; ++r) wb[bi * BS + r] = w[r];
     }
-    __syncthreads();
+    lds_exchange();
     T wc[BS];
 #pragma unroll
     for (int c = 0; c < BS; ++c) wc[c] = wb[bj * BS + c];
@@ -208,7 +208,7 @@ struct Sym2D {
       for (int c = 0; c < BS; ++c) s = fma(m[r][c], wc[c], s);
       out[r] = rowblock_sum(s);
     }
-    __syncthreads();
+    lds_exchange();
   }
 };
 
