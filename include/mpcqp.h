@@ -77,8 +77,12 @@ extern "C" {
 #define MPCQP_STATUS_INFEASIBLE 3  /* lb > ub, or polytope empty */
 #define MPCQP_STATUS_NONFINITE 4   /* NaN/Inf in the data */
 
-/* condense flags */
-#define MPCQP_TV 1 /* A, B are per-stage: N*nx*nx / N*nx*nu per instance */
+/* condense / MPC-step flags */
+#define MPCQP_TV 1  /* A, B are per-stage: N*nx*nx / N*nx*nu per instance */
+#define MPCQP_IPM 2 /* mpcqp_mpc_qp: solve on the stage-wise interior point (mpcqp_mpc_ipm) */
+
+/* status bit 24: the solution was polished to the exact active-set vertex */
+#define MPCQP_STATUS_POLISHED (1 << 24)
 
 int mpcqp_abi_version(void);
 const char* mpcqp_last_error(void);
@@ -273,9 +277,12 @@ int mpcqp_solve_box_ws(int dtype, int batch, int n,
  * computed from the DYNAMICS in fp64 (forward rollout + adjoint), so the
  * fp32 path converges to the solution of the QP its inputs define rather
  * than to that of the fp32-rounded condensed matrices; fp64 or small QPs:
- * the workgroup QP kernel.  Limits: nx, nu <= 16, N*(nu + nx) (state box) or
- * N*nu <= mpcqp_max_qp_size(dtype).  workspace: mpcqp_mpc_qp_workspace()
- * bytes of device scratch (state_box = 1 when xlo or xhi is given).
+ * the workgroup QP kernel.  Steps beyond the dense size limit (N*(nu + nx)
+ * with the state box, or N*nu, > mpcqp_max_qp_size(dtype)) -- and every step
+ * when flags has MPCQP_IPM -- run on the stage-wise interior point
+ * (mpcqp_mpc_ipm) when nx <= 4 and nu <= 2.  Limits: nx, nu <= 16.
+ * workspace: mpcqp_mpc_qp_workspace() bytes of device scratch (state_box = 1
+ * when xlo or xhi is given).
  */
 size_t mpcqp_mpc_qp_workspace(int dtype, int batch, int nx, int nu, int N, int state_box);
 int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
@@ -287,6 +294,83 @@ int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
                  const void* lb, int64_t strideLb, const void* ub, int64_t strideUb,
                  void* z, void* y, void* X, int32_t* status, int max_iter, double tol,
                  void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * The same MPC step (same problem, arguments and outputs as mpcqp_mpc_qp) on
+ * the NON-condensed structure, for any horizon N: the reference's own
+ * controllers run N = 50 with the state box (session4_sol.py:342,391,445,
+ * bounds session4_sol.py:176-181), n + m = 300, beyond the dense kernels.
+ * One instance per lane; primal-dual interior point (Mehrotra
+ * predictor-corrector) whose Newton systems are solved by a Riccati sweep
+ * over the stages, O(N (nx+nu)^3) per iteration, then an exact polish on the
+ * identified active set (status bit MPCQP_STATUS_POLISHED).  Arithmetic is
+ * fp64 for both dtypes.
+ * Extra arguments: U0 (optional, N*nu per instance, stride strideU0): the
+ * starting inputs; H2, q2 (optional, (nx+nu)^2 and nx+nu per stage, N
+ * stages per instance, strides strideH2/strideq2): an extra stage cost
+ * 1/2 [x_k; u_k]'H2_k [x_k; u_k] + q2_k'[x_k; u_k] -- the curvature of the
+ * dynamics in an exact-Hessian SQP; it may be indefinite (the interior
+ * point corrects the inertia of its Newton systems).  Outputs: lam_u
+ * (optional, N*nu): input-bound multipliers, > 0 at ub; pi (optional, N*nx):
+ * costates of x_{k+1} = A_k x_k + B_k u_k + c_k; y (optional, N*nx):
+ * state-bound multipliers, > 0 at xhi.  status: MPCQP_STATUS_NOT_CONVEX when
+ * no inertia correction up to 1e12 makes the Newton system definite.
+ * Limits: nx <= 4, nu <= 2.  workspace: mpcqp_mpc_ipm_workspace() bytes
+ * (N * ~100 doubles per instance).
+ */
+size_t mpcqp_mpc_ipm_workspace(int dtype, int batch, int nx, int nu, int N);
+int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
+                  const void* A, int64_t strideA, const void* Bm, int64_t strideB,
+                  const void* Q, int64_t strideQ, const void* R, int64_t strideR,
+                  const void* Qf, int64_t strideQf, const void* c, int64_t strideC,
+                  const void* x0, int64_t strideX0,
+                  const void* xlo, const void* xhi, int64_t strideXb,
+                  const void* lb, int64_t strideLb, const void* ub, int64_t strideUb,
+                  const void* U0, int64_t strideU0, const void* H2, int64_t strideH2,
+                  const void* q2, int64_t strideq2,
+                  void* z, void* y, void* X, void* lam_u, void* pi, int32_t* status,
+                  int max_iter, double tol, void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * Converged MPCController.solve (session_4/main.py:115-116: IPOPT's optimum
+ * of the single-shooting NLP of main.py:41-113 / session4_sol.py:132-217)
+ * as an SQP over batched initial states, one iteration =
+ *   mpcqp_bicycle_rti (linearise at U, states X) -> [mpcqp_bicycle_hessian]
+ *   -> mpcqp_mpc_ipm (H2, q2; outputs z, y, pi) -> mpcqp_bicycle_sqp_step.
+ * mpcqp_bicycle_hessian: per instance and stage, H2_k = sum_i pi_{k+1,i}
+ *   d2 fe_i / d(x,u)2 at (x_k, u_k) + mu I (6 x 6 over [x; u]; mu the
+ *   instance's Levenberg-Marquardt damping, NULL = 0) and q2_k = -H2_k w_k,
+ *   so that the QP's extra cost is 1/2 (w - w_k)'H2_k (w - w_k); zeros for
+ *   instances whose flags lack MPCQP_SQP_EXACT (flags NULL = all exact).
+ *   X ((N+1) x 4), U (N x 2), pi (N x 4) per instance.
+ * mpcqp_bicycle_sqp_step: per instance not yet MPCQP_SQP_DONE: step d = Z - U
+ *   (Z the QP solution; an instance whose qp_status is not OPTIMAL takes no
+ *   step and leaves exact-Hessian mode), L1 merit 1/2 J + rho |state-box violation|_1 with
+ *   rho >= 2 max|yq|, Armijo backtracking by quadratic interpolation; then
+ *   U += alpha d, y += alpha (yq - y), pi += alpha (piq - pi), the rollout X
+ *   ((N+1) x 4) at the new U and the first-order optimality residual of the
+ *   NLP there (projected gradient of the Lagrangian on the input box,
+ *   state-box violation, complementarity of y) -> kkt.  flags: DONE when
+ *   kkt <= tol; EXACT (use the exact Hessian from now on) once kkt < 1e-2;
+ *   bits 8..23 count the iterations.  mu (Levenberg-Marquardt damping of the
+ *   exact-Hessian QPs, caller-initialised, e.g. 0.1): divided by 4 after a
+ *   full step (to 0 below 1e-11), multiplied by 4 (at least 1e-3) after a
+ *   step that needed backtracking or a failed QP.  rho, mu, kkt: one double
+ *   per instance (rho initialised to 0).  Q, R, Qf shared (4x4, 2x2, 4x4);
+ *   bounds as in mpcqp_mpc_qp (lb/ub stride strideLb).  fp64.
+ */
+#define MPCQP_SQP_DONE 1
+#define MPCQP_SQP_EXACT 2
+int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
+                          const void* X, const void* U, const void* pi, const int32_t* flags,
+                          const double* mu, void* H2, void* q2, void* stream);
+int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts, const double* params,
+                           const void* x0, int64_t strideX0, const void* Q, const void* R,
+                           const void* Qf, const void* xlo, const void* xhi, int64_t strideXb,
+                           const void* lb, const void* ub, int64_t strideLb, void* U,
+                           const void* Z, const void* yq, const void* piq,
+                           const int32_t* qp_status, void* y, void* pi, void* X, double* rho,
+                           double* kkt, double* mu, int32_t* flags, double tol, void* stream);
 
 /*
  * Batched finite-horizon Riccati recursion, FHC.py:51-61:

@@ -18,6 +18,10 @@ LIB_PATH = os.environ.get("MPCQP_LIB", os.path.join(_HERE, "lib", "libmpcqp.so")
 F64 = 0
 F32 = 1
 TV = 1
+IPM = 2
+STATUS_POLISHED = 1 << 24
+SQP_DONE = 1
+SQP_EXACT = 2
 
 STATUS_OPTIMAL = 0
 STATUS_MAXITER = 1
@@ -65,6 +69,17 @@ SIGNATURES = {
                           _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                           _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                           _vp, _vp, _vp, _vp, _i, _d, _vp, ctypes.c_size_t, _vp]),
+    "mpcqp_mpc_ipm_workspace": (ctypes.c_size_t, [_i, _i, _i, _i, _i]),
+    "mpcqp_mpc_ipm": (_i, [_i, _i, _i, _i, _i, _i,
+                           _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
+                           _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
+                           _vp, _i64, _vp, _i64,
+                           _vp, _vp, _vp, _vp, _vp, _vp, _i, _d, _vp, ctypes.c_size_t, _vp]),
+    "mpcqp_bicycle_hessian": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _vp, _vp,
+                                   _vp, _vp, _vp, _vp, _vp]),
+    "mpcqp_bicycle_sqp_step": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _i64,
+                                    _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _vp]),
     "mpcqp_riccati": (_i, [_i, _i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                            _vp, _i64, _vp, _vp, _vp]),
     "mpcqp_bicycle_rti": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _i64, _vp, _i64,

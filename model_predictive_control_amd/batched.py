@@ -24,8 +24,8 @@ import torch
 from . import _native as nat
 
 __all__ = [
-    "condense", "solve_box", "mpc_box", "mpc_qp", "solve_poly", "solve_qp", "sweep", "riccati", "gemv",
-    "rollout",
+    "condense", "solve_box", "mpc_box", "mpc_qp", "mpc_ipm", "solve_poly", "solve_qp", "sweep", "riccati", "gemv",
+    "rollout", "bicycle_rti", "bicycle_hessian", "bicycle_sqp_step",
     "pack_lower", "unpack_lower", "status_code", "status_iters", "workspace_bytes",
 ]
 
@@ -159,9 +159,7 @@ def condense(A, B, Q, R, Qf, N: int, x0=None, c=None, *, tv: bool = False,
     A, B, Q, R, Qf = (_dev(v, dt, dev) for v in (A, B, Q, R, Qf))
     x0, c = _dev(x0, dt, dev), _dev(c, dt, dev)
     nx, nu = int(B.shape[-2]), int(B.shape[-1])
-    if R.ndim == 1 or (R.ndim == 2 and R.shape != (nu, nu) and R.shape[-1] == nu):
-        # FHC.py:141 passes R with shape (1,); numpy broadcasting semantics
-        R = R.expand(nu, nu).contiguous() if R.ndim == 1 else R
+    R = _weight_r(R, nu)
     base = 3 if tv else 2
     sA, bA = _inst(A, base, "A")
     sB, bB = _inst(B, base, "B")
@@ -199,8 +197,7 @@ def mpc_box(A, B, Q, R, Qf, N: int, x0, lb=None, ub=None, c=None, *, tv: bool = 
     A, B, Q, R, Qf = (_dev(v, dt, dev) for v in (A, B, Q, R, Qf))
     x0, c = _dev(x0, dt, dev), _dev(c, dt, dev)
     nx, nu = int(B.shape[-2]), int(B.shape[-1])
-    if R.ndim == 1:
-        R = R.expand(nu, nu).contiguous()
+    R = _weight_r(R, nu)
     n = N * nu
     base = 3 if tv else 2
     sA, bA = _inst(A, base, "A")
@@ -236,24 +233,16 @@ def mpc_qp_workspace_bytes(dtype: torch.dtype, batch: int, nx: int, nu: int, N: 
     return int(_lib().mpcqp_mpc_qp_workspace(_code(dtype), batch, nx, nu, N, int(bool(state_box))))
 
 
-def mpc_qp(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=None, *,
-           tv: bool = False, states: bool = False, max_iter: int = 0, tol: float = 0.0,
-           out: tuple | None = None, ws: torch.Tensor | None = None):
-    """One MPC step with input box and state box, end to end (include/mpcqp.h
-    ``mpcqp_mpc_qp``): condense + QP, fp32 refined against the dynamics.
-
-    Plant conventions as ``condense``; xlo/xhi: state bounds on x_1..x_N,
-    (nx,) repeated over the horizon, (N*nx,) shared or (b, N*nx); lb/ub as
-    ``mpc_box``.  Returns (z (b, N*nu), y (b, N*nx) or None, status[, X
-    (b, N, nx) when ``states``]); y are the state-row multipliers (> 0 at xhi).
-    """
+def _mpc_step_args(A, B, Q, R, Qf, N, x0, xlo, xhi, lb, ub, c, tv):
+    """Normalise the arguments shared by mpc_qp / mpc_ipm (plant conventions
+    of ``condense``; state bounds (nx,) repeated over the horizon, (N*nx,)
+    shared or (b, N*nx); input bounds as ``mpc_box``)."""
     dt = A.dtype if isinstance(A, torch.Tensor) else torch.float64
     dev = A.device if isinstance(A, torch.Tensor) else torch.device("cuda")
     A, B, Q, R, Qf = (_dev(v, dt, dev) for v in (A, B, Q, R, Qf))
     x0, c = _dev(x0, dt, dev), _dev(c, dt, dev)
     nx, nu = int(B.shape[-2]), int(B.shape[-1])
-    if R.ndim == 1:
-        R = R.expand(nu, nu).contiguous()
+    R = _weight_r(R, nu)
     n, m = N * nu, N * nx
     base = 3 if tv else 2
     sA, bA = _inst(A, base, "A")
@@ -286,7 +275,30 @@ def mpc_qp(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=N
                       (sxl, bxl), (sxh, bxh),
                       (slb, lbt.shape[0] if lbt is not None and lbt.ndim == 2 else None),
                       (sub, ubt.shape[0] if ubt is not None and ubt.ndim == 2 else None))
-    sbox = xlo_t is not None or xhi_t is not None
+    return dict(dt=dt, dev=dev, nx=nx, nu=nu, n=n, m=m, batch=batch,
+                head=(_ptr(A), sA, _ptr(B), sB, _ptr(Q), sQ, _ptr(R), sR, _ptr(Qf), sQf,
+                      _ptr(c), sC, _ptr(x0), sX, _ptr(xlo_t), _ptr(xhi_t), sXb,
+                      _ptr(lbt), slb, _ptr(ubt), sub),
+                keep=(A, B, Q, R, Qf, c, x0, xlo_t, xhi_t, lbt, ubt),
+                sbox=xlo_t is not None or xhi_t is not None)
+
+
+def mpc_qp(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=None, *,
+           tv: bool = False, states: bool = False, max_iter: int = 0, tol: float = 0.0,
+           out: tuple | None = None, ws: torch.Tensor | None = None, ipm: bool = False):
+    """One MPC step with input box and state box, end to end (include/mpcqp.h
+    ``mpcqp_mpc_qp``): condense + QP, fp32 refined against the dynamics.
+    Steps beyond the dense kernels' size (and every step with ``ipm=True``)
+    run on the stage-wise interior point (``mpc_ipm``).
+
+    Plant conventions as ``condense``; xlo/xhi: state bounds on x_1..x_N,
+    (nx,) repeated over the horizon, (N*nx,) shared or (b, N*nx); lb/ub as
+    ``mpc_box``.  Returns (z (b, N*nu), y (b, N*nx) or None, status[, X
+    (b, N, nx) when ``states``]); y are the state-row multipliers (> 0 at xhi).
+    """
+    g = _mpc_step_args(A, B, Q, R, Qf, N, x0, xlo, xhi, lb, ub, c, tv)
+    dt, dev, batch, n, m, nx = g["dt"], g["dev"], g["batch"], g["n"], g["m"], g["nx"]
+    sbox = g["sbox"]
     if out is None:
         z = torch.empty((batch, n), dtype=dt, device=dev)
         y = torch.empty((batch, m), dtype=dt, device=dev) if sbox else None
@@ -296,16 +308,61 @@ def mpc_qp(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=N
         z, y, status = out[:3]
         X = out[3] if len(out) > 3 else None
     lib = _lib()
-    wsb = int(lib.mpcqp_mpc_qp_workspace(_code(dt), batch, nx, nu, N, int(sbox)))
+    wsb = int(lib.mpcqp_mpc_qp_workspace(_code(dt), batch, nx, g["nu"], N, int(sbox)))
     ws = _workspace(wsb, dev, ws)
-    rc = lib.mpcqp_mpc_qp(
-        _code(dt), batch, nx, nu, N, nat.TV if tv else 0,
-        _ptr(A), sA, _ptr(B), sB, _ptr(Q), sQ, _ptr(R), sR, _ptr(Qf), sQf, _ptr(c), sC,
-        _ptr(x0), sX, _ptr(xlo_t), _ptr(xhi_t), sXb, _ptr(lbt), slb, _ptr(ubt), sub,
-        _ptr(z), _ptr(y), _ptr(X), _ptr(status), int(max_iter), float(tol), _ptr(ws), wsb,
-        _stream())
+    flags = (nat.TV if tv else 0) | (nat.IPM if ipm else 0)
+    rc = lib.mpcqp_mpc_qp(_code(dt), batch, nx, g["nu"], N, flags, *g["head"],
+                          _ptr(z), _ptr(y), _ptr(X), _ptr(status), int(max_iter), float(tol),
+                          _ptr(ws), wsb, _stream())
     nat.check(rc, "mpcqp_mpc_qp")
     return (z, y, status, X) if states else (z, y, status)
+
+
+def mpc_ipm(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=None, *,
+            tv: bool = False, U0=None, H2=None, q2=None, max_iter: int = 0, tol: float = 0.0,
+            out: dict | None = None, ws: torch.Tensor | None = None):
+    """The MPC step of ``mpc_qp`` on the stage-wise interior point, any horizon
+    (include/mpcqp.h ``mpcqp_mpc_ipm``; nx <= 4, nu <= 2).  U0: optional
+    starting inputs (b, N, nu) or (b, N*nu).  H2 (b, N, nx+nu, nx+nu), q2
+    (b, N, nx+nu): optional extra stage cost 1/2 w'H2 w + q2'w over
+    w = [x_k; u_k] (may be indefinite).  Returns a dict with z (b, N*nu),
+    X (b, N, nx) = x_1..x_N, y (b, N*nx) state-bound and lam_u (b, N*nu)
+    input-bound multipliers (> 0 at the upper bound), pi (b, N, nx) costates
+    of the dynamics, status (b,).  ``out``: a dict of preallocated outputs."""
+    g = _mpc_step_args(A, B, Q, R, Qf, N, x0, xlo, xhi, lb, ub, c, tv)
+    dt, dev, batch, n, m, nx = g["dt"], g["dev"], g["batch"], g["n"], g["m"], g["nx"]
+    U0t = None if U0 is None else _dev(U0, dt, dev).reshape(batch, n)
+    n2 = nx + g["nu"]
+    H2t = None if H2 is None else _dev(H2, dt, dev).reshape(batch, N * n2 * n2)
+    q2t = None if q2 is None else _dev(q2, dt, dev).reshape(batch, N * n2)
+    o = dict(out or {})
+    shapes = dict(z=((batch, n), dt), y=((batch, m), dt), lam_u=((batch, n), dt),
+                  X=((batch, N, nx), dt), pi=((batch, N, nx), dt), status=((batch,), torch.int32))
+    for k, (shp, kd) in shapes.items():
+        if k not in o:
+            o[k] = torch.empty(shp, dtype=kd, device=dev)
+    lib = _lib()
+    wsb = int(lib.mpcqp_mpc_ipm_workspace(_code(dt), batch, nx, g["nu"], N))
+    ws = _workspace(wsb, dev, ws)
+    rc = lib.mpcqp_mpc_ipm(_code(dt), batch, nx, g["nu"], N, nat.TV if tv else 0, *g["head"],
+                           _ptr(U0t), 0 if U0t is None else n, _ptr(H2t),
+                           0 if H2t is None else N * n2 * n2, _ptr(q2t),
+                           0 if q2t is None else N * n2, _ptr(o["z"]), _ptr(o["y"]), _ptr(o["X"]),
+                           _ptr(o["lam_u"]), _ptr(o["pi"]), _ptr(o["status"]), int(max_iter),
+                           float(tol), _ptr(ws), wsb, _stream())
+    nat.check(rc, "mpcqp_mpc_ipm")
+    return o
+
+
+def _weight_r(R, nu: int):
+    """R as (nu, nu) (or batched).  FHC.py:141 passes R with shape (1,), which
+    NumPy broadcasts; a 1-D R is accepted only for nu == 1 (shape (1,)) -- a
+    vector of diagonal weights must be given as a matrix (torch.diag)."""
+    if R.ndim == 1:
+        if R.shape[0] != 1 or nu != 1:
+            raise ValueError(f"R of shape {tuple(R.shape)} with nu={nu}: pass an (nu, nu) matrix")
+        return R.reshape(1, 1).contiguous()
+    return R
 
 
 # ----------------------------------------------------------------- box QP
@@ -545,8 +602,7 @@ def riccati(A, B, Q, R, Pf, N: int):
     dev = A.device
     A, B, Q, R, Pf = (_dev(v, dt, dev) for v in (A, B, Q, R, Pf))
     nx, nu = int(B.shape[-2]), int(B.shape[-1])
-    if R.ndim == 1:
-        R = R.expand(nu, nu).contiguous()
+    R = _weight_r(R, nu)
     sA, bA = _inst(A, 2, "A")
     sB, bB = _inst(B, 2, "B")
     sQ, bQ = _inst(Q, 2, "Q")
@@ -592,12 +648,56 @@ def bicycle_rti(x0, U, params, ts: float, *, states: bool = False):
     B = torch.empty((b, N, 4, 2), dtype=dt, device=dev)
     c = torch.empty((b, N, 4), dtype=dt, device=dev)
     X = torch.empty((b, N + 1, 4), dtype=dt, device=dev) if states else None
-    prm = (ctypes.c_double * 4)(params.axis_front, params.axis_rear, params.acceleration,
-                                params.friction)
+    prm = _bike_params(params)
     rc = _lib().mpcqp_bicycle_rti(_code(dt), b, N, float(ts), prm, _ptr(x0), 4, _ptr(U), 2 * N,
                                   _ptr(X), _ptr(A), _ptr(B), _ptr(c), _stream())
     nat.check(rc, "mpcqp_bicycle_rti")
     return (A, B, c, X) if states else (A, B, c)
+
+
+def _bike_params(params):
+    return (ctypes.c_double * 4)(params.axis_front, params.axis_rear, params.acceleration,
+                                 params.friction)
+
+
+def bicycle_hessian(X, U, pi, params, ts: float, flags=None, mu=None,
+                    out: tuple | None = None):
+    """Per stage, the curvature of the dynamics weighted by the costates plus
+    a proximal mu I (include/mpcqp.h ``mpcqp_bicycle_hessian``): X (b, N+1,
+    4), U (b, N, 2), pi (b, N, 4) fp64, mu (b,) or None -> H2 (b, N, 6, 6),
+    q2 (b, N, 6); zeros where flags (b,) lacks SQP_EXACT."""
+    b, N = int(U.shape[0]), int(U.shape[1])
+    if out is None:
+        H2 = torch.empty((b, N, 6, 6), dtype=torch.float64, device=U.device)
+        q2 = torch.empty((b, N, 6), dtype=torch.float64, device=U.device)
+    else:
+        H2, q2 = out
+    rc = _lib().mpcqp_bicycle_hessian(nat.F64, b, N, float(ts), _bike_params(params), _ptr(X),
+                                      _ptr(U), _ptr(pi), _ptr(flags), _ptr(mu), _ptr(H2),
+                                      _ptr(q2), _stream())
+    nat.check(rc, "mpcqp_bicycle_hessian")
+    return H2, q2
+
+
+def bicycle_sqp_step(x0, U, Z, yq, piq, y, pi, X, state: dict, params, ts: float, Q, R, Qf,
+                     xlo=None, xhi=None, lb=None, ub=None, tol: float = 1e-9, qp_status=None):
+    """Line search + update + NLP optimality residual (include/mpcqp.h
+    ``mpcqp_bicycle_sqp_step``), in place on U, y, pi, X and ``state``
+    (rho, kkt, mu float64 (b,), flags int32 (b,)).  Bounds: xlo/xhi (N*4,)
+    shared or (b, N*4); lb/ub (N*2,) shared or (b, N*2)."""
+    b, N = int(U.shape[0]), int(U.shape[1])
+    sxb = 0 if xlo is None or xlo.ndim == 1 else 4 * N
+    if xhi is not None and xhi.ndim == 2:
+        sxb = 4 * N
+    slb = 0 if lb is None or lb.ndim == 1 else 2 * N
+    if ub is not None and ub.ndim == 2:
+        slb = 2 * N
+    rc = _lib().mpcqp_bicycle_sqp_step(
+        nat.F64, b, N, float(ts), _bike_params(params), _ptr(x0), 4, _ptr(Q), _ptr(R), _ptr(Qf),
+        _ptr(xlo), _ptr(xhi), sxb, _ptr(lb), _ptr(ub), slb, _ptr(U), _ptr(Z), _ptr(yq), _ptr(piq),
+        _ptr(qp_status), _ptr(y), _ptr(pi), _ptr(X), _ptr(state["rho"]), _ptr(state["kkt"]), _ptr(state["mu"]),
+        _ptr(state["flags"]), float(tol), _stream())
+    nat.check(rc, "mpcqp_bicycle_sqp_step")
 
 
 # --------------------------------------------------------------- rollout

@@ -1,0 +1,140 @@
+// ipm.hip -- mpcqp_mpc_ipm: one MPC step with input box and state box on the
+// stage-wise (non-condensed) structure, one instance per lane, for any
+// horizon.  The algorithm is in ipm_lane.hpp (primal-dual interior point,
+// Mehrotra predictor-corrector, Riccati factorisation per iteration).
+//
+// Where it sits: the condensed kernels (mpcqp_mpc_qp's sweep + product-form
+// and workgroup active sets) hold dense (N(nu+nx))^2 matrices and stop at
+// N(nu+nx) = 192.  The reference's own controllers go beyond that:
+// session4_sol.py:342,391,445 run N = 50 with the state box of
+// session4_sol.py:176-181 and the input box, i.e. n + m = 100 + 200.  Here the
+// work per iteration is O(N (nx+nu)^3) and the memory O(N), so the horizon is
+// unbounded; mpcqp_mpc_qp routes such steps here.
+//
+// Mapping: lane = instance, 64 instances per workgroup (one wave).  Every lane
+// runs the same sequence of operations on its own data (no divergence except
+// the iteration count, which the wave pays as its maximum), and every
+// workspace access is one fp64 per lane at consecutive addresses.
+#include "common.hpp"
+
+#define MPCQP_HD __host__ __device__
+#include "ipm_lane.hpp"
+
+namespace mpcqp {
+
+template <typename T, int NX, int NU>
+__global__ __launch_bounds__(64) void ipm_kernel(ipm::Args<T> a) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= a.batch) return;
+  ipm::solve_lane<T, NX, NU>(a, b);
+}
+
+static int64_t ipm_ldb(int batch) { return ((int64_t)batch + 63) / 64 * 64; }
+
+static bool ipm_dims(int nx, int nu, int& NX, int& NU) {
+  if (nx <= 2 && nu <= 1) { NX = 2; NU = 1; return true; }
+  if (nx <= 4 && nu <= 2) { NX = 4; NU = 2; return true; }
+  return false;
+}
+
+size_t ipm_ws_bytes(int batch, int nx, int nu, int N) {
+  int NX, NU;
+  if (batch <= 0 || N < 1 || !ipm_dims(nx, nu, NX, NU)) return 0;
+  const int F = (NX == 2) ? ipm::Layout<2, 1>::F : ipm::Layout<4, 2>::F;
+  return (size_t)N * F * ipm_ldb(batch) * sizeof(double);
+}
+
+bool ipm_supported(int nx, int nu) {
+  int NX, NU;
+  return ipm_dims(nx, nu, NX, NU);
+}
+
+template <typename T>
+static int ipm_launch(ipm::Args<T>& a, hipStream_t st) {
+  int NX, NU;
+  ipm_dims(a.nx, a.nu, NX, NU);
+  const dim3 grid((unsigned)((a.batch + 63) / 64)), blk(64);
+  if (NX == 2)
+    hipLaunchKernelGGL((ipm_kernel<T, 2, 1>), grid, blk, 0, st, a);
+  else
+    hipLaunchKernelGGL((ipm_kernel<T, 4, 2>), grid, blk, 0, st, a);
+  MPCQP_CHECK_LAUNCH("ipm_kernel");
+  return MPCQP_OK;
+}
+
+int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const void* A,
+                 int64_t sA, const void* Bm, int64_t sB, const void* Q, int64_t sQ, const void* R,
+                 int64_t sR, const void* Qf, int64_t sQf, const void* c, int64_t sC,
+                 const void* x0, int64_t sX0, const void* xlo, const void* xhi, int64_t sXb,
+                 const void* lb, int64_t sLb, const void* ub, int64_t sUb, const void* U0,
+                 int64_t sU0, const void* H2, int64_t sH2, const void* q2, int64_t sq2, void* z,
+                 void* y, void* X, void* lam_u, void* pi, int32_t* status, int max_iter,
+                 double tol, void* ws, size_t ws_bytes, hipStream_t st) {
+  const size_t need = ipm_ws_bytes(batch, nx, nu, N);
+  MPCQP_CHECK_ARG(ws && ws_bytes >= need, "mpcqp_mpc_ipm: workspace %zu bytes < %zu", ws_bytes,
+                  need);
+  auto fill = [&](auto& a, auto tp) {
+    using T = decltype(tp);
+    a.batch = batch; a.nx = nx; a.nu = nu; a.N = N; a.tv = (flags & MPCQP_TV) ? 1 : 0;
+    a.max_iter = max_iter > 0 ? max_iter : 100;
+    a.tol = tol > 0 ? tol : 1e-10;
+    a.tol_mu = 1e-2 * a.tol;
+    a.tol_polish = 1e-6;
+    a.mu_polish = 1e-6;
+    a.A = (const T*)A; a.sA = sA; a.B = (const T*)Bm; a.sB = sB; a.c = (const T*)c; a.sC = sC;
+    a.Q = (const T*)Q; a.sQ = sQ; a.R = (const T*)R; a.sR = sR; a.Qf = (const T*)Qf; a.sQf = sQf;
+    a.x0 = (const T*)x0; a.sX0 = sX0;
+    a.xlo = (const T*)xlo; a.xhi = (const T*)xhi; a.sXb = sXb;
+    a.lb = (const T*)lb; a.sLb = sLb; a.ub = (const T*)ub; a.sUb = sUb;
+    a.U0 = (const T*)U0; a.sU0 = sU0;
+    a.H2 = (const T*)H2; a.sH2 = sH2; a.q2 = (const T*)q2; a.sq2 = sq2;
+    a.z = (T*)z; a.y = (T*)y; a.X = (T*)X; a.lam_u = (T*)lam_u; a.pi = (T*)pi; a.status = status;
+    a.ws = (double*)ws; a.ldb = ipm_ldb(batch);
+  };
+  if (dtype == MPCQP_F64) {
+    ipm::Args<double> a;
+    fill(a, 0.0);
+    return ipm_launch(a, st);
+  }
+  ipm::Args<float> a;
+  fill(a, 0.0f);
+  return ipm_launch(a, st);
+}
+
+}  // namespace mpcqp
+
+extern "C" size_t mpcqp_mpc_ipm_workspace(int dtype, int batch, int nx, int nu, int N) {
+  if (dtype != MPCQP_F64 && dtype != MPCQP_F32) return 0;
+  return mpcqp::ipm_ws_bytes(batch, nx, nu, N);
+}
+
+extern "C" int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
+                             const void* A, int64_t strideA, const void* Bm, int64_t strideB,
+                             const void* Q, int64_t strideQ, const void* R, int64_t strideR,
+                             const void* Qf, int64_t strideQf, const void* c, int64_t strideC,
+                             const void* x0, int64_t strideX0, const void* xlo, const void* xhi,
+                             int64_t strideXb, const void* lb, int64_t strideLb, const void* ub,
+                             int64_t strideUb, const void* U0, int64_t strideU0, const void* H2,
+                             int64_t strideH2, const void* q2, int64_t strideq2, void* z, void* y,
+                             void* X, void* lam_u, void* pi, int32_t* status, int max_iter,
+                             double tol, void* ws, size_t ws_bytes, void* stream) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64 || dtype == MPCQP_F32, "mpcqp_mpc_ipm: bad dtype %d", dtype);
+  MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "mpcqp_mpc_ipm: bad sizes (batch=%d, N=%d)", batch, N);
+  MPCQP_CHECK_ARG(nx >= 1 && nu >= 1, "mpcqp_mpc_ipm: nx=%d nu=%d", nx, nu);
+  if (!ipm_supported(nx, nu)) {
+    set_error("mpcqp_mpc_ipm: nx=%d nu=%d outside the compiled set (nx <= 4, nu <= 2)", nx, nu);
+    return MPCQP_ENOTSUP;
+  }
+  MPCQP_CHECK_ARG(A && Bm && Q && R && Qf && x0 && z && status,
+                  "mpcqp_mpc_ipm: A, B, Q, R, Qf, x0, z, status are required");
+  MPCQP_CHECK_ARG(strideA >= 0 && strideB >= 0 && strideQ >= 0 && strideR >= 0 && strideQf >= 0 &&
+                      strideC >= 0 && strideX0 >= 0 && strideXb >= 0 && strideLb >= 0 &&
+                      strideUb >= 0 && strideU0 >= 0 && strideH2 >= 0 && strideq2 >= 0,
+                  "mpcqp_mpc_ipm: negative stride");
+  if (batch == 0) return MPCQP_OK;
+  return mpc_ipm_impl(dtype, batch, nx, nu, N, flags, A, strideA, Bm, strideB, Q, strideQ, R,
+                      strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi, strideXb, lb,
+                      strideLb, ub, strideUb, U0, strideU0, H2, strideH2, q2, strideq2, z, y, X,
+                      lam_u, pi, status, max_iter, tol, ws, ws_bytes, (hipStream_t)stream);
+}

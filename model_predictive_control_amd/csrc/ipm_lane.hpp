@@ -1,0 +1,908 @@
+// ipm_lane.hpp -- one instance of the box-constrained, time-varying LQ
+// problem of an MPC step, solved by a primal-dual interior-point method on the
+// NON-condensed (stage-wise) structure with a Riccati factorisation per
+// iteration.  Included by ipm.hip (one instance per lane) with
+// MPCQP_HD = __host__ __device__.
+//
+// Problem (the OCP of session_4/main.py:41-113 / session4_sol.py:132-217 on
+// linear(ised) dynamics, cost scaled by 1/2 like the condensed QP):
+//   min  1/2 sum_{k<N} (x_k'Q x_k + u_k'R u_k) + 1/2 x_N'Qf x_N
+//   s.t. x_{k+1} = A_k x_k + B_k u_k + c_k,   x_0 given,
+//        lb_k <= u_k <= ub_k,   xlo_k <= x_{k+1} <= xhi_k     (k = 0..N-1)
+// Any bound may be infinite.  No limit on N: the work is O(N (nx+nu)^3) per
+// iteration and nothing is dense in N (the condensed kernels need
+// N (nx+nu) <= 192, which the reference's N = 50 controllers,
+// session4_sol.py:342,391,445, exceed).
+//
+// Method: Mehrotra predictor-corrector.  The bounded variables stay strictly
+// inside their boxes (slacks s = v - lo, hi - v are derived, never stored);
+// the dynamics may be violated by the iterate (infeasible start) and are
+// driven to zero by the Newton steps.  Each iteration is four sweeps over the
+// horizon:
+//   1. backward: apply the previous step, residuals, Sigma = lam/s, Riccati
+//      factorisation (P_k, K_k, G_k^-1) and the predictor right-hand side;
+//   2. forward: predictor direction, its step to the boundary and the
+//      affine complementarity (a quadratic in alpha, accumulated on the way);
+//   3. backward: corrector right-hand side on the stored factorisation;
+//   4. forward: corrector direction, step length.
+// Stage k owns u_k, x_{k+1}, pi_{k+1} (the costate of x_{k+1} = ...), the
+// bound duals of u_k and x_{k+1}, and the factor data; everything lives in a
+// stage-major, field-major, instance-minor workspace (one fp64 per lane per
+// field), so every access of a wavefront is one coalesced 512-byte row.
+#pragma once
+
+#include <stdint.h>
+
+#include <cmath>
+
+#ifndef MPCQP_HD
+#error "define MPCQP_HD before including ipm_lane.hpp"
+#endif
+
+namespace mpcqp {
+namespace ipm {
+
+// per-stage field offsets (in doubles) of the workspace
+template <int NX, int NU>
+struct Layout {
+  static constexpr int NB = NU + NX;  // bounded components of stage k: u_k then x_{k+1}
+  // iterate
+  static constexpr int U = 0, X = U + NU, PI = X + NX, LL = PI + NX, LU = LL + NB;
+  // corrector direction (du, dx, dpi) and predictor direction (duA, dxA)
+  static constexpr int DU = LU + NB, DX = DU + NU, DPI = DX + NX, DUA = DPI + NX, DXA = DUA + NU;
+  // factorisation and right-hand sides
+  static constexpr int PP = DXA + NX;                 // P_{k+1}, packed lower
+  static constexpr int KM = PP + NX * (NX + 1) / 2;   // K_k (NU x NX)
+  static constexpr int GI = KM + NU * NX;             // G_k^-1, packed lower
+  static constexpr int E = GI + NU * (NU + 1) / 2;    // e_k: dynamics residual
+  static constexpr int KV = E + NX;                   // k_k: feed-forward
+  static constexpr int PV = KV + NU;                  // p_{k+1}
+  static constexpr int GA = PV + NX;                  // gradient without bound duals
+  // the stage data, converted to fp64
+  static constexpr int DA = GA + NB, DB = DA + NX * NX, DC = DB + NX * NU;
+  static constexpr int F = DC + NX;
+};
+
+template <typename T>
+struct Args {
+  int batch, nx, nu, N, tv, max_iter;
+  double tol, tol_mu;          // convergence of the interior-point iteration
+  double tol_polish, mu_polish;  // first polish attempt: residuals and mu below these
+  const T* A; int64_t sA;
+  const T* B; int64_t sB;
+  const T* c; int64_t sC;
+  const T* Q; int64_t sQ;
+  const T* R; int64_t sR;
+  const T* Qf; int64_t sQf;
+  const T* x0; int64_t sX0;
+  const T* xlo; const T* xhi; int64_t sXb;
+  const T* lb; int64_t sLb;
+  const T* ub; int64_t sUb;
+  const T* U0; int64_t sU0;  // optional starting inputs (N x nu); NULL = 0
+  // optional extra stage cost 1/2 [x_k; u_k]'H2_k [x_k; u_k] + q2_k'[x_k; u_k],
+  // k = 0..N-1, (nx+nu)^2 and nx+nu per stage (the curvature of the dynamics
+  // in an exact-Hessian SQP); NULL = none
+  const T* H2; int64_t sH2;
+  const T* q2; int64_t sq2;
+  T* z;                      // N*nu
+  T* y;                      // optional N*nx: state-bound multipliers, > 0 at xhi
+  T* X;                      // optional N*nx: x_1..x_N
+  T* lam_u;                  // optional N*nu: input-bound multipliers, > 0 at ub
+  T* pi;                     // optional N*nx: costates of x_{k+1} = A x_k + B u_k + c_k
+  int32_t* status;
+  double* ws;
+  int64_t ldb;               // instance stride of one field (>= batch)
+};
+
+constexpr double kInf = __builtin_huge_val();
+
+MPCQP_HD inline bool fin(double v) { return __builtin_isfinite(v); }
+MPCQP_HD inline int pk(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
+// Stage bounds of the NB components (u_k then x_{k+1}); +-inf where absent.
+template <typename T, int NX, int NU>
+MPCQP_HD inline void load_bounds(const Args<T>& a, int b, int k, double* lo, double* hi) {
+  for (int j = 0; j < NU; ++j) {
+    const bool on = j < a.nu;
+    lo[j] = (on && a.lb) ? (double)a.lb[(int64_t)b * a.sLb + (int64_t)k * a.nu + j] : -kInf;
+    hi[j] = (on && a.ub) ? (double)a.ub[(int64_t)b * a.sUb + (int64_t)k * a.nu + j] : kInf;
+  }
+  for (int i = 0; i < NX; ++i) {
+    const bool on = i < a.nx;
+    const int64_t o = (int64_t)b * a.sXb + (int64_t)k * a.nx + i;
+    lo[NU + i] = (on && a.xlo) ? (double)a.xlo[o] : -kInf;
+    hi[NU + i] = (on && a.xhi) ? (double)a.xhi[o] : kInf;
+  }
+}
+
+// Q (stage < N) or Qf, entry (i, j) with zero padding.
+template <typename T>
+MPCQP_HD inline double wq(const Args<T>& a, int b, bool term, int i, int j) {
+  if (i >= a.nx || j >= a.nx) return 0.0;
+  const T* M = term ? a.Qf + (int64_t)b * a.sQf : a.Q + (int64_t)b * a.sQ;
+  return (double)M[i * a.nx + j];
+}
+// R, padded with the identity (a padded input has zero B column: it stays 0)
+template <typename T>
+MPCQP_HD inline double wr(const Args<T>& a, int b, int i, int j) {
+  if (i >= a.nu || j >= a.nu) return i == j ? 1.0 : 0.0;
+  return (double)a.R[(int64_t)b * a.sR + i * a.nu + j];
+}
+
+// Extra stage cost of stage k (zero when absent, for k = N, and on padding):
+// xx block (i, j < nx), xu block (i < nx, r < nu), uu block, linear terms.
+template <typename T>
+MPCQP_HD inline const T* h2_stage(const Args<T>& a, int b, int k) {
+  const int n2 = a.nx + a.nu;
+  return a.H2 + (int64_t)b * a.sH2 + (int64_t)k * n2 * n2;
+}
+template <typename T>
+MPCQP_HD inline double h2xx(const Args<T>& a, int b, int k, int i, int j) {
+  if (!a.H2 || k >= a.N || i >= a.nx || j >= a.nx) return 0.0;
+  return (double)h2_stage(a, b, k)[i * (a.nx + a.nu) + j];
+}
+template <typename T>
+MPCQP_HD inline double h2xu(const Args<T>& a, int b, int k, int i, int r) {
+  if (!a.H2 || k >= a.N || i >= a.nx || r >= a.nu) return 0.0;
+  return (double)h2_stage(a, b, k)[i * (a.nx + a.nu) + a.nx + r];
+}
+template <typename T>
+MPCQP_HD inline double h2uu(const Args<T>& a, int b, int k, int r, int q) {
+  if (!a.H2 || k >= a.N || r >= a.nu || q >= a.nu) return 0.0;
+  return (double)h2_stage(a, b, k)[(a.nx + r) * (a.nx + a.nu) + a.nx + q];
+}
+template <typename T>
+MPCQP_HD inline double q2x(const Args<T>& a, int b, int k, int i) {
+  if (!a.q2 || k >= a.N || i >= a.nx) return 0.0;
+  return (double)a.q2[(int64_t)b * a.sq2 + (int64_t)k * (a.nx + a.nu) + i];
+}
+template <typename T>
+MPCQP_HD inline double q2u(const Args<T>& a, int b, int k, int r) {
+  if (!a.q2 || k >= a.N || r >= a.nu) return 0.0;
+  return (double)a.q2[(int64_t)b * a.sq2 + (int64_t)k * (a.nx + a.nu) + a.nx + r];
+}
+
+// Gradient of the cost plus the dynamics terms (no bound duals) for u_k
+// (g[0..NU)) and x_{k+1} (g[NU..NB)): v = [u_k; x_{k+1}], pi = pi_{k+1},
+// xk = x_k, and from stage k+1: A1 = A_{k+1}, pi2 = pi_{k+2}, u1 = u_{k+1}.
+template <typename T, int NX, int NU>
+MPCQP_HD inline void stage_grad(const Args<T>& a, int b, int k, const double (&Bm)[NX][NU],
+                                const double (&A1)[NX][NX], const double* v,
+                                const double (&pi)[NX], const double (&pi2)[NX],
+                                const double (&xk)[NX], const double (&u1)[NU], double* g) {
+  const bool term = (k == a.N - 1);
+  for (int j = 0; j < NU; ++j) {
+    double s = q2u(a, b, k, j);
+    for (int q = 0; q < NU; ++q) s = fma(wr(a, b, j, q) + h2uu(a, b, k, j, q), v[q], s);
+    for (int i = 0; i < NX; ++i) s = fma(h2xu(a, b, k, i, j), xk[i], s);
+    for (int i = 0; i < NX; ++i) s = fma(Bm[i][j], pi[i], s);
+    g[j] = s;
+  }
+  for (int i = 0; i < NX; ++i) {
+    double s = q2x(a, b, k + 1, i) - pi[i];
+    for (int q = 0; q < NX; ++q)
+      s = fma(wq(a, b, term, i, q) + h2xx(a, b, k + 1, i, q), v[NU + q], s);
+    for (int r = 0; r < NU; ++r) s = fma(h2xu(a, b, k + 1, i, r), u1[r], s);
+    for (int q = 0; q < NX; ++q) s = fma(A1[q][i], pi2[q], s);  // A_{k+1}' pi_{k+2}
+    g[NU + i] = s;
+  }
+}
+
+// Symmetric positive-definite NU x NU inverse, packed lower in and out.
+// Returns false on a non-positive pivot.
+template <int NU>
+MPCQP_HD inline bool spd_inv(const double* G, double* Gi) {
+  if constexpr (NU == 1) {
+    if (!(G[0] > 0.0)) return false;
+    Gi[0] = 1.0 / G[0];
+    return true;
+  } else if constexpr (NU == 2) {
+    const double det = G[0] * G[2] - G[1] * G[1];
+    if (!(G[0] > 0.0) || !(det > 0.0)) return false;
+    const double r = 1.0 / det;
+    Gi[0] = G[2] * r;
+    Gi[1] = -G[1] * r;
+    Gi[2] = G[0] * r;
+    return true;
+  } else {
+    // Gauss-Jordan on a full copy (no pivoting: SPD)
+    double M[NU][NU], I[NU][NU];
+    for (int i = 0; i < NU; ++i)
+      for (int j = 0; j < NU; ++j) {
+        M[i][j] = G[pk(i, j)];
+        I[i][j] = i == j ? 1.0 : 0.0;
+      }
+    for (int p = 0; p < NU; ++p) {
+      if (!(M[p][p] > 0.0)) return false;
+      const double r = 1.0 / M[p][p];
+      for (int j = 0; j < NU; ++j) { M[p][j] *= r; I[p][j] *= r; }
+      for (int i = 0; i < NU; ++i) {
+        if (i == p) continue;
+        const double f = M[i][p];
+        for (int j = 0; j < NU; ++j) { M[i][j] -= f * M[p][j]; I[i][j] -= f * I[p][j]; }
+      }
+    }
+    for (int i = 0; i < NU; ++i)
+      for (int j = 0; j <= i; ++j) Gi[pk(i, j)] = 0.5 * (I[i][j] + I[j][i]);
+    return true;
+  }
+}
+
+// One backward Riccati step of the Newton system.  In: the cost-to-go of
+// x_{k+1} from the stages after k (Ph, ph), the stage data, the gradient g and
+// the diagonal barrier/penalty Sigma of u_k (first NU) and x_{k+1} (next NX).
+// Out: P_{k+1}, p_{k+1} (the full cost-to-go of x_{k+1}), K_k, k_k, G_k^-1, and
+// Ph, ph overwritten with the cost-to-go of x_k.  dreg is added to every
+// Hessian diagonal (inertia correction of a non-convex stage cost, H2).
+// False on a non-positive pivot of G = R + Sigma_u + B'P B: the reduced
+// Hessian of the Newton system is not positive definite.
+template <typename T, int NX, int NU>
+MPCQP_HD inline bool riccati_stage(const Args<T>& a, int b, int k, const double (&Am)[NX][NX],
+                                   const double (&Bm)[NX][NU], const double (&e)[NX],
+                                   const double* g, const double* sig, double (&Ph)[NX][NX],
+                                   double (&ph)[NX], double (&P)[NX][NX], double (&p)[NX],
+                                   double (&K)[NU][NX], double (&kk)[NU], double* Gi,
+                                   double dreg) {
+  // P_{k+1} = Q' + H2xx_{k+1} + Sigma_x + Ph,  p_{k+1} = g_x + ph
+  const bool term = (k == a.N - 1);
+  for (int i = 0; i < NX; ++i) {
+    for (int j = 0; j < NX; ++j) P[i][j] = wq(a, b, term, i, j) + h2xx(a, b, k + 1, i, j) + Ph[i][j];
+    P[i][i] += sig[NU + i] + dreg;
+    p[i] = g[NU + i] + ph[i];
+  }
+  // Pe = P e + p;  PA = P A;  PB = P B
+  double Pe[NX], PA[NX][NX], PB[NX][NU];
+  for (int i = 0; i < NX; ++i) {
+    double s = p[i];
+    for (int j = 0; j < NX; ++j) s = fma(P[i][j], e[j], s);
+    Pe[i] = s;
+    for (int j = 0; j < NX; ++j) {
+      double t = 0.0;
+      for (int q = 0; q < NX; ++q) t = fma(P[i][q], Am[q][j], t);
+      PA[i][j] = t;
+    }
+    for (int j = 0; j < NU; ++j) {
+      double t = 0.0;
+      for (int q = 0; q < NX; ++q) t = fma(P[i][q], Bm[q][j], t);
+      PB[i][j] = t;
+    }
+  }
+  // G = R + H2uu + Sigma_u + B'PB,  Hx = H2xu' + B'PA,  h = g_u + B'Pe
+  double G[NU * (NU + 1) / 2], Hx[NU][NX], h[NU];
+  for (int r = 0; r < NU * (NU + 1) / 2; ++r) Gi[r] = 0.0;
+  for (int r = 0; r < NU; ++r) {
+    for (int q = 0; q <= r; ++q) {
+      double s = wr(a, b, r, q) + h2uu(a, b, k, r, q) + (r == q ? sig[r] + dreg : 0.0);
+      for (int i = 0; i < NX; ++i) s = fma(Bm[i][r], PB[i][q], s);
+      G[pk(r, q)] = s;
+    }
+    for (int j = 0; j < NX; ++j) {
+      double s = h2xu(a, b, k, j, r);
+      for (int i = 0; i < NX; ++i) s = fma(Bm[i][r], PA[i][j], s);
+      Hx[r][j] = s;
+    }
+    double s = g[r];
+    for (int i = 0; i < NX; ++i) s = fma(Bm[i][r], Pe[i], s);
+    h[r] = s;
+  }
+  const bool ok = spd_inv<NU>(G, Gi);
+  // K = -Gi Hx,  kk = -Gi h
+  for (int r = 0; r < NU; ++r) {
+    for (int j = 0; j < NX; ++j) {
+      double s = 0.0;
+      for (int q = 0; q < NU; ++q) s = fma(Gi[pk(r, q)], Hx[q][j], s);
+      K[r][j] = -s;
+    }
+    double s = 0.0;
+    for (int q = 0; q < NU; ++q) s = fma(Gi[pk(r, q)], h[q], s);
+    kk[r] = -s;
+  }
+  // Ph = A'PA + Hx'K,  ph = A'Pe + Hx'kk   (the cost-to-go of x_k)
+  for (int i = 0; i < NX; ++i) {
+    for (int j = 0; j <= i; ++j) {
+      double s = 0.0;
+      for (int q = 0; q < NX; ++q) s = fma(Am[q][i], PA[q][j], s);
+      for (int r = 0; r < NU; ++r) s = fma(Hx[r][i], K[r][j], s);
+      Ph[i][j] = s;
+      Ph[j][i] = s;
+    }
+    double s = 0.0;
+    for (int q = 0; q < NX; ++q) s = fma(Am[q][i], Pe[q], s);
+    for (int r = 0; r < NU; ++r) s = fma(Hx[r][i], kk[r], s);
+    ph[i] = s;
+  }
+  return ok;
+}
+
+// Workspace accessor: field f of stage k of this lane's instance.
+template <int F>
+struct Ws {
+  double* W;
+  int64_t ld;
+  MPCQP_HD double& operator()(int k, int f) const { return W[((int64_t)k * F + f) * ld]; }
+};
+
+// Starting margin inside a box: a point at least this far from a finite bound.
+MPCQP_HD inline double interior(double v, double lo, double hi) {
+  const bool fl = fin(lo), fh = fin(hi);
+  if (fl && fh) {
+    const double m = 0.05 * (hi - lo);
+    return fmin(fmax(v, lo + m), hi - m);
+  }
+  if (fl) return fmax(v, lo + 0.05 * (1.0 + fabs(lo)));
+  if (fh) return fmin(v, hi - 0.05 * (1.0 + fabs(hi)));
+  return v;
+}
+
+// ------------------------------------------------------------- polish
+// Guess the active set from the interior-point iterate (lam > s), then
+// solve the QP with those bounds as equalities exactly: method of
+// multipliers on  L = J + y'(v - b) + rho/2 |v - b|^2  over the active
+// components, each step one Riccati sweep pair on the same structure.
+// Accepted when the inactive bounds hold and the multipliers have the
+// right sign; the result is then the vertex solution itself, not a
+// barrier-perturbed point (weakly active bounds would otherwise leave an
+// O(sqrt(mu)) error).  The iterate lives in DU/DX/DPI (v, pi), the
+// multipliers in DUA/DXA and the active flags in GA; the interior-point
+// iterate in U/X/PI/LL/LU is not touched.
+template <typename T, int NX, int NU>
+MPCQP_HD bool polish(const Args<T>& a, int b, const Ws<Layout<NX, NU>::F>& at, const double* x0) {
+  using L = Layout<NX, NU>;
+  constexpr int NB = L::NB;
+  const int N = a.N;
+  for (int k = 0; k < N; ++k) {
+    double lo[NB], hi[NB];
+    load_bounds<T, NX, NU>(a, b, k, lo, hi);
+    for (int j = 0; j < NB; ++j) {
+      const double vj = j < NU ? at(k, L::U + j) : at(k, L::X + j - NU);
+      const double l = at(k, L::LL + j), u = at(k, L::LU + j);
+      const double rl = fin(lo[j]) ? l / (vj - lo[j]) : 0.0;
+      const double ru = fin(hi[j]) ? u / (hi[j] - vj) : 0.0;
+      const double act = (ru > 1.0 && ru >= rl) ? 1.0 : ((rl > 1.0) ? -1.0 : 0.0);
+      at(k, L::GA + j) = act;
+      const double y = act > 0.0 ? u : (act < 0.0 ? -l : 0.0);
+      if (j < NU) { at(k, L::DU + j) = vj; at(k, L::DUA + j) = y; }
+      else { at(k, L::DX + j - NU) = vj; at(k, L::DXA + j - NU) = y; }
+    }
+    for (int i = 0; i < NX; ++i) at(k, L::DPI + i) = at(k, L::PI + i);
+  }
+  // rounds: after each, violated inactive bounds join the active set and
+  // active ones with a wrong-sign multiplier leave it (a primal-dual
+  // active-set step from the interior-point guess); accepted when a round
+  // changes nothing
+  // penalty per step: a large rho pins the active components and moves the
+  // multipliers close in one step, but rho * (v - b) carries rho times the
+  // rounding of v - b (~1e-16 |b|) into y; the smaller ones that follow
+  // contract the remaining error by ~curvature / rho each with a floor of
+  // 1e-12 (rho = 1e4)
+  constexpr int kSteps = 4, kRounds = 4;
+  constexpr double kRho[kSteps] = {1e8, 1e6, 1e4, 1e4};
+  for (int round = 0; round < kRounds; ++round) {
+  bool good = true, changed = false;
+  for (int step = 0; step < kSteps; ++step) {
+    const double rho = kRho[step];
+    double Ph[NX][NX], ph[NX], A1[NX][NX], pi2[NX], u1[NU];
+    for (int i = 0; i < NX; ++i) {
+      ph[i] = 0.0;
+      pi2[i] = 0.0;
+      for (int j = 0; j < NX; ++j) { Ph[i][j] = 0.0; A1[i][j] = 0.0; }
+    }
+    for (int r = 0; r < NU; ++r) u1[r] = 0.0;
+    for (int k = N - 1; k >= 0; --k) {
+      double v[NB], pi[NX], lo[NB], hi[NB];
+      for (int j = 0; j < NU; ++j) v[j] = at(k, L::DU + j);
+      for (int i = 0; i < NX; ++i) { v[NU + i] = at(k, L::DX + i); pi[i] = at(k, L::DPI + i); }
+      load_bounds<T, NX, NU>(a, b, k, lo, hi);
+      double xk[NX];
+      for (int i = 0; i < NX; ++i) xk[i] = k == 0 ? x0[i] : at(k - 1, L::DX + i);
+      double Am[NX][NX], Bm[NX][NU], e[NX];
+      for (int i = 0; i < NX; ++i) {
+        for (int j = 0; j < NX; ++j) Am[i][j] = at(k, L::DA + i * NX + j);
+        for (int j = 0; j < NU; ++j) Bm[i][j] = at(k, L::DB + i * NU + j);
+      }
+      for (int i = 0; i < NX; ++i) {
+        double s = at(k, L::DC + i) - v[NU + i];
+        for (int j = 0; j < NX; ++j) s = fma(Am[i][j], xk[j], s);
+        for (int j = 0; j < NU; ++j) s = fma(Bm[i][j], v[j], s);
+        e[i] = s;
+      }
+      double g[NB], sig[NB];
+      stage_grad<T, NX, NU>(a, b, k, Bm, A1, v, pi, pi2, xk, u1, g);
+      for (int j = 0; j < NB; ++j) {
+        const double act = at(k, L::GA + j);
+        const double y = j < NU ? at(k, L::DUA + j) : at(k, L::DXA + j - NU);
+        sig[j] = act != 0.0 ? rho : 0.0;
+        if (act != 0.0) g[j] += y + rho * (v[j] - (act > 0.0 ? hi[j] : lo[j]));
+      }
+      double P[NX][NX], p[NX], K[NU][NX], kk[NU], Gi[NU * (NU + 1) / 2];
+      good = riccati_stage<T, NX, NU>(a, b, k, Am, Bm, e, g, sig, Ph, ph, P, p, K, kk, Gi, 0.0) &&
+             good;
+      for (int i = 0; i < NX; ++i) {
+        for (int j = 0; j <= i; ++j) at(k, L::PP + pk(i, j)) = P[i][j];
+        for (int r = 0; r < NU; ++r) at(k, L::KM + r * NX + i) = K[r][i];
+        at(k, L::E + i) = e[i];
+        at(k, L::PV + i) = p[i];
+      }
+      for (int r = 0; r < NU; ++r) at(k, L::KV + r) = kk[r];
+      for (int i = 0; i < NX; ++i) {
+        pi2[i] = pi[i];
+        for (int j = 0; j < NX; ++j) A1[i][j] = Am[i][j];
+      }
+      for (int r = 0; r < NU; ++r) u1[r] = v[r];
+    }
+    // forward: full Newton step, then the multiplier update
+    const bool last = step == kSteps - 1;
+    double dx[NX];
+    for (int i = 0; i < NX; ++i) dx[i] = 0.0;
+    for (int k = 0; k < N; ++k) {
+      double du[NU], dxn[NX];
+      for (int r = 0; r < NU; ++r) {
+        double s = at(k, L::KV + r);
+        for (int j = 0; j < NX; ++j) s = fma(at(k, L::KM + r * NX + j), dx[j], s);
+        du[r] = s;
+      }
+      for (int i = 0; i < NX; ++i) {
+        double s = at(k, L::E + i);
+        for (int j = 0; j < NX; ++j) s = fma(at(k, L::DA + i * NX + j), dx[j], s);
+        for (int r = 0; r < NU; ++r) s = fma(at(k, L::DB + i * NU + r), du[r], s);
+        dxn[i] = s;
+      }
+      for (int i = 0; i < NX; ++i) {
+        double s = at(k, L::PV + i);
+        for (int j = 0; j < NX; ++j) s = fma(at(k, L::PP + pk(i, j)), dxn[j], s);
+        at(k, L::DPI + i) += s;
+      }
+      double lo[NB], hi[NB];
+      load_bounds<T, NX, NU>(a, b, k, lo, hi);
+      for (int j = 0; j < NB; ++j) {
+        double& vr = j < NU ? at(k, L::DU + j) : at(k, L::DX + j - NU);
+        const double vj = vr + (j < NU ? du[j] : dxn[j - NU]);
+        vr = vj;
+        const double act = at(k, L::GA + j);
+        if (act != 0.0) {
+          double& yr = j < NU ? at(k, L::DUA + j) : at(k, L::DXA + j - NU);
+          const double bnd = act > 0.0 ? hi[j] : lo[j];
+          const double y = yr + rho * (vj - bnd);
+          yr = y;
+          if (last) {
+            good = good && fabs(vj - bnd) <= 1e-9 * (1.0 + fabs(bnd));
+            if (act > 0.0 ? y < -1e-9 * (1.0 + fabs(y)) : y > 1e-9 * (1.0 + fabs(y))) {
+              at(k, L::GA + j) = 0.0;  // wrong sign: release
+              yr = 0.0;
+              changed = true;
+            }
+          }
+        } else if (last) {
+          const double jl = (lo[j] - vj) / (1.0 + fabs(lo[j]));
+          const double jh = (vj - hi[j]) / (1.0 + fabs(hi[j]));
+          if (jl > 1e-9 || jh > 1e-9) {  // violated: fix at the violated side
+            at(k, L::GA + j) = jl > jh ? -1.0 : 1.0;
+            changed = true;
+          }
+        }
+      }
+      for (int i = 0; i < NX; ++i) dx[i] = dxn[i];
+    }
+  }
+  if (good && !changed) return true;
+  if (!good) return false;
+  }
+  return false;
+}
+
+// Outputs of one instance.  polished: v in DU/DX, multipliers (> 0 at the
+// upper bound) in DUA/DXA; else the interior-point iterate, multipliers
+// lam_u - lam_l.
+template <typename T, int NX, int NU>
+MPCQP_HD void emit(const Args<T>& a, int b, const Ws<Layout<NX, NU>::F>& at, bool polished,
+                   int code, int it) {
+  using L = Layout<NX, NU>;
+  const int N = a.N, nx = a.nx, nu = a.nu;
+  const int fu = polished ? L::DU : L::U, fx = polished ? L::DX : L::X;
+  for (int k = 0; k < N; ++k) {
+    for (int j = 0; j < nu; ++j) a.z[(int64_t)b * N * nu + (int64_t)k * nu + j] = (T)at(k, fu + j);
+    if (a.lam_u)
+      for (int j = 0; j < nu; ++j)
+        a.lam_u[(int64_t)b * N * nu + (int64_t)k * nu + j] =
+            (T)(polished ? at(k, L::DUA + j) : at(k, L::LU + j) - at(k, L::LL + j));
+    if (a.X)
+      for (int i = 0; i < nx; ++i)
+        a.X[(int64_t)b * N * nx + (int64_t)k * nx + i] = (T)at(k, fx + i);
+    if (a.pi)
+      for (int i = 0; i < nx; ++i)
+        a.pi[(int64_t)b * N * nx + (int64_t)k * nx + i] = (T)at(k, (polished ? L::DPI : L::PI) + i);
+    if (a.y)
+      for (int i = 0; i < nx; ++i)
+        a.y[(int64_t)b * N * nx + (int64_t)k * nx + i] =
+            (T)(polished ? at(k, L::DXA + i)
+                         : at(k, L::LU + NU + i) - at(k, L::LL + NU + i));
+  }
+  a.status[b] = code | ((it & 0xFFFF) << 8) | (polished ? (1 << 24) : 0);
+}
+
+template <typename T, int NX, int NU>
+MPCQP_HD void solve_lane(const Args<T>& a, int b) {
+  using L = Layout<NX, NU>;
+  constexpr int NB = L::NB;
+  const int N = a.N, nx = a.nx, nu = a.nu;
+  const Ws<L::F> at{a.ws + b, a.ldb};
+
+  double x0[NX];
+  for (int i = 0; i < NX; ++i) x0[i] = i < nx ? (double)a.x0[(int64_t)b * a.sX0 + i] : 0.0;
+
+  // ---------------------------------------------------------------- start
+  // copy the stage data (fp64, padded), inputs strictly inside their box,
+  // states rolled out and pushed inside theirs, pi = 0, duals = 1
+  int mcount = 0;
+  {
+    double x[NX];
+    for (int i = 0; i < NX; ++i) x[i] = x0[i];
+    for (int k = 0; k < N; ++k) {
+      const T* Ak = a.A + (int64_t)b * a.sA + (a.tv ? (int64_t)k * nx * nx : 0);
+      const T* Bk = a.B + (int64_t)b * a.sB + (a.tv ? (int64_t)k * nx * nu : 0);
+      const T* ck = a.c ? a.c + (int64_t)b * a.sC + (int64_t)k * nx : nullptr;
+      double Am[NX][NX], Bm[NX][NU], cm[NX];
+      for (int i = 0; i < NX; ++i) {
+        for (int j = 0; j < NX; ++j) Am[i][j] = (i < nx && j < nx) ? (double)Ak[i * nx + j] : 0.0;
+        for (int j = 0; j < NU; ++j) Bm[i][j] = (i < nx && j < nu) ? (double)Bk[i * nu + j] : 0.0;
+        cm[i] = (ck && i < nx) ? (double)ck[i] : 0.0;
+      }
+      for (int i = 0; i < NX; ++i) {
+        for (int j = 0; j < NX; ++j) at(k, L::DA + i * NX + j) = Am[i][j];
+        for (int j = 0; j < NU; ++j) at(k, L::DB + i * NU + j) = Bm[i][j];
+        at(k, L::DC + i) = cm[i];
+      }
+      double lo[NB], hi[NB];
+      load_bounds<T, NX, NU>(a, b, k, lo, hi);
+      double u[NU];
+      for (int j = 0; j < NU; ++j) {
+        const double u0 = (a.U0 && j < nu) ? (double)a.U0[(int64_t)b * a.sU0 + (int64_t)k * nu + j] : 0.0;
+        u[j] = interior(u0, lo[j], hi[j]);
+      }
+      double xn[NX];
+      for (int i = 0; i < NX; ++i) {
+        double s = cm[i];
+        for (int j = 0; j < NX; ++j) s = fma(Am[i][j], x[j], s);
+        for (int j = 0; j < NU; ++j) s = fma(Bm[i][j], u[j], s);
+        xn[i] = interior(s, lo[NU + i], hi[NU + i]);
+      }
+      for (int j = 0; j < NU; ++j) at(k, L::U + j) = u[j];
+      for (int i = 0; i < NX; ++i) {
+        at(k, L::X + i) = xn[i];
+        at(k, L::PI + i) = 0.0;
+        x[i] = xn[i];
+      }
+      for (int j = 0; j < NB; ++j) {
+        at(k, L::LL + j) = fin(lo[j]) ? 1.0 : 0.0;
+        at(k, L::LU + j) = fin(hi[j]) ? 1.0 : 0.0;
+        mcount += (fin(lo[j]) ? 1 : 0) + (fin(hi[j]) ? 1 : 0);
+      }
+    }
+  }
+
+
+  // every exit writes the outputs and returns from inside the loop
+  double alpha = 0.0, sigmu = 0.0;  // step and sigma*mu of the last corrector
+  double mu_pol = a.mu_polish;      // next polish attempt below this mu
+  // inertia correction (only a non-convex H2 needs it): on a non-positive
+  // pivot pass 1 runs again with a growing dreg; each iteration starts a
+  // third below the last one that worked (0 once it falls below 1e-12).  It
+  // changes the Newton direction, not the residuals, so the iterate still
+  // converges to a KKT point of the QP.
+  double dreg = 0.0, dlast = 0.0;
+  const int max_iter = a.max_iter;
+  for (int it = 0;; ++it) {
+    // ======================================== pass 1: backward factorisation
+    double Ph[NX][NX], ph[NX], A1[NX][NX], pi2[NX], u1[NU];
+    for (int i = 0; i < NX; ++i) {
+      ph[i] = 0.0;
+      pi2[i] = 0.0;
+      for (int j = 0; j < NX; ++j) { Ph[i][j] = 0.0; A1[i][j] = 0.0; }
+    }
+    for (int r = 0; r < NU; ++r) u1[r] = 0.0;
+    double rstat = 0.0, rdyn = 0.0, musum = 0.0;
+    bool pd = true;
+    for (int k = N - 1; k >= 0; --k) {
+      double v[NB], ll[NB], lu[NB], pi[NX], lo[NB], hi[NB];
+      for (int j = 0; j < NU; ++j) v[j] = at(k, L::U + j);
+      for (int i = 0; i < NX; ++i) { v[NU + i] = at(k, L::X + i); pi[i] = at(k, L::PI + i); }
+      for (int j = 0; j < NB; ++j) { ll[j] = at(k, L::LL + j); lu[j] = at(k, L::LU + j); }
+      load_bounds<T, NX, NU>(a, b, k, lo, hi);
+      if (alpha > 0.0) {  // apply the corrector step of the previous iteration
+        for (int j = 0; j < NB; ++j) {
+          const double dv = j < NU ? at(k, L::DU + j) : at(k, L::DX + j - NU);
+          const double dva = j < NU ? at(k, L::DUA + j) : at(k, L::DXA + j - NU);
+          if (fin(lo[j])) {
+            const double sl = v[j] - lo[j];
+            const double dla = -ll[j] * (1.0 + dva / sl);
+            const double rc = sigmu - sl * ll[j] - dva * dla;
+            ll[j] += alpha * ((rc - ll[j] * dv) / sl);
+          }
+          if (fin(hi[j])) {
+            const double su = hi[j] - v[j];
+            const double dua = -lu[j] * (1.0 - dva / su);
+            const double rc = sigmu - su * lu[j] + dva * dua;
+            lu[j] += alpha * ((rc + lu[j] * dv) / su);
+          }
+          v[j] += alpha * dv;
+        }
+        for (int i = 0; i < NX; ++i) pi[i] += alpha * at(k, L::DPI + i);
+        for (int j = 0; j < NU; ++j) at(k, L::U + j) = v[j];
+        for (int i = 0; i < NX; ++i) { at(k, L::X + i) = v[NU + i]; at(k, L::PI + i) = pi[i]; }
+        for (int j = 0; j < NB; ++j) { at(k, L::LL + j) = ll[j]; at(k, L::LU + j) = lu[j]; }
+      }
+      // x_k: the previous stage's state (its own pass applies the same step)
+      double xk[NX];
+      if (k == 0) {
+        for (int i = 0; i < NX; ++i) xk[i] = x0[i];
+      } else {
+        for (int i = 0; i < NX; ++i) {
+          xk[i] = at(k - 1, L::X + i);
+          if (alpha > 0.0) xk[i] += alpha * at(k - 1, L::DX + i);
+        }
+      }
+      double Am[NX][NX], Bm[NX][NU], e[NX];
+      for (int i = 0; i < NX; ++i) {
+        for (int j = 0; j < NX; ++j) Am[i][j] = at(k, L::DA + i * NX + j);
+        for (int j = 0; j < NU; ++j) Bm[i][j] = at(k, L::DB + i * NU + j);
+      }
+      // dynamics residual e_k = A x_k + B u_k + c_k - x_{k+1}
+      for (int i = 0; i < NX; ++i) {
+        double s = at(k, L::DC + i) - v[NU + i];
+        for (int j = 0; j < NX; ++j) s = fma(Am[i][j], xk[j], s);
+        for (int j = 0; j < NU; ++j) s = fma(Bm[i][j], v[j], s);
+        e[i] = s;
+        rdyn = fmax(rdyn, fabs(s));
+      }
+      // gradients without the bound duals
+      double g[NB];
+      stage_grad<T, NX, NU>(a, b, k, Bm, A1, v, pi, pi2, xk, u1, g);
+      // stationarity residual, complementarity, Sigma
+      double sig[NB];
+      for (int j = 0; j < NB; ++j) {
+        double sj = 0.0;
+        double r = g[j];
+        if (fin(lo[j])) {
+          const double sl = v[j] - lo[j];
+          sj += ll[j] / sl;
+          musum += sl * ll[j];
+          r -= ll[j];
+        }
+        if (fin(hi[j])) {
+          const double su = hi[j] - v[j];
+          sj += lu[j] / su;
+          musum += su * lu[j];
+          r += lu[j];
+        }
+        sig[j] = sj;
+        rstat = fmax(rstat, fabs(r));
+      }
+      double P[NX][NX], p[NX], K[NU][NX], kk[NU], Gi[NU * (NU + 1) / 2];
+      const bool ok =
+          riccati_stage<T, NX, NU>(a, b, k, Am, Bm, e, g, sig, Ph, ph, P, p, K, kk, Gi, dreg);
+      pd = pd && ok;
+      for (int i = 0; i < NX; ++i) {
+        for (int j = 0; j <= i; ++j) at(k, L::PP + pk(i, j)) = P[i][j];
+        for (int r = 0; r < NU; ++r) at(k, L::KM + r * NX + i) = K[r][i];
+        at(k, L::E + i) = e[i];
+        at(k, L::PV + i) = p[i];
+      }
+      for (int r = 0; r < NU; ++r) {
+        for (int q = 0; q <= r; ++q) at(k, L::GI + pk(r, q)) = Gi[pk(r, q)];
+        at(k, L::KV + r) = kk[r];
+      }
+      for (int j = 0; j < NB; ++j) at(k, L::GA + j) = g[j];
+      for (int i = 0; i < NX; ++i) {
+        pi2[i] = pi[i];
+        for (int j = 0; j < NX; ++j) A1[i][j] = Am[i][j];
+      }
+      for (int r = 0; r < NU; ++r) u1[r] = v[r];
+    }
+    const double mu = mcount ? musum / mcount : 0.0;
+    if (!fin(rstat) || !fin(rdyn) || !fin(mu)) {
+      emit<T, NX, NU>(a, b, at, false, MPCQP_STATUS_NONFINITE, it);
+      return;
+    }
+    if (!pd) {
+      dreg = dreg > 0.0 ? 8.0 * dreg : (dlast > 0.0 ? dlast : 1e-4);
+      if (dreg > 1e12 || it >= max_iter) {
+        emit<T, NX, NU>(a, b, at, false, MPCQP_STATUS_NOT_CONVEX, it);
+        return;
+      }
+      alpha = 0.0;  // the pending step is applied already
+      continue;
+    }
+    if (dreg > 0.0) {  // next iteration starts a third lower
+      dlast = dreg;
+      dreg = dreg / 3.0 > 1e-12 ? dreg / 3.0 : 0.0;
+    }
+
+    const bool conv = rstat <= a.tol && rdyn <= a.tol && mu <= a.tol_mu;
+    if (mcount && mu_pol > 0.0 && mu <= mu_pol && rstat <= a.tol_polish && rdyn <= a.tol_polish) {
+      if (polish<T, NX, NU>(a, b, at, x0)) {
+        emit<T, NX, NU>(a, b, at, true, MPCQP_STATUS_OPTIMAL, it);
+        return;
+      }
+      // wrong active-set guess: keep iterating, try again at a smaller mu;
+      // the polish overwrote the factorisation, so pass 1 runs again
+      mu_pol *= 1e-2;
+      alpha = 0.0;
+      if (conv || it >= max_iter) {
+        emit<T, NX, NU>(a, b, at, false, conv ? MPCQP_STATUS_OPTIMAL : MPCQP_STATUS_MAXITER, it);
+        return;
+      }
+      continue;
+    }
+    if (conv || it >= max_iter) {
+      emit<T, NX, NU>(a, b, at, false, conv ? MPCQP_STATUS_OPTIMAL : MPCQP_STATUS_MAXITER, it);
+      return;
+    }
+
+    // ========================================== pass 2: forward predictor
+    double amax = 1.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
+    {
+      double dx[NX];
+      for (int i = 0; i < NX; ++i) dx[i] = 0.0;
+      for (int k = 0; k < N; ++k) {
+        double du[NU], dxn[NX];
+        for (int r = 0; r < NU; ++r) {
+          double s = at(k, L::KV + r);
+          for (int j = 0; j < NX; ++j) s = fma(at(k, L::KM + r * NX + j), dx[j], s);
+          du[r] = s;
+        }
+        for (int i = 0; i < NX; ++i) {
+          double s = at(k, L::E + i);
+          for (int j = 0; j < NX; ++j) s = fma(at(k, L::DA + i * NX + j), dx[j], s);
+          for (int r = 0; r < NU; ++r) s = fma(at(k, L::DB + i * NU + r), du[r], s);
+          dxn[i] = s;
+        }
+        for (int r = 0; r < NU; ++r) at(k, L::DUA + r) = du[r];
+        for (int i = 0; i < NX; ++i) at(k, L::DXA + i) = dxn[i];
+        double lo[NB], hi[NB];
+        load_bounds<T, NX, NU>(a, b, k, lo, hi);
+        for (int j = 0; j < NB; ++j) {
+          const double vj = j < NU ? at(k, L::U + j) : at(k, L::X + j - NU);
+          const double dv = j < NU ? du[j] : dxn[j - NU];
+          if (fin(lo[j])) {
+            const double sl = vj - lo[j], l = at(k, L::LL + j);
+            const double dl = -l * (1.0 + dv / sl);
+            if (dv < 0.0) amax = fmin(amax, -sl / dv);
+            if (dl < 0.0) amax = fmin(amax, -l / dl);
+            c0 += sl * l;
+            c1 += sl * dl + l * dv;
+            c2 += dv * dl;
+          }
+          if (fin(hi[j])) {
+            const double su = hi[j] - vj, l = at(k, L::LU + j);
+            const double dl = -l * (1.0 - dv / su);
+            if (dv > 0.0) amax = fmin(amax, su / dv);
+            if (dl < 0.0) amax = fmin(amax, -l / dl);
+            c0 += su * l;
+            c1 += su * dl - l * dv;
+            c2 -= dv * dl;
+          }
+        }
+        for (int i = 0; i < NX; ++i) dx[i] = dxn[i];
+      }
+    }
+    if (mcount) {
+      const double mua = (c0 + amax * (c1 + amax * c2)) / mcount;
+      const double r = fmax(0.0, fmin(1.0, mua / mu));
+      sigmu = r * r * r * mu;
+    } else {
+      sigmu = 0.0;
+    }
+
+    // ================================ pass 3: backward corrector right side
+    {
+      double phc[NX];
+      for (int i = 0; i < NX; ++i) phc[i] = 0.0;
+      for (int k = N - 1; k >= 0; --k) {
+        double lo[NB], hi[NB], g[NB];
+        load_bounds<T, NX, NU>(a, b, k, lo, hi);
+        for (int j = 0; j < NB; ++j) {
+          const double vj = j < NU ? at(k, L::U + j) : at(k, L::X + j - NU);
+          const double dva = j < NU ? at(k, L::DUA + j) : at(k, L::DXA + j - NU);
+          double s = at(k, L::GA + j);
+          if (fin(lo[j])) {
+            const double sl = vj - lo[j], l = at(k, L::LL + j);
+            s += (-sigmu - dva * l * (1.0 + dva / sl)) / sl;
+          }
+          if (fin(hi[j])) {
+            const double su = hi[j] - vj, l = at(k, L::LU + j);
+            s += (sigmu - dva * l * (1.0 - dva / su)) / su;
+          }
+          g[j] = s;
+        }
+        double P[NX][NX], p[NX], Pe[NX];
+        for (int i = 0; i < NX; ++i)
+          for (int j = 0; j <= i; ++j) P[i][j] = P[j][i] = at(k, L::PP + pk(i, j));
+        for (int i = 0; i < NX; ++i) p[i] = g[NU + i] + phc[i];
+        for (int i = 0; i < NX; ++i) {
+          double s = p[i];
+          for (int j = 0; j < NX; ++j) s = fma(P[i][j], at(k, L::E + j), s);
+          Pe[i] = s;
+        }
+        double h[NU], kk[NU];
+        for (int r = 0; r < NU; ++r) {
+          double s = g[r];
+          for (int i = 0; i < NX; ++i) s = fma(at(k, L::DB + i * NU + r), Pe[i], s);
+          h[r] = s;
+        }
+        for (int r = 0; r < NU; ++r) {
+          double s = 0.0;
+          for (int q = 0; q < NU; ++q) s = fma(at(k, L::GI + pk(r, q)), h[q], s);
+          kk[r] = -s;
+        }
+        // ph = A'Pe + Hx'kk = A'Pe + K'h
+        for (int i = 0; i < NX; ++i) {
+          double s = 0.0;
+          for (int q = 0; q < NX; ++q) s = fma(at(k, L::DA + q * NX + i), Pe[q], s);
+          for (int r = 0; r < NU; ++r) s = fma(at(k, L::KM + r * NX + i), h[r], s);
+          phc[i] = s;
+        }
+        for (int r = 0; r < NU; ++r) at(k, L::KV + r) = kk[r];
+        for (int i = 0; i < NX; ++i) at(k, L::PV + i) = p[i];
+      }
+    }
+
+    // ========================================== pass 4: forward corrector
+    {
+      double dx[NX];
+      for (int i = 0; i < NX; ++i) dx[i] = 0.0;
+      amax = 1.0;
+      for (int k = 0; k < N; ++k) {
+        double du[NU], dxn[NX];
+        for (int r = 0; r < NU; ++r) {
+          double s = at(k, L::KV + r);
+          for (int j = 0; j < NX; ++j) s = fma(at(k, L::KM + r * NX + j), dx[j], s);
+          du[r] = s;
+        }
+        for (int i = 0; i < NX; ++i) {
+          double s = at(k, L::E + i);
+          for (int j = 0; j < NX; ++j) s = fma(at(k, L::DA + i * NX + j), dx[j], s);
+          for (int r = 0; r < NU; ++r) s = fma(at(k, L::DB + i * NU + r), du[r], s);
+          dxn[i] = s;
+        }
+        // dpi_{k+1} = P_{k+1} dx_{k+1} + p_{k+1}
+        for (int i = 0; i < NX; ++i) {
+          double s = at(k, L::PV + i);
+          for (int j = 0; j < NX; ++j) s = fma(at(k, L::PP + pk(i, j)), dxn[j], s);
+          at(k, L::DPI + i) = s;
+        }
+        for (int r = 0; r < NU; ++r) at(k, L::DU + r) = du[r];
+        for (int i = 0; i < NX; ++i) at(k, L::DX + i) = dxn[i];
+        double lo[NB], hi[NB];
+        load_bounds<T, NX, NU>(a, b, k, lo, hi);
+        for (int j = 0; j < NB; ++j) {
+          const double vj = j < NU ? at(k, L::U + j) : at(k, L::X + j - NU);
+          const double dv = j < NU ? du[j] : dxn[j - NU];
+          const double dva = j < NU ? at(k, L::DUA + j) : at(k, L::DXA + j - NU);
+          if (fin(lo[j])) {
+            const double sl = vj - lo[j], l = at(k, L::LL + j);
+            const double dla = -l * (1.0 + dva / sl);
+            const double dl = (sigmu - sl * l - dva * dla - l * dv) / sl;
+            if (dv < 0.0) amax = fmin(amax, -sl / dv);
+            if (dl < 0.0) amax = fmin(amax, -l / dl);
+          }
+          if (fin(hi[j])) {
+            const double su = hi[j] - vj, l = at(k, L::LU + j);
+            const double dua = -l * (1.0 - dva / su);
+            const double dl = (sigmu - su * l + dva * dua + l * dv) / su;
+            if (dv > 0.0) amax = fmin(amax, su / dv);
+            if (dl < 0.0) amax = fmin(amax, -l / dl);
+          }
+        }
+        for (int i = 0; i < NX; ++i) dx[i] = dxn[i];
+      }
+    }
+    // fraction to the boundary.  Fixed, not tightened towards 1 as mu -> 0:
+    // the slacks are differences v - lo, and a slack driven below the rounding
+    // of v would turn Sigma = lam / s into inf
+    alpha = fmin(1.0, 0.995 * amax);
+  }
+
+}
+
+}  // namespace ipm
+}  // namespace mpcqp

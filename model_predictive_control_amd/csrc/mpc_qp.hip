@@ -132,11 +132,22 @@ static int launch_states(int batch, int nx, int nu, int N, int tv, const void* A
 
 }  // namespace mpcqp
 
+// the stage-wise interior point takes the step when the caller asks for it
+// (MPCQP_IPM) or when the condensed QP exceeds the dense kernels' size
+static bool mpc_use_ipm(int dtype, int nx, int nu, int N, int sbox, int flags) {
+  if (!mpcqp::ipm_supported(nx, nu)) return false;
+  if (flags & MPCQP_IPM) return true;
+  return N * (nu + (sbox ? nx : 0)) > mpcqp::max_qp_size_dtype(dtype);
+}
+
 extern "C" size_t mpcqp_mpc_qp_workspace(int dtype, int batch, int nx, int nu, int N,
                                          int state_box) {
   if ((dtype != MPCQP_F64 && dtype != MPCQP_F32) || batch <= 0 || nx < 1 || nu < 1 || N < 1)
     return 0;
-  return mpcqp::mpc_ws_layout(dtype, batch, nx, nu, N, state_box ? 1 : 0).total;
+  const size_t dense = mpcqp::mpc_ws_layout(dtype, batch, nx, nu, N, state_box ? 1 : 0).total;
+  // room for either path (the flags are not known here)
+  const size_t ipm = mpcqp::ipm_supported(nx, nu) ? mpcqp::ipm_ws_bytes(batch, nx, nu, N) : 0;
+  return mpc_use_ipm(dtype, nx, nu, N, state_box ? 1 : 0, 0) ? ipm : (dense > ipm ? dense : ipm);
 }
 
 extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
@@ -160,6 +171,14 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
                   "mpcqp_mpc_qp: negative stride");
   const int sbox = (xlo || xhi) ? 1 : 0;
   const int n = N * nu, m = sbox ? N * nx : 0;
+  if (mpc_use_ipm(dtype, nx, nu, N, sbox, flags)) {
+    if (batch == 0) return MPCQP_OK;
+    return mpc_ipm_impl(dtype, batch, nx, nu, N, flags, A, strideA, Bm, strideB, Q, strideQ, R,
+                        strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi, strideXb, lb,
+                        strideLb, ub, strideUb, nullptr, 0, nullptr, 0, nullptr, 0, z, y, X,
+                        nullptr, nullptr, status, max_iter, tol, ws, ws_bytes,
+                        (hipStream_t)stream);
+  }
   MPCQP_CHECK_ARG(n + m <= max_qp_size_dtype(dtype),
                   "mpcqp_mpc_qp: N*(nu%s) = %d exceeds the QP size limit %d", sbox ? "+nx" : "",
                   n + m, max_qp_size_dtype(dtype));

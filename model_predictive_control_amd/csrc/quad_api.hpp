@@ -60,6 +60,18 @@ int solve_box_wg(int dtype, int batch, int n, const void* H, int64_t sH, const v
                  int32_t* status, int max_iter, double tol, hipStream_t st,
                  const void* Ms = nullptr);
 int max_qp_size_dtype(int dtype);
+
+// ipm.hip: stage-wise interior point (any horizon; nx <= 4, nu <= 2)
+bool ipm_supported(int nx, int nu);
+size_t ipm_ws_bytes(int batch, int nx, int nu, int N);
+int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const void* A,
+                 int64_t sA, const void* Bm, int64_t sB, const void* Q, int64_t sQ, const void* R,
+                 int64_t sR, const void* Qf, int64_t sQf, const void* c, int64_t sC,
+                 const void* x0, int64_t sX0, const void* xlo, const void* xhi, int64_t sXb,
+                 const void* lb, int64_t sLb, const void* ub, int64_t sUb, const void* U0,
+                 int64_t sU0, const void* H2, int64_t sH2, const void* q2, int64_t sq2, void* z,
+                 void* y, void* X, void* lam_u, void* pi, int32_t* status, int max_iter,
+                 double tol, void* ws, size_t ws_bytes, hipStream_t st);
 size_t qp_ws_bytes(int dtype, int batch, int n, int m);
 struct PfDyn;
 // dyn != NULL: refine from the dynamics (pf.hpp); refine < 0: default steps

@@ -1,0 +1,358 @@
+// sqp.hip -- the outer loop of a CONVERGED MPCController.solve: the
+// reference's per-step call hands IPOPT the single-shooting NLP of
+// session_4/main.py:41-113 (session4_sol.py:132-217) and returns its optimum
+// (main.py:115-116).  Here that NLP is solved by SQP on device, batched over
+// initial states; every QP is the stage-wise interior point (ipm.hip), so
+// the horizon is unbounded.  Per iteration:
+//   mpcqp_bicycle_rti      linearise at U            (bicycle.hip)
+//   mpcqp_bicycle_hessian  sum_i pi_i d2 fe_i (exact-Hessian iterations)
+//   mpcqp_mpc_ipm          QP -> Z, state multipliers, costates
+//   mpcqp_bicycle_sqp_step line search on an L1 merit function, update, and
+//                          the first-order optimality (KKT) residual of the
+//                          NLP at the new point -- the stopping test.
+// Far from a solution the QP uses the Gauss-Newton Hessian (positive
+// definite, globally well behaved); once the KKT residual is below 1e-2 the
+// exact Hessian of the Lagrangian takes over (quadratic local convergence),
+// damped Levenberg-Marquardt style by a proximal term mu/2 |w - w_k|^2 per
+// stage: a full step divides mu by 4 (down to 0), a step that needs
+// backtracking or a QP that fails multiplies it by 4 (at least 1e-3).
+#include "bike.hpp"
+
+namespace mpcqp {
+
+constexpr int kSqpDone = 1, kSqpExact = 2;
+constexpr double kSqpSwitch = 1e-2;  // KKT residual below which the exact Hessian is used
+
+__global__ void bike_hess_kernel(int batch, int N, Bike p, const double* X, const double* U,
+                                 const double* pi, const int32_t* flags, const double* mu,
+                                 double* H2, double* q2) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)batch * N) return;
+  const int64_t b = e / N;
+  const int k = (int)(e - b * N);
+  double* H = H2 + e * 36;
+  double* q = q2 + e * 6;
+  const bool exact = flags == nullptr || (flags[b] & kSqpExact);
+  if (!exact) {
+    for (int i = 0; i < 36; ++i) H[i] = 0.0;
+    for (int i = 0; i < 6; ++i) q[i] = 0.0;
+    return;
+  }
+  const double* x = X + (b * (N + 1) + k) * 4;
+  const double* u = U + (b * N + k) * 2;
+  const double* lam = pi + (b * N + k) * 4;  // costate of x_{k+1} = fe(x_k, u_k)
+  const BikePt pt = bike_pt(p, x, u);
+  double Hl[36];
+  bike_lag_hess(p, pt, x, lam, Hl);
+  if (mu)
+    for (int i = 0; i < 6; ++i) Hl[i * 6 + i] += mu[b];
+  const double w[6] = {x[0], x[1], x[2], x[3], u[0], u[1]};
+  // 1/2 (w - wbar)' H (w - wbar) = 1/2 w'H w - (H wbar)'w + const
+  for (int i = 0; i < 6; ++i) {
+    double s = 0.0;
+    for (int j = 0; j < 6; ++j) s = fma(Hl[i * 6 + j], w[j], s);
+    q[i] = -s;
+  }
+  for (int i = 0; i < 36; ++i) H[i] = Hl[i];
+}
+
+struct SqpArgs {
+  int batch, N;
+  Bike p;
+  const double* x0; int64_t sX0;
+  const double *Q, *R, *Qf;
+  const double *xlo, *xhi; int64_t sXb;
+  const double *lb, *ub; int64_t sLb;
+  double* U;
+  const double *Z, *yq, *piq;
+  const int32_t* qp_status;
+  double *y, *pi, *X;
+  double *rho, *kkt, *mu;
+  int32_t* flags;
+  double tol;
+};
+
+// 1/2 J(U) and the l1 violation of the state box along a rollout
+struct Merit {
+  double J, viol;
+};
+
+__device__ double sq_form(const double* M, int n, const double* v) {
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double t = 0.0;
+    for (int j = 0; j < n; ++j) t = fma(M[i * n + j], v[j], t);
+    s = fma(v[i], t, s);
+  }
+  return s;
+}
+
+__device__ double box_viol(const SqpArgs& a, int64_t b, int k, const double* x) {
+  double v = 0.0;
+  for (int i = 0; i < 4; ++i) {
+    const int64_t o = b * a.sXb + (int64_t)k * 4 + i;
+    if (a.xhi) v += fmax(0.0, x[i] - a.xhi[o]);
+    if (a.xlo) v += fmax(0.0, a.xlo[o] - x[i]);
+  }
+  return v;
+}
+
+// rollout of U + alpha d (d = Z - U), merit terms only
+__device__ Merit merit_at(const SqpArgs& a, int64_t b, double alpha) {
+  const int N = a.N;
+  const double* U = a.U + b * N * 2;
+  const double* Z = a.Z + b * N * 2;
+  double x[4];
+  for (int i = 0; i < 4; ++i) x[i] = a.x0[b * a.sX0 + i];
+  Merit m{0.0, 0.0};
+  for (int k = 0; k < N; ++k) {
+    double u[2];
+    for (int r = 0; r < 2; ++r) u[r] = fma(alpha, Z[k * 2 + r] - U[k * 2 + r], U[k * 2 + r]);
+    m.J += 0.5 * (sq_form(a.Q, 4, x) + sq_form(a.R, 2, u));
+    const BikePt pt = bike_pt(a.p, x, u);
+    double xn[4];
+    bike_step(a.p, pt, x, u, xn);
+    for (int i = 0; i < 4; ++i) x[i] = xn[i];
+    m.viol += box_viol(a, b, k, x);
+  }
+  m.J += 0.5 * sq_form(a.Qf, 4, x);
+  return m;
+}
+
+__global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
+  const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (b >= a.batch) return;
+  int fl = a.flags[b];
+  if (fl & kSqpDone) return;
+  const int N = a.N;
+  if (a.qp_status && (a.qp_status[b] & 0xFF) != MPCQP_STATUS_OPTIMAL) {
+    // the QP failed (non-convex beyond the inertia correction, or not
+    // converged): no step; an exact-Hessian iteration falls back to
+    // Gauss-Newton (positive definite) until the residual drops 10x
+    const int iters = ((fl >> 8) & 0xFFFF) + 1;
+    if (fl & kSqpExact) a.mu[b] = fmax(4.0 * a.mu[b], 1e-3);
+    a.flags[b] = (iters << 8) | (fl & kSqpExact);
+    return;
+  }
+  double* U = a.U + b * N * 2;
+  const double* Z = a.Z + b * N * 2;
+  const double* yq = a.yq + b * N * 4;
+  const double* piq = a.piq + b * N * 4;
+  double* y = a.y + b * N * 4;
+  double* pi = a.pi + b * N * 4;
+  double* X = a.X + b * (N + 1) * 4;
+
+  // ----------------------------------------- merit, directional derivative
+  double ymax = 0.0, dmax = 0.0, umax = 0.0;
+  for (int i = 0; i < 4 * N; ++i) ymax = fmax(ymax, fabs(yq[i]));
+  for (int i = 0; i < 2 * N; ++i) {
+    dmax = fmax(dmax, fabs(Z[i] - U[i]));
+    umax = fmax(umax, fabs(U[i]));
+  }
+  const double rho = fmax(a.rho[b], 2.0 * ymax);
+  double D = 0.0;  // d(1/2 J)/dU . d
+  Merit m0{0.0, 0.0};
+  {
+    double x[4], dx[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = 0; i < 4; ++i) x[i] = a.x0[b * a.sX0 + i];
+    for (int k = 0; k < N; ++k) {
+      const double u[2] = {U[2 * k], U[2 * k + 1]};
+      const double d[2] = {Z[2 * k] - u[0], Z[2 * k + 1] - u[1]};
+      m0.J += 0.5 * (sq_form(a.Q, 4, x) + sq_form(a.R, 2, u));
+      for (int i = 0; i < 4; ++i) {
+        double t = 0.0;
+        for (int j = 0; j < 4; ++j) t = fma(a.Q[i * 4 + j], x[j], t);
+        D = fma(t, dx[i], D);
+      }
+      for (int r = 0; r < 2; ++r) {
+        double t = 0.0;
+        for (int q = 0; q < 2; ++q) t = fma(a.R[r * 2 + q], u[q], t);
+        D = fma(t, d[r], D);
+      }
+      const BikePt pt = bike_pt(a.p, x, u);
+      double A[4][4], B[4][2], xn[4], dxn[4];
+      bike_jac(a.p, pt, x, A, B);
+      bike_step(a.p, pt, x, u, xn);
+      for (int i = 0; i < 4; ++i) {
+        double s = B[i][0] * d[0] + B[i][1] * d[1];
+        for (int j = 0; j < 4; ++j) s = fma(A[i][j], dx[j], s);
+        dxn[i] = s;
+      }
+      for (int i = 0; i < 4; ++i) { x[i] = xn[i]; dx[i] = dxn[i]; }
+      m0.viol += box_viol(a, b, k, x);
+    }
+    m0.J += 0.5 * sq_form(a.Qf, 4, x);
+    for (int i = 0; i < 4; ++i) {
+      double t = 0.0;
+      for (int j = 0; j < 4; ++j) t = fma(a.Qf[i * 4 + j], x[j], t);
+      D = fma(t, dx[i], D);
+    }
+  }
+  const double phi0 = m0.J + rho * m0.viol;
+  const double Dm = D - rho * m0.viol;
+
+  // --------------------------- backtracking (quadratic interpolation), Armijo
+  // the acceptance test is relaxed by the rounding noise of phi: near a
+  // solution the predicted decrease (|d| * residual) falls below it and an
+  // exact test would reject every step
+  double alpha = 1.0;
+  const double noise = 1e-14 * (1.0 + fabs(phi0));
+  if (dmax > 1e-14 * (1.0 + umax)) {
+    for (int t = 0; t < 40; ++t) {
+      const Merit m = merit_at(a, b, alpha);
+      const double phi = m.J + rho * m.viol;
+      if (phi <= phi0 + 1e-4 * alpha * Dm + noise) break;
+      const double den = 2.0 * (phi - phi0 - alpha * Dm);
+      const double at = den > 0.0 ? -Dm * alpha * alpha / den : 0.5 * alpha;
+      alpha = fmin(0.5 * alpha, fmax(0.1 * alpha, at));
+      if (alpha < 1e-10) break;
+    }
+  }
+  for (int i = 0; i < 2 * N; ++i) U[i] = fma(alpha, Z[i] - U[i], U[i]);
+  for (int i = 0; i < 4 * N; ++i) {
+    y[i] = fma(alpha, yq[i] - y[i], y[i]);
+    pi[i] = fma(alpha, piq[i] - pi[i], pi[i]);
+  }
+
+  // ------------------------------------------ KKT residual at the new point
+  // gradient of 1/2 J + y'[x_1..x_N] by the adjoint, projected on the input
+  // box; state-box violation; complementarity of the state multipliers
+  {
+    double x[4];
+    for (int i = 0; i < 4; ++i) X[i] = x[i] = a.x0[b * a.sX0 + i];
+    for (int k = 0; k < N; ++k) {
+      const double u[2] = {U[2 * k], U[2 * k + 1]};
+      const BikePt pt = bike_pt(a.p, x, u);
+      double xn[4];
+      bike_step(a.p, pt, x, u, xn);
+      for (int i = 0; i < 4; ++i) X[(k + 1) * 4 + i] = x[i] = xn[i];
+    }
+  }
+  double r = 0.0;
+  {
+    double lam[4];
+    const double* xN = X + N * 4;
+    for (int i = 0; i < 4; ++i) {
+      double s = y[(N - 1) * 4 + i];
+      for (int j = 0; j < 4; ++j) s = fma(a.Qf[i * 4 + j], xN[j], s);
+      lam[i] = s;
+    }
+    for (int k = N - 1; k >= 0; --k) {
+      const double* x = X + k * 4;
+      const double u[2] = {U[2 * k], U[2 * k + 1]};
+      const BikePt pt = bike_pt(a.p, x, u);
+      double A[4][4], B[4][2];
+      bike_jac(a.p, pt, x, A, B);
+      for (int q = 0; q < 2; ++q) {
+        double g = 0.0;
+        for (int j = 0; j < 2; ++j) g = fma(a.R[q * 2 + j], u[j], g);
+        for (int i = 0; i < 4; ++i) g = fma(B[i][q], lam[i], g);
+        const int64_t o = b * a.sLb + (int64_t)k * 2 + q;
+        double t = u[q] - g;
+        if (a.lb) t = fmax(t, a.lb[o]);
+        if (a.ub) t = fmin(t, a.ub[o]);
+        r = fmax(r, fabs(u[q] - t));
+      }
+      // state x_{k+1}: feasibility and complementarity of y_k
+      const double* xk1 = X + (k + 1) * 4;
+      for (int i = 0; i < 4; ++i) {
+        const int64_t o = b * a.sXb + (int64_t)k * 4 + i;
+        const double hi = a.xhi ? a.xhi[o] : Lim<double>::inf();
+        const double lo = a.xlo ? a.xlo[o] : -Lim<double>::inf();
+        const double yi = y[k * 4 + i];
+        r = fmax(r, fmax(xk1[i] - hi, lo - xk1[i]));
+        if (yi > 0.0) r = fmax(r, fmin(yi, hi - xk1[i]));
+        if (yi < 0.0) r = fmax(r, fmin(-yi, xk1[i] - lo));
+      }
+      if (k > 0) {
+        double ln[4];
+        for (int i = 0; i < 4; ++i) {
+          double s = y[(k - 1) * 4 + i];
+          for (int j = 0; j < 4; ++j) s = fma(a.Q[i * 4 + j], x[j], s);
+          for (int j = 0; j < 4; ++j) s = fma(A[j][i], lam[j], s);
+          ln[i] = s;
+        }
+        for (int i = 0; i < 4; ++i) lam[i] = ln[i];
+      }
+    }
+  }
+  if (!(r == r)) r = Lim<double>::inf();
+
+  // ---------------------------------------------------- Hessian mode, flags
+  if (fl & kSqpExact) {
+    double mu = a.mu[b];
+    mu = alpha == 1.0 ? (mu > 4e-12 ? 0.25 * mu : 0.0) : fmax(4.0 * mu, 1e-3);
+    a.mu[b] = mu;
+  }
+  const int iters = ((fl >> 8) & 0xFFFF) + 1;
+  const bool exact = (fl & kSqpExact) || r < kSqpSwitch;  // sticky
+  fl = (iters << 8) | (r <= a.tol ? kSqpDone : 0) | (exact ? kSqpExact : 0);
+  a.flags[b] = fl;
+  a.rho[b] = rho;
+  a.kkt[b] = r;
+}
+
+}  // namespace mpcqp
+
+using mpcqp::Bike;
+
+static Bike bike_of(double ts, const double* prm) {
+  Bike p;
+  p.ts = ts; p.lf = prm[0]; p.lr = prm[1]; p.acc = prm[2]; p.fric = prm[3];
+  return p;
+}
+
+extern "C" int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
+                                     const void* X, const void* U, const void* pi,
+                                     const int32_t* flags, const double* mu, void* H2, void* q2,
+                                     void* stream) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_bicycle_hessian: MPCQP_F64 only");
+  MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "mpcqp_bicycle_hessian: bad sizes");
+  MPCQP_CHECK_ARG(params && X && U && pi && H2 && q2, "mpcqp_bicycle_hessian: null pointer");
+  MPCQP_CHECK_ARG(params[1] > 0 && params[0] + params[1] > 0,
+                  "mpcqp_bicycle_hessian: bad axle lengths");
+  if (batch == 0) return MPCQP_OK;
+  const int64_t total = (int64_t)batch * N;
+  hipLaunchKernelGGL(bike_hess_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, batch, N, bike_of(ts, params), (const double*)X,
+                     (const double*)U, (const double*)pi, flags, mu, (double*)H2, (double*)q2);
+  MPCQP_CHECK_LAUNCH("bike_hess_kernel");
+  return MPCQP_OK;
+}
+
+extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,
+                                      const double* params, const void* x0, int64_t strideX0,
+                                      const void* Q, const void* R, const void* Qf,
+                                      const void* xlo, const void* xhi, int64_t strideXb,
+                                      const void* lb, const void* ub, int64_t strideLb, void* U,
+                                      const void* Z, const void* yq, const void* piq,
+                                      const int32_t* qp_status, void* y, void* pi, void* X,
+                                      double* rho, double* kkt, double* mu, int32_t* flags,
+                                      double tol, void* stream) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_bicycle_sqp_step: MPCQP_F64 only");
+  MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "mpcqp_bicycle_sqp_step: bad sizes");
+  MPCQP_CHECK_ARG(params && x0 && Q && R && Qf && U && Z && yq && piq && y && pi && X && rho &&
+                      kkt && mu && flags,
+                  "mpcqp_bicycle_sqp_step: null pointer");
+  MPCQP_CHECK_ARG(params[1] > 0 && params[0] + params[1] > 0,
+                  "mpcqp_bicycle_sqp_step: bad axle lengths");
+  MPCQP_CHECK_ARG(strideX0 >= 0 && strideXb >= 0 && strideLb >= 0,
+                  "mpcqp_bicycle_sqp_step: negative stride");
+  if (batch == 0) return MPCQP_OK;
+  SqpArgs a;
+  a.batch = batch; a.N = N; a.p = bike_of(ts, params);
+  a.x0 = (const double*)x0; a.sX0 = strideX0;
+  a.Q = (const double*)Q; a.R = (const double*)R; a.Qf = (const double*)Qf;
+  a.xlo = (const double*)xlo; a.xhi = (const double*)xhi; a.sXb = strideXb;
+  a.lb = (const double*)lb; a.ub = (const double*)ub; a.sLb = strideLb;
+  a.U = (double*)U; a.Z = (const double*)Z; a.yq = (const double*)yq; a.piq = (const double*)piq;
+  a.qp_status = qp_status;
+  a.y = (double*)y; a.pi = (double*)pi; a.X = (double*)X;
+  a.rho = rho; a.kkt = kkt; a.mu = mu; a.flags = flags; a.tol = tol > 0 ? tol : 1e-9;
+  hipLaunchKernelGGL(sqp_step_kernel, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0,
+                     (hipStream_t)stream, a);
+  MPCQP_CHECK_LAUNCH("sqp_step_kernel");
+  return MPCQP_OK;
+}

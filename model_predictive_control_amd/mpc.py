@@ -2,25 +2,32 @@
 
 Reference: ``MPCController`` in session_4/main.py:29-129 (and the box-only
 variant session4_sol.py:113-230).  The reference builds a single-shooting
-NLP in CasADi (z = [u_0..u_{N-1}], main.py:46; cost main.py:86-106) and calls
-IPOPT every closed-loop step (``solve`` main.py:115-116, ``__call__``
-main.py:121-129).  Here each ``solve`` is a real-time-iteration SQP step on
-device:
+NLP in CasADi (z = [u_0..u_{N-1}], main.py:46; cost main.py:86-106; input box
+main.py:68-69; state box on x_1..x_N main.py:58-61) and returns IPOPT's
+optimum every closed-loop step (``solve`` main.py:115-116, ``__call__``
+main.py:121-129).  Here ``solve`` returns the optimum of the same NLP, found
+on device by SQP (``mode="sqp"``, the default):
 
-  1.+2. nominal rollout of the forward-Euler model from x0 with the warm-
-     started input sequence (previous solution shifted one stage) and the
-     per-stage linearisation (A_k, B_k, c_k)    (libmpcqp ``mpcqp_bicycle_rti``),
-  3.+4. time-varying condensing and the QP, with the predicted states, in
-     one call                                (libmpcqp ``mpcqp_mpc_qp``),
+  1. linearise the forward-Euler bicycle at the current inputs U
+     (libmpcqp ``mpcqp_bicycle_rti``);
+  2. once the optimality residual is small, the curvature of the dynamics
+     weighted by the costates -- the exact Hessian of the Lagrangian
+     (``mpcqp_bicycle_hessian``); before that, Gauss-Newton;
+  3. the QP on the stage-wise interior point (``mpcqp_mpc_ipm``, any
+     horizon: the reference's own N = 50 controllers of session4_sol.py
+     included);
+  4. an L1-merit line search, the update, and the first-order optimality
+     (KKT) residual of the NLP at the new point (``mpcqp_bicycle_sqp_step``)
+     -- iterations stop when it is below ``tol`` (status OPTIMAL), or at
+     ``max_iter`` (status MAXITER).
 
-repeated ``sqp_iters`` times.  Any number of initial states is solved in one
-batch (``solve`` accepts x of shape (nx,) or (batch, nx)).
+``mode="rti"`` keeps the real-time-iteration scheme: exactly ``sqp_iters``
+linearise + QP steps (``mpcqp_mpc_qp``) from the shifted previous solution,
+no convergence test -- the fixed-cost step of the batched benchmark.
 
-With ``state_box=True`` (default) the state box of main.py:58-61 on x_1..x_N
-is enforced as well (rows  x_min - xbar <= Gam z <= x_max - xbar  of the
-condensed QP; needs N*(nx+nu) <= 192, i.e. N <= 32); without it the QP has
-the input box only.  The
-collision rows of main.py:95-104 are non-convex and out of scope.
+Any number of initial states is solved in one batch (``solve`` accepts x of
+shape (nx,) or (batch, nx)).  The collision rows of main.py:95-104 are
+non-convex and out of scope.
 """
 from __future__ import annotations
 
@@ -31,14 +38,21 @@ import numpy as np
 import torch
 
 from . import batched
+from ._native import SQP_DONE, STATUS_MAXITER, STATUS_OPTIMAL
 from .bicycle import KinematicBicycle
 from .parameters import VehicleParameters
+
+# the weights of the two reference controllers
+WEIGHTS_MAIN = dict(Q=np.diag([1., 6., 0.2, 0.05]), QN_scale=100.0, R=np.diag([1., 0.01]))  # main.py:72-74
+WEIGHTS_SOL = dict(Q=np.diag([1., 3., 0.1, 0.01]), QN_scale=10.0, R=np.diag([1., 1e-2]))    # session4_sol.py:166-169
 
 
 class MPCController:
     def __init__(self, N: int, ts: float, params: VehicleParameters | None = None, model=None,
-                 x_obs=None, *, Q=None, QN=None, R=None, sqp_iters: int = 3,
-                 state_box: bool = True, dtype=torch.float64, device=None) -> None:
+                 x_obs=None, *, Q=None, QN=None, R=None, mode: str = "sqp",
+                 max_iter: int = 200, tol: float = 1e-9, hessian: str = "exact",
+                 sqp_iters: int = 3, state_box: bool = True, dtype=torch.float64,
+                 device=None) -> None:
         self.N = N
         self.ts = ts
         # The prediction model is linearised on device (mpcqp_bicycle_rti),
@@ -58,16 +72,21 @@ class MPCController:
             warnings.warn("MPCController: x_obs is ignored -- the collision rows of "
                           "main.py:95-104 are non-convex and not part of the QP path",
                           stacklevel=2)
+        if mode not in ("sqp", "rti"):
+            raise ValueError(f"mode must be 'sqp' or 'rti', got {mode!r}")
+        if hessian not in ("exact", "gauss-newton"):
+            raise ValueError(f"hessian must be 'exact' or 'gauss-newton', got {hessian!r}")
+        self.mode, self.hessian = mode, hessian
+        self.max_iter, self.tol = int(max_iter), float(tol)
         self.nx, self.nu = 4, 2
-        # weights of main.py:72-74
-        Q = np.diag([1., 6., 0.2, 0.05]) if Q is None else np.asarray(Q, float)
-        QN = 100 * Q if QN is None else np.asarray(QN, float)
-        R = np.diag([1, 0.01]) if R is None else np.asarray(R, float)
-        self.dtype = dtype
+        Q = WEIGHTS_MAIN["Q"] if Q is None else np.asarray(Q, float)
+        QN = WEIGHTS_MAIN["QN_scale"] * Q if QN is None else np.asarray(QN, float)
+        R = WEIGHTS_MAIN["R"] if R is None else np.asarray(R, float)
+        self.dtype = dtype if mode == "rti" else torch.float64  # the SQP runs in fp64
         self.device = device or torch.device("cuda")
         if not torch.cuda.is_available():
             raise RuntimeError("MPCController needs a ROCm GPU (no CPU fallback)")
-        t = lambda a: torch.as_tensor(a, dtype=dtype, device=self.device)  # noqa: E731
+        t = lambda a: torch.as_tensor(a, dtype=self.dtype, device=self.device)  # noqa: E731
         self.Q, self.QN, self.R = t(Q), t(QN), t(R)
         p = self.params
         # input box of main.py:68-69 (drive, steer), repeated over the horizon
@@ -77,8 +96,6 @@ class MPCController:
         # state box of main.py:58-61 on x_1..x_N (the g rows of main.py:99-100)
         self.lb_states, self.ub_states = p.state_box()
         self.state_box = state_box
-        if state_box and N * (self.nx + self.nu) > batched.max_qp_size(dtype):
-            raise ValueError(f"state box needs N*(nx+nu) <= {batched.max_qp_size(dtype)} (N={N})")
         self.xmin = t(np.tile(self.lb_states, N))
         self.xmax = t(np.tile(self.ub_states, N))
         self.bounds = dict(lbx=np.tile(self.lb_inputs, N), ubx=np.tile(self.ub_inputs, N),
@@ -86,26 +103,46 @@ class MPCController:
         self.sqp_iters = sqp_iters
         self._warm = None
         self.last_status = None
+        self.last_kkt = None
+        self.last_iters = None
+
+    @classmethod
+    def from_session4_sol(cls, N: int, ts: float, *, params: VehicleParameters | None = None,
+                          **kw) -> "MPCController":
+        """The controller of session4_sol.py:113-230 (``MPCController(N, ts, *,
+        params)``): its weights Q = diag(1, 3, .1, .01), Q_N = 10 Q,
+        R = diag(1, 1e-2) (session4_sol.py:166-169), input and state box."""
+        Q = WEIGHTS_SOL["Q"]
+        return cls(N, ts, params, Q=Q, QN=WEIGHTS_SOL["QN_scale"] * Q, R=WEIGHTS_SOL["R"], **kw)
 
     # ------------------------------------------------------------- solve
     def solve_batch(self, X0: torch.Tensor):
         """X0 (batch, 4) device tensor -> (z (batch, N*nu), status (batch,))."""
-        N, nu = self.N, self.nu
         X0 = X0.to(self.dtype).contiguous()
-        b = X0.shape[0]
+        if self.mode == "rti":
+            return self._solve_rti(X0)
+        return self._solve_sqp(X0)
+
+    def _warm_start(self, b: int):
         if self._warm is not None and self._warm.shape[0] == b:
-            U = self._warm
-        else:
-            U = torch.zeros((b, N, nu), dtype=self.dtype, device=self.device)
+            return self._warm.clone()
+        return torch.zeros((b, self.N, self.nu), dtype=self.dtype, device=self.device)
+
+    def _box(self):
+        return dict(xlo=self.xmin, xhi=self.xmax) if self.state_box else {}
+
+    def _solve_rti(self, X0):
+        N, nu = self.N, self.nu
+        b = X0.shape[0]
+        U = self._warm_start(b)
         z = status = X = None
         for _ in range(self.sqp_iters):
             # FE rollout from x0 under U + per-stage (A_k, B_k, c_k): one launch
             A, B, c = batched.bicycle_rti(X0, U, self.params, self.ts)
             # condense + QP (+ predicted states) in one libmpcqp call
-            box = dict(xlo=self.xmin, xhi=self.xmax) if self.state_box else {}
             z, lam, status, X = batched.mpc_qp(A, B, self.Q, self.R, self.QN, N, X0, c=c,
                                                lb=self.lbz, ub=self.ubz, tv=True, states=True,
-                                               **box)
+                                               **self._box())
             self.last_lam_g = lam
             U = z.view(b, N, nu)
         # predicted states x_1..x_N of the last linearisation (IPOPT's "g" rows)
@@ -114,8 +151,52 @@ class MPCController:
         self.last_status = status
         return z, status
 
+    def _solve_sqp(self, X0):
+        """SQP to a first-order point of the NLP (module docstring)."""
+        N, nu, dev = self.N, self.nu, self.device
+        b = X0.shape[0]
+        f64 = dict(dtype=torch.float64, device=dev)
+        U = self._warm_start(b)
+        y = torch.zeros((b, N * 4), **f64)
+        pi = torch.zeros((b, N, 4), **f64)
+        X = torch.empty((b, N + 1, 4), **f64)
+        state = dict(rho=torch.zeros(b, **f64), kkt=torch.full((b,), float("inf"), **f64),
+                     mu=torch.full((b,), 0.1, **f64),
+                     flags=torch.zeros(b, dtype=torch.int32, device=dev))
+        box = self._box()
+        exact = self.hessian == "exact"
+        qp_out = None
+        for _ in range(self.max_iter):
+            A, B, c, Xr = batched.bicycle_rti(X0, U, self.params, self.ts, states=True)
+            H2 = q2 = None
+            if exact:
+                H2, q2 = batched.bicycle_hessian(Xr, U, pi, self.params, self.ts,
+                                                 flags=state["flags"], mu=state["mu"])
+            qp_out = batched.mpc_ipm(A, B, self.Q, self.R, self.QN, N, X0, lb=self.lbz,
+                                     ub=self.ubz, c=c, tv=True, H2=H2, q2=q2, out=qp_out, **box)
+            batched.bicycle_sqp_step(X0, U, qp_out["z"], qp_out["y"], qp_out["pi"], y, pi, X,
+                                     state, self.params, self.ts, self.Q, self.R, self.QN,
+                                     xlo=box.get("xlo"), xhi=box.get("xhi"), lb=self.lbz,
+                                     ub=self.ubz, tol=self.tol, qp_status=qp_out["status"])
+            if bool((state["flags"] & SQP_DONE).all()):
+                break
+        done = (state["flags"] & SQP_DONE) != 0
+        iters = (state["flags"] >> 8) & 0xFFFF
+        status = torch.where(done, STATUS_OPTIMAL, STATUS_MAXITER).to(torch.int32) | (iters << 8)
+        self.last_prediction = X[:, 1:]
+        self.last_lam_g = y
+        self.last_costates = pi
+        self.last_kkt = state["kkt"]
+        self.last_iters = iters
+        self._warm = torch.cat([U[:, 1:], U[:, -1:]], 1).contiguous()
+        self.last_status = status
+        return U.reshape(b, N * nu), status
+
     def solve(self, x) -> dict:
-        """main.py:115-116: returns {"x": (N*nu, 1)} (or (batch, N*nu))."""
+        """main.py:115-116: returns {"x": (N*nu, 1)} (or (batch, N*nu)) with
+        "g" (the predicted states x_1..x_N, IPOPT's constraint rows),
+        "lam_g" (state-box multipliers), "status", "success" and, in SQP
+        mode, "kkt" (the NLP optimality residual) and "iterations"."""
         xa = np.asarray(x, dtype=float)
         single = xa.ndim == 1
         X0 = torch.as_tensor(xa.reshape(-1, self.nx), dtype=self.dtype, device=self.device)
@@ -123,18 +204,38 @@ class MPCController:
         zn = z.cpu().numpy()
         st = batched.status_code(status).cpu().numpy()
         g = self.last_prediction.reshape(X0.shape[0], -1).cpu().numpy()
-        return {"x": zn.reshape(-1, 1) if single else zn,
-                "g": g.reshape(-1, 1) if single else g,
-                "status": st[0] if single else st,
-                "success": bool(st[0] == 0) if single else st == 0}
+        lam = self.last_lam_g.reshape(X0.shape[0], -1).cpu().numpy() \
+            if self.last_lam_g is not None else None
+        one = (lambda a: a[0].reshape(-1, 1)) if single else (lambda a: a)  # noqa: E731
+        out = {"x": one(zn), "g": one(g), "status": st[0] if single else st,
+               "success": bool(st[0] == 0) if single else st == 0}
+        if lam is not None:
+            out["lam_g"] = one(lam)
+        if self.mode == "sqp":
+            kkt = self.last_kkt.cpu().numpy()
+            it = self.last_iters.cpu().numpy()
+            out["kkt"] = float(kkt[0]) if single else kkt
+            out["iterations"] = int(it[0]) if single else it
+        return out
 
     def log_step(self, log, sol, x0) -> None:
         """Append one step to a session_2/log.py:8-12 ControllerLog:
-        solver_success, state_prediction (N+1, nx) = [x0; g], input_prediction (N, nu)."""
-        log.solver_success.append(bool(sol["success"]))
-        log.state_prediction.append(np.vstack([np.asarray(x0, float).reshape(1, -1),
-                                               np.asarray(sol["g"]).reshape(-1, self.nx)]))
-        log.input_prediction.append(self.reshape_input(sol))
+        solver_success, state_prediction (N+1, nx) = [x0; g], input_prediction
+        (N, nu).  ``sol`` may be a batch (solve() of (batch, nx)): each field
+        then gets the batch's arrays -- (batch,), (batch, N+1, nx),
+        (batch, N, nu)."""
+        x0 = np.asarray(x0, float)
+        if x0.ndim == 1:
+            log.solver_success.append(bool(sol["success"]))
+            log.state_prediction.append(np.vstack([x0.reshape(1, -1),
+                                                   np.asarray(sol["g"]).reshape(-1, self.nx)]))
+            log.input_prediction.append(self.reshape_input(sol))
+            return
+        b = x0.shape[0]
+        g = np.asarray(sol["g"]).reshape(b, -1, self.nx)
+        log.solver_success.append(np.asarray(sol["success"], bool).reshape(b))
+        log.state_prediction.append(np.concatenate([x0.reshape(b, 1, self.nx), g], 1))
+        log.input_prediction.append(np.asarray(sol["x"]).reshape(b, -1, self.nu))
 
     def reshape_input(self, sol):
         """main.py:118-119."""

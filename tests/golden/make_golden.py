@@ -15,7 +15,10 @@ boxqp_cfg2.npz -- config 2 (double integrator of FHC.py:136-142, N=20,
                  certified by KKT residuals (the reference's own solver,
                  CasADi/IPOPT, is not installed: parity vs IPOPT unpinned).
 vehicle.npz   -- every field of session_4's ``VehicleParameters`` dataclass,
-                 imported from /root/reference/session_4/parameters.py.
+                 read statically (ast) from /root/reference/session_4/parameters.py.
+nlp_s4.npz    -- NLP-optimal inputs of the session-4 MPC step (main.py and
+                 session4_sol.py controllers) from the oracle SQP + Newton
+                 polish (KKT < 1e-11), agreeing with SciPy SLSQP to 1e-5.
 polyqp_s2.npz -- session-2/3 problem data with input box and state box
                  (x_1..x_N), solved by the Goldfarb-Idnani oracle, KKT
                  certified.
@@ -157,17 +160,76 @@ def make_problems():
 
 
 def make_vehicle():
-    import dataclasses
-    import importlib
+    """Field names and defaults of ``VehicleParameters`` read STATICALLY from
+    session_4/parameters.py (ast; nothing of the file is executed): each
+    annotated assignment of the dataclass body, its default evaluated with
+    literal_eval, or as ``2*np.pi`` / ``-2*np.pi`` (the only non-literal
+    defaults)."""
+    import ast
+    import math
 
-    sys.path.insert(0, os.path.join(REF, "session_4"))
-    mod = importlib.import_module("parameters")
-    p = mod.VehicleParameters()
-    out = {f.name: np.array(float(getattr(p, f.name))) for f in dataclasses.fields(p)}
-    out["_field_order"] = np.array([f.name for f in dataclasses.fields(p)])
-    del sys.modules["parameters"]
-    sys.path.pop(0)
+    src = open(os.path.join(REF, "session_4", "parameters.py")).read()
+    cls = next(n for n in ast.parse(src).body
+               if isinstance(n, ast.ClassDef) and n.name == "VehicleParameters")
+    out, order = {}, []
+
+    def value(node):
+        seg = ast.get_source_segment(src, node).replace(" ", "")
+        if seg in ("2*np.pi", "-2*np.pi"):
+            return (-1.0 if seg.startswith("-") else 1.0) * 2.0 * math.pi
+        return float(ast.literal_eval(node))
+
+    for st in cls.body:
+        if isinstance(st, ast.AnnAssign) and isinstance(st.target, ast.Name):
+            out[st.target.id] = np.array(value(st.value))
+            order.append(st.target.id)
+    out["_field_order"] = np.array(order)
     np.savez_compressed(os.path.join(HERE, "vehicle.npz"), **out)
+    return out
+
+
+def make_nlp():
+    """NLP-optimal inputs of the session-4 MPC step (the NLP IPOPT solves in
+    MPCController.solve, main.py:115-116, without the non-convex collision
+    rows; session4_sol.py:132-217 exactly) for the two reference
+    controllers, from oracle/nlp.py (SQP + Newton polish, KKT-certified) and
+    cross-checked against SciPy SLSQP on the same NLP: only initial states
+    where the two agree to 1e-5 (the same local optimum) are kept.
+      main: N = 30, ts = 0.08, weights main.py:72-74, x0 of main.py:248 + 4 seeded
+      sol:  N = 50, ts = 0.05, weights session4_sol.py:166-169, x0 of
+            session4_sol.py:344 + 2 seeded"""
+    from oracle import nlp
+
+    xlo = np.array([-3.0, -2.0, -2 * np.pi, -0.5])
+    lbu = np.array([-1.0, -0.384])
+    Qm, Qs = np.diag([1., 6., .2, .05]), np.diag([1., 3., .1, .01])
+    cases = {"main": (30, 0.08, Qm, 100 * Qm, np.diag([1., .01]), [0.3, -0.1, 0.0, 0.0], 4),
+             "sol": (50, 0.05, Qs, 10 * Qs, np.diag([1., 1e-2]), [0.6, -0.25, 0.0, 0.0], 2)}
+    out = {}
+    rng = np.random.default_rng(20261015 + 40)
+    for tag, (N, ts, Q, QN, R, xref, nrand) in cases.items():
+        ocp = nlp.OCP(N, ts, Q, QN, R, xlo, -xlo, lbu, -lbu)
+        cand = [np.array(xref)] + [np.array([rng.uniform(-.8, .8), rng.uniform(-.4, .4),
+                                             rng.uniform(-.5, .5), rng.uniform(-.2, .2)])
+                                   for _ in range(2 * nrand)]
+        X0, Us, Ys, Xs, K, J, Usl = [], [], [], [], [], [], []
+        for x0 in cand:
+            U, y, k = ocp.solve(x0)
+            Usq, _ = ocp.solve_slsqp(x0)
+            if k > 1e-11 or np.abs(U - Usq).max() > 1e-5:
+                continue
+            X0.append(x0); Us.append(U); Ys.append(y); Xs.append(ocp.rollout(x0, U)); K.append(k)
+            J.append(ocp.cost(x0, U)); Usl.append(Usq)
+            if len(X0) == nrand + 1:
+                break
+        assert len(X0) == nrand + 1, (tag, len(X0))
+        out.update({f"{tag}_N": np.array(N), f"{tag}_ts": np.array(ts), f"{tag}_Q": Q,
+                    f"{tag}_QN": QN, f"{tag}_R": R, f"{tag}_x0": np.array(X0),
+                    f"{tag}_U": np.array(Us), f"{tag}_y": np.array(Ys), f"{tag}_X": np.array(Xs),
+                    f"{tag}_kkt": np.array(K), f"{tag}_J": np.array(J),
+                    f"{tag}_U_slsqp": np.array(Usl)})
+    out["xlo"], out["lbu"] = xlo, lbu
+    np.savez_compressed(os.path.join(HERE, "nlp_s4.npz"), **out)
     return out
 
 
@@ -224,9 +286,16 @@ def make_polyqp_s2(pr):
 
 
 if __name__ == "__main__":
-    s1 = make_session1()
-    pr = make_problems()
-    make_vehicle()
-    make_boxqp_cfg2(s1)
-    make_polyqp_s2(pr)
+    only = sys.argv[1:]
+    if not only or "session1" in only:
+        s1 = make_session1()
+    if not only or "problems" in only:
+        pr = make_problems()
+    if not only or "vehicle" in only:
+        make_vehicle()
+    if not only:
+        make_boxqp_cfg2(s1)
+        make_polyqp_s2(pr)
+    if not only or "nlp" in only:
+        make_nlp()
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

@@ -191,16 +191,19 @@ def test_mpc_qp_shared_plant_and_bounds(dev):
 
 
 def test_mpc_qp_errors(dev):
-    A = torch.eye(2, dtype=torch.float64, device=dev)
-    B = torch.ones((2, 1), dtype=torch.float64, device=dev)
-    Q = torch.eye(2, dtype=torch.float64, device=dev)
+    # nx = 5: outside the stage-wise interior point's set (nx <= 4), so a
+    # horizon beyond the dense kernels' size has no path and must raise
+    nx = 5
+    A = torch.eye(nx, dtype=torch.float64, device=dev)
+    B = torch.ones((nx, 1), dtype=torch.float64, device=dev)
+    Q = torch.eye(nx, dtype=torch.float64, device=dev)
     R = torch.eye(1, dtype=torch.float64, device=dev)
-    x0 = torch.zeros((3, 2), dtype=torch.float64, device=dev)
+    x0 = torch.zeros((3, nx), dtype=torch.float64, device=dev)
     with pytest.raises(ValueError):
         batched.mpc_qp(A, B, Q, R, Q, 10, x0, xlo=torch.zeros(7, dtype=torch.float64, device=dev))
     from model_predictive_control_amd._native import MpcqpError
     with pytest.raises(MpcqpError):  # N*(nu+nx) beyond the QP size limit
-        batched.mpc_qp(A, B, Q, R, Q, 400, x0, xlo=-torch.ones(2, dtype=torch.float64, device=dev))
+        batched.mpc_qp(A, B, Q, R, Q, 400, x0, xlo=-torch.ones(nx, dtype=torch.float64, device=dev))
 
 
 @pytest.mark.parametrize("dt,tol", [(torch.float64, 1e-10)])

@@ -1,0 +1,137 @@
+"""GPU parity: the CONVERGED MPCController.solve (SQP on device: bicycle_rti
+-> bicycle_hessian -> mpc_ipm -> bicycle_sqp_step) against the NLP-optimal
+fixtures of tests/golden/nlp_s4.npz -- the optimum of the NLP IPOPT solves in
+the reference's MPCController.solve (session_4/main.py:115-116 on the OCP of
+main.py:41-113 without the non-convex collision rows; session4_sol.py:132-217
+exactly), from oracle/nlp.py (SQP + Newton polish, KKT < 1e-11) and agreeing
+with SciPy SLSQP.  The bicycle ODE itself is the build's restatement
+(rcracers is absent): parity of the model is unpinned, parity of the
+optimiser on that model is what these tests pin."""
+import numpy as np
+import pytest
+import torch
+
+from model_predictive_control_amd import batched
+from model_predictive_control_amd.mpc import MPCController
+from model_predictive_control_amd.parameters import VehicleParameters
+from oracle import nlp
+
+pytestmark = pytest.mark.gpu
+
+TOL_U = 1e-7      # the fixtures are KKT points to 1e-11; the bar is 1e-5
+TOL_KKT = 1e-8
+
+
+def _ocp(g, tag):
+    xlo, lbu = g["xlo"], g["lbu"]
+    return nlp.OCP(int(g[f"{tag}_N"]), float(g[f"{tag}_ts"]), g[f"{tag}_Q"], g[f"{tag}_QN"],
+                   g[f"{tag}_R"], xlo, -xlo, lbu, -lbu)
+
+
+def _controller(g, tag):
+    N, ts = int(g[f"{tag}_N"]), float(g[f"{tag}_ts"])
+    if tag == "sol":  # session4_sol.py:342,455: MPCController(N=50, ts=0.05, params=...)
+        return MPCController.from_session4_sol(N, ts, params=VehicleParameters())
+    return MPCController(N, ts, VehicleParameters())  # main.py:242-251 weights and box
+
+
+@pytest.mark.parametrize("tag", ["main", "sol"])
+def test_solve_matches_nlp_fixtures(golden, tag):
+    """One solve per fixture x0 (the reference's single-x0 call surface):
+    u within 1e-7 of the NLP optimum, status optimal, NLP KKT residual (the
+    device's and the oracle's evaluation of it) below 1e-8."""
+    g = golden("nlp_s4.npz")
+    ocp = _ocp(g, tag)
+    X0, Ustar = g[f"{tag}_x0"], g[f"{tag}_U"]
+    for i, x0 in enumerate(X0):
+        ctl = _controller(g, tag)
+        sol = ctl.solve(x0)
+        U = np.asarray(sol["x"]).reshape(-1)
+        assert sol["success"], (i, sol["status"], sol["kkt"], sol["iterations"])
+        assert sol["kkt"] < TOL_KKT, (i, sol["kkt"])
+        err = np.abs(U - Ustar[i]).max()
+        assert err < TOL_U, (i, err)
+        # the oracle's own evaluation of first-order optimality at (U, lam_g)
+        assert ocp.kkt(x0, U, np.asarray(sol["lam_g"]).reshape(-1)) < 10 * TOL_KKT
+        # g: the predicted states x_1..x_N along the solution
+        assert np.abs(np.asarray(sol["g"]).reshape(-1, 4) - g[f"{tag}_X"][i][1:]).max() < 1e-6
+        # __call__ (main.py:121-129) returns u_0 of a fresh solve
+        u0 = _controller(g, tag)(x0)
+        assert np.abs(u0 - Ustar[i][:2]).max() < TOL_U
+
+
+@pytest.mark.parametrize("tag", ["main", "sol"])
+def test_batched_solve_equals_single(golden, tag):
+    """All fixture x0 in one batched call: the same optimum per instance."""
+    g = golden("nlp_s4.npz")
+    X0, Ustar = g[f"{tag}_x0"], g[f"{tag}_U"]
+    sol = _controller(g, tag).solve(X0)
+    assert np.asarray(sol["success"]).all(), (sol["status"], sol["kkt"])
+    assert np.abs(np.asarray(sol["x"]) - Ustar).max() < TOL_U
+    assert (np.asarray(sol["kkt"]) < TOL_KKT).all()
+
+
+def test_n50_state_box_controller_runs(golden):
+    """session4_sol.py:342 exercise3 exactly: N = 50, ts = 0.05, x0 =
+    [0.6, -0.25, 0, 0] with the state box (n + m = 300: the case the dense
+    kernels' 192 cap refused)."""
+    g = golden("nlp_s4.npz")
+    ctl = MPCController.from_session4_sol(50, 0.05, params=VehicleParameters())
+    sol = ctl.solve(np.array([0.6, -0.25, 0.0, 0.0]))
+    assert sol["success"] and sol["kkt"] < TOL_KKT
+    assert np.abs(ctl.reshape_input(sol) - g["sol_U"][0].reshape(-1, 2)).max() < TOL_U
+
+
+def test_hessian_kernel_vs_oracle(dev):
+    """mpcqp_bicycle_hessian (analytic second derivatives, bike.hpp) against
+    the oracle's complex-step + central-difference curvature."""
+    p = VehicleParameters()
+    rng = np.random.default_rng(21)
+    b, N, ts = 3, 5, 0.08
+    X = rng.normal(size=(b, N + 1, 4)) * [1, 1, 1, 0.3]
+    U = rng.uniform(-0.35, 0.35, (b, N, 2))
+    pi = rng.normal(size=(b, N, 4)) * 10
+    t = lambda a: torch.as_tensor(a, dtype=torch.float64, device=dev)  # noqa: E731
+    H2, q2 = batched.bicycle_hessian(t(X), t(U), t(pi), p, ts)
+    torch.cuda.synchronize()
+    H2, q2 = H2.cpu().numpy(), q2.cpu().numpy()
+    for i in range(b):
+        for k in range(N):
+            w = np.concatenate([X[i, k], U[i, k]])
+            L = nlp._stage_curvature(w, pi[i, k], ts, nlp.PARAMS)
+            assert np.abs(H2[i, k] - L).max() < 1e-6 * (1 + np.abs(L).max())
+            assert np.abs(q2[i, k] + H2[i, k] @ w).max() < 1e-12 * (1 + np.abs(q2[i, k]).max())
+
+
+def test_gauss_newton_mode_and_rti_mode(golden):
+    """hessian='gauss-newton' converges to the same optimum (more
+    iterations); mode='rti' keeps the fixed-iteration scheme (no KKT)."""
+    g = golden("nlp_s4.npz")
+    x0, Ustar = g["main_x0"][0], g["main_U"][0]
+    gn = MPCController(30, 0.08, VehicleParameters(), hessian="gauss-newton", max_iter=400,
+                       tol=1e-8)
+    s1 = gn.solve(x0)
+    ex = MPCController(30, 0.08, VehicleParameters())
+    s2 = ex.solve(x0)
+    assert s1["success"] and s2["success"]
+    assert s2["iterations"] < s1["iterations"]
+    assert np.abs(np.asarray(s1["x"]).reshape(-1) - Ustar).max() < 1e-5
+    rti = MPCController(30, 0.08, VehicleParameters(), mode="rti", sqp_iters=3)
+    s3 = rti.solve(x0)
+    assert "kkt" not in s3 and np.asarray(s3["x"]).shape == (60, 1)
+
+
+def test_receding_horizon_warm_start(golden):
+    """Consecutive solves along the closed loop (main.py:270-271) start from
+    the shifted previous solution and need fewer iterations than a cold
+    start; every step converges."""
+    g = golden("nlp_s4.npz")
+    ctl = MPCController(30, 0.08, VehicleParameters())
+    x = g["main_x0"][0].copy()
+    its = []
+    for _ in range(5):
+        sol = ctl.solve(x)
+        assert sol["success"] and sol["kkt"] < TOL_KKT
+        its.append(sol["iterations"])
+        x = nlp.fe(x, ctl.reshape_input(sol)[0], 0.08)
+    assert max(its[1:]) < its[0], its
