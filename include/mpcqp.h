@@ -373,6 +373,33 @@ int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts, const double*
                            double* kkt, double* mu, int32_t* flags, double tol, void* stream);
 
 /*
+ * The receding-horizon loop on device (rcracers.simulate(x0, dynamics,
+ * n_steps, policy=controller), session_4/main.py:270-271; session4_sol.py:
+ * 458,465), one step of it per call pair:
+ * mpcqp_bicycle_plant: x_next = F(x, u) with u = U[b][0..1] (instance stride
+ *   strideU: the first input of each instance's solution, __call__
+ *   main.py:121-129), F = MPCQP_PLANT_FE (fwd_euler, main.py:132-135),
+ *   MPCQP_PLANT_RK4 (runge_kutta4, main.py:138-147) or MPCQP_PLANT_RK4_SUB
+ *   (RK4 over `substeps` sub-intervals: the stand-in for odeint,
+ *   exact_integration main.py:150-170) with the PLANT's parameters (which
+ *   may differ from the controller's, session4_sol.py:461-462); u_rec
+ *   (optional, 2 per instance) records u.  x, x_next: 4 per instance.
+ * mpcqp_sqp_shift: warm start of the next step -- U (N x 2), y, pi (N x 4)
+ *   move one stage forward (last stage repeated; NULL = skip) and the SQP
+ *   state restarts (flags 0, rho 0, mu = mu0, kkt = inf; NULL = skip).
+ * Both are plain launches on the stream, so a T-step loop of
+ * (MPC step; plant; shift) can be captured in one HIP graph.  fp64.
+ */
+#define MPCQP_PLANT_FE 0
+#define MPCQP_PLANT_RK4 1
+#define MPCQP_PLANT_RK4_SUB 2
+int mpcqp_bicycle_plant(int dtype, int batch, double ts, const double* params, int integrator,
+                        int substeps, const void* x, const void* U, int64_t strideU,
+                        void* x_next, void* u_rec, void* stream);
+int mpcqp_sqp_shift(int dtype, int batch, int N, void* U, void* y, void* pi, int32_t* flags,
+                    double* rho, double* mu, double* kkt, double mu0, void* stream);
+
+/*
  * Batched finite-horizon Riccati recursion, FHC.py:51-61:
  *   K_k = -(R + B'P B)^{-1} B'P A,  P_k = Q + A'P A + A'P B K_k,  P_N = Pf
  * Outputs in the reference's order (lists reversed: K[0] is the first-stage

@@ -22,6 +22,9 @@ IPM = 2
 STATUS_POLISHED = 1 << 24
 SQP_DONE = 1
 SQP_EXACT = 2
+PLANT_FE = 0
+PLANT_RK4 = 1
+PLANT_RK4_SUB = 2
 
 STATUS_OPTIMAL = 0
 STATUS_MAXITER = 1
@@ -80,6 +83,9 @@ SIGNATURES = {
     "mpcqp_bicycle_sqp_step": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _i64,
                                     _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _vp]),
+    "mpcqp_bicycle_plant": (_i, [_i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _i, _vp, _vp,
+                                 _i64, _vp, _vp, _vp]),
+    "mpcqp_sqp_shift": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _vp]),
     "mpcqp_riccati": (_i, [_i, _i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                            _vp, _i64, _vp, _vp, _vp]),
     "mpcqp_bicycle_rti": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _i64, _vp, _i64,

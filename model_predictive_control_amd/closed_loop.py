@@ -1,0 +1,167 @@
+"""The receding-horizon loop on device.
+
+Reference: ``simulate(x0, dynamics, n_steps, policy=controller)`` of the
+course package (rcracers, main.py:270-271; session4_sol.py:458,465): every
+step calls ``MPCController.__call__`` (main.py:121-129) -- a full NLP solve --
+and advances the plant (``exact_integration``/``fwd_euler``, main.py:132-170)
+with the first input.  ``mpc.simulate`` restates that host loop; here the
+whole loop stays on the GPU for a batch of initial states:
+
+  per step t:  MPC solve (SQP iterations or RTI steps, no host sync)
+               -> plant x_{t+1} = F(x_t, u_t)   (libmpcqp ``mpcqp_bicycle_plant``)
+               -> warm start: shift U, y, pi    (``mpcqp_sqp_shift``)
+
+and the T steps are captured once in a HIP graph and replayed.  The plant
+may use its own parameters (the friction mismatch of session4_sol.py:
+461-462) and integrator (FE, RK4, or RK4 with sub-steps as the stand-in for
+odeint).  The per-step ``ControllerLog`` fields (session_2/log.py:8-12) are
+recorded batched: solver_success (T, b), state_prediction (T, b, N+1, 4),
+input_prediction (T, b, N, 2).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as nat
+from . import batched
+from .mpc import MPCController
+from .parameters import VehicleParameters
+
+PLANTS = {"fe": nat.PLANT_FE, "rk4": nat.PLANT_RK4, "exact": nat.PLANT_RK4_SUB}
+
+
+class ClosedLoop:
+    """Batched closed loop of ``controller`` on a kinematic-bicycle plant.
+
+    ``controller.mode == "sqp"``: each step runs ``iters_per_step`` SQP
+    iterations from the shifted previous solution (instances that reach the
+    KKT tolerance earlier are frozen by the step kernel); ``"rti"``: each
+    step runs the controller's ``sqp_iters`` linearise + QP steps.
+    """
+
+    def __init__(self, controller: MPCController, plant: str = "fe",
+                 plant_params: VehicleParameters | None = None, substeps: int = 20,
+                 iters_per_step: int = 10, graph: bool = True):
+        if plant not in PLANTS:
+            raise ValueError(f"plant must be one of {sorted(PLANTS)}, got {plant!r}")
+        self.ctl = controller
+        self.plant = PLANTS[plant]
+        self.plant_params = plant_params or controller.params
+        self.substeps = int(substeps)
+        self.iters = int(iters_per_step)
+        self.graph = graph
+        self._graphs: dict = {}
+
+    # ----------------------------------------------------------- buffers
+    def _alloc(self, b: int, T: int):
+        ctl, N, dev = self.ctl, self.ctl.N, self.ctl.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        s = dict(
+            xs=torch.zeros((T + 1, b, 4), **f64), us=torch.zeros((T, b, 2), **f64),
+            U=torch.zeros((b, N, 2), **f64), y=torch.zeros((b, N * 4), **f64),
+            pi=torch.zeros((b, N, 4), **f64), X=torch.zeros((b, N + 1, 4), **f64),
+            rho=torch.zeros(b, **f64), kkt=torch.full((b,), float("inf"), **f64),
+            mu=torch.full((b,), 0.1, **f64),
+            flags=torch.zeros(b, dtype=torch.int32, device=dev),
+            success=torch.zeros((T, b), dtype=torch.bool, device=dev),
+            iters=torch.zeros((T, b), dtype=torch.int32, device=dev),
+            state_prediction=torch.zeros((T, b, N + 1, 4), **f64),
+            input_prediction=torch.zeros((T, b, N, 2), **f64))
+        s["qp"] = None
+        return s
+
+    # ------------------------------------------------------------ one step
+    def _mpc(self, s, t):
+        ctl, N = self.ctl, self.ctl.N
+        x0 = s["xs"][t]
+        box = ctl._box()
+        if ctl.mode == "rti":
+            U = s["U"]
+            for _ in range(ctl.sqp_iters):
+                A, B, c = batched.bicycle_rti(x0, U, ctl.params, ctl.ts)
+                z, _, st, X = batched.mpc_qp(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, c=c, lb=ctl.lbz,
+                                             ub=ctl.ubz, tv=True, states=True, **box)
+                U.copy_(z.view_as(U))
+            s["X"][:, 0].copy_(x0)
+            s["X"][:, 1:].copy_(X)
+            s["success"][t].copy_(batched.status_code(st) == 0)
+            return
+        for _ in range(self.iters):
+            A, B, c, Xr = batched.bicycle_rti(x0, s["U"], ctl.params, ctl.ts, states=True)
+            H2 = q2 = None
+            if ctl.hessian == "exact":
+                H2, q2 = batched.bicycle_hessian(Xr, s["U"], s["pi"], ctl.params, ctl.ts,
+                                                 flags=s["flags"], mu=s["mu"])
+            s["qp"] = batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, lb=ctl.lbz, ub=ctl.ubz,
+                                      c=c, tv=True, H2=H2, q2=q2, out=s["qp"], **box)
+            batched.bicycle_sqp_step(x0, s["U"], s["qp"]["z"], s["qp"]["y"], s["qp"]["pi"],
+                                     s["y"], s["pi"], s["X"], s, ctl.params, ctl.ts, ctl.Q, ctl.R,
+                                     ctl.QN, xlo=box.get("xlo"), xhi=box.get("xhi"), lb=ctl.lbz,
+                                     ub=ctl.ubz, tol=ctl.tol, qp_status=s["qp"]["status"])
+        s["success"][t].copy_((s["flags"] & nat.SQP_DONE) != 0)
+        s["iters"][t].copy_((s["flags"] >> 8) & 0xFFFF)
+
+    def _step(self, s, t):
+        ctl = self.ctl
+        b = s["U"].shape[0]
+        self._mpc(s, t)
+        # ControllerLog of the step: [x_t; predicted states], the input plan
+        s["state_prediction"][t].copy_(s["X"])
+        s["input_prediction"][t].copy_(s["U"])
+        p = self.plant_params
+        prm = batched._bike_params(p)
+        lib = nat.load()
+        rc = lib.mpcqp_bicycle_plant(nat.F64, b, float(ctl.ts), prm, self.plant, self.substeps,
+                                     s["xs"][t].data_ptr(), s["U"].data_ptr(), 2 * ctl.N,
+                                     s["xs"][t + 1].data_ptr(), s["us"][t].data_ptr(),
+                                     batched._stream())
+        nat.check(rc, "mpcqp_bicycle_plant")
+        rc = lib.mpcqp_sqp_shift(nat.F64, b, ctl.N, s["U"].data_ptr(), s["y"].data_ptr(),
+                                 s["pi"].data_ptr(), s["flags"].data_ptr(), s["rho"].data_ptr(),
+                                 s["mu"].data_ptr(), s["kkt"].data_ptr(), 0.1, batched._stream())
+        nat.check(rc, "mpcqp_sqp_shift")
+
+    # ---------------------------------------------------------------- run
+    def run(self, X0, steps: int) -> dict:
+        """X0 (b, 4) -> dict of device tensors: xs (T+1, b, 4), us (T, b, 2),
+        success (T, b), iters (T, b) (SQP iterations per step; 0 in RTI mode),
+        state_prediction (T, b, N+1, 4), input_prediction (T, b, N, 2)."""
+        X0 = torch.as_tensor(X0, dtype=torch.float64, device=self.ctl.device).reshape(-1, 4)
+        b, T = X0.shape[0], int(steps)
+        key = (b, T)
+        if self.graph:
+            g = self._graphs.get(key)
+            if g is None:
+                s = self._alloc(b, T)
+                s["xs"][0].copy_(X0)
+                # warm up (allocations, workspaces, kernel loading) off the graph
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    self._step(s, 0)
+                torch.cuda.current_stream().wait_stream(side)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    self._reset(s)
+                    for t in range(T):
+                        self._step(s, t)
+                g = self._graphs[key] = (graph, s)
+            graph, s = g
+            s["xs"][0].copy_(X0)
+            graph.replay()
+        else:
+            s = self._alloc(b, T)
+            s["xs"][0].copy_(X0)
+            for t in range(T):
+                self._step(s, t)
+        return {k: s[k] for k in ("xs", "us", "success", "iters", "state_prediction",
+                                  "input_prediction")}
+
+    def _reset(self, s):
+        s["U"].zero_()
+        s["y"].zero_()
+        s["pi"].zero_()
+        s["flags"].zero_()
+        s["rho"].zero_()
+        s["mu"].fill_(0.1)
+        s["kkt"].fill_(float("inf"))

@@ -697,14 +697,19 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
     // tolerance; a bound the fp32 active set left within a.tol of violation
     // (invisible to it, but amplified by ill-conditioning) re-enters the
     // active set, and the refinement runs again
-    float tolc = a.tol;
+    // Only the first scan of a round >= 1 sees refined values; every later
+    // scan follows refresh() or fp32 active-set steps and keeps a.tol (the
+    // fp32 floor would show as spurious violations of kDynTol)
     for (int round = 0; round < (NXP > 0 ? 3 : 1); ++round) {
     bool active = true;
+    bool tight = round > 0;
     for (int pass = 0; pass < 3 && active; ++pass) {
       while (true) {
         float viol;
         int p;
         scan(viol, p);
+        const float tolc = tight ? kDynTol : a.tol;
+        tight = false;
         if (!(viol > tolc)) break;
         const float valp0 = pick<NR>(val, p);
         float valp = valp0;
@@ -878,7 +883,7 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
         float viol;
         int p;
         scan(viol, p);
-        active = viol > tolc;
+        active = viol > a.tol;
       }
     }
     if (active) code = MPCQP_STATUS_MAXITER;
@@ -1040,7 +1045,6 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
       scan(viol, p);
       MPCQP_PHASE_D(6);
       if (!(viol > kDynTol) || code != MPCQP_STATUS_OPTIMAL) break;
-      tolc = kDynTol;
     } else {
       break;
     }

@@ -292,6 +292,88 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
   a.kkt[b] = r;
 }
 
+// -------------------------------------------------- receding-horizon loop
+// The plant of the closed loop (rcracers.simulate(x0, dynamics, n_steps,
+// policy), main.py:270-271; session4_sol.py:458,465): x_{t+1} = F(x_t, u_t)
+// with u_t = U[0] (the first input of the step's solution, __call__
+// main.py:121-129) and F one of
+//   0: forward Euler (fwd_euler, main.py:132-135)
+//   1: RK4 (runge_kutta4, main.py:138-147)
+//   2: RK4 over `substeps` sub-intervals -- the stand-in for odeint
+//      (exact_integration, main.py:150-170)
+// with the plant's own parameters (e.g. friction x 0.8, session4_sol.py:
+// 461-462).  One lane per instance; writes x_{t+1} and records u_t.
+__device__ void bike_f(const Bike& p, const double* x, const double* u, double* f) {
+  const double kk = p.k();
+  const double beta = atan(kk * tan(u[1]));
+  double s, c;
+  sincos(x[2] + beta, &s, &c);
+  f[0] = x[3] * c;
+  f[1] = x[3] * s;
+  f[2] = x[3] / p.lr * sin(beta);
+  f[3] = p.acc * u[0] - p.fric * x[3];
+}
+
+__device__ void bike_rk4(const Bike& p, double h, const double* x, const double* u, double* xn) {
+  double k1[4], k2[4], k3[4], k4[4], t[4];
+  bike_f(p, x, u, k1);
+  for (int i = 0; i < 4; ++i) t[i] = x[i] + 0.5 * h * k1[i];
+  bike_f(p, t, u, k2);
+  for (int i = 0; i < 4; ++i) t[i] = x[i] + 0.5 * h * k2[i];
+  bike_f(p, t, u, k3);
+  for (int i = 0; i < 4; ++i) t[i] = x[i] + h * k3[i];
+  bike_f(p, t, u, k4);
+  for (int i = 0; i < 4; ++i) xn[i] = x[i] + h / 6.0 * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
+}
+
+__global__ void plant_kernel(int batch, Bike p, int integrator, int substeps, const double* x,
+                             const double* U, int64_t sU, double* xn, double* u_rec) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  double xs[4], u[2] = {U[(int64_t)b * sU], U[(int64_t)b * sU + 1]};
+  for (int i = 0; i < 4; ++i) xs[i] = x[(int64_t)b * 4 + i];
+  if (integrator == 0) {
+    double f[4];
+    bike_f(p, xs, u, f);
+    for (int i = 0; i < 4; ++i) xs[i] += p.ts * f[i];
+  } else {
+    const int m = integrator == 1 ? 1 : substeps;
+    const double h = p.ts / m;
+    for (int s = 0; s < m; ++s) {
+      double t[4];
+      bike_rk4(p, h, xs, u, t);
+      for (int i = 0; i < 4; ++i) xs[i] = t[i];
+    }
+  }
+  for (int i = 0; i < 4; ++i) xn[(int64_t)b * 4 + i] = xs[i];
+  if (u_rec) {
+    u_rec[(int64_t)b * 2] = u[0];
+    u_rec[(int64_t)b * 2 + 1] = u[1];
+  }
+}
+
+// Warm start of the next receding-horizon step: every per-stage array moves
+// one stage forward (the last stage repeated) and the SQP state restarts.
+__global__ void sqp_shift_kernel(int batch, int N, double* U, double* y, double* pi,
+                                 int32_t* flags, double* rho, double* mu, double* kkt,
+                                 double mu0) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  auto shift = [&](double* a, int w) {
+    if (!a) return;
+    double* r = a + (int64_t)b * N * w;
+    for (int k = 0; k + 1 < N; ++k)
+      for (int j = 0; j < w; ++j) r[k * w + j] = r[(k + 1) * w + j];
+  };
+  shift(U, 2);
+  shift(y, 4);
+  shift(pi, 4);
+  if (flags) flags[b] = 0;
+  if (rho) rho[b] = 0.0;
+  if (mu) mu[b] = mu0;
+  if (kkt) kkt[b] = Lim<double>::inf();
+}
+
 }  // namespace mpcqp
 
 using mpcqp::Bike;
@@ -354,5 +436,38 @@ extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,
   hipLaunchKernelGGL(sqp_step_kernel, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0,
                      (hipStream_t)stream, a);
   MPCQP_CHECK_LAUNCH("sqp_step_kernel");
+  return MPCQP_OK;
+}
+
+extern "C" int mpcqp_bicycle_plant(int dtype, int batch, double ts, const double* params,
+                                   int integrator, int substeps, const void* x, const void* U,
+                                   int64_t strideU, void* x_next, void* u_rec, void* stream) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_bicycle_plant: MPCQP_F64 only");
+  MPCQP_CHECK_ARG(batch >= 0 && strideU >= 2, "mpcqp_bicycle_plant: bad sizes");
+  MPCQP_CHECK_ARG(integrator >= 0 && integrator <= 2 && (integrator != 2 || substeps >= 1),
+                  "mpcqp_bicycle_plant: integrator %d / substeps %d", integrator, substeps);
+  MPCQP_CHECK_ARG(params && x && U && x_next, "mpcqp_bicycle_plant: null pointer");
+  MPCQP_CHECK_ARG(params[1] > 0 && params[0] + params[1] > 0,
+                  "mpcqp_bicycle_plant: bad axle lengths");
+  if (batch == 0) return MPCQP_OK;
+  hipLaunchKernelGGL(plant_kernel, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     batch, bike_of(ts, params), integrator, substeps, (const double*)x,
+                     (const double*)U, strideU, (double*)x_next, (double*)u_rec);
+  MPCQP_CHECK_LAUNCH("plant_kernel");
+  return MPCQP_OK;
+}
+
+extern "C" int mpcqp_sqp_shift(int dtype, int batch, int N, void* U, void* y, void* pi,
+                               int32_t* flags, double* rho, double* mu, double* kkt, double mu0,
+                               void* stream) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_sqp_shift: MPCQP_F64 only");
+  MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "mpcqp_sqp_shift: bad sizes");
+  if (batch == 0) return MPCQP_OK;
+  hipLaunchKernelGGL(sqp_shift_kernel, dim3((batch + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, batch, N, (double*)U, (double*)y, (double*)pi, flags,
+                     rho, mu, kkt, mu0);
+  MPCQP_CHECK_LAUNCH("sqp_shift_kernel");
   return MPCQP_OK;
 }

@@ -226,3 +226,38 @@ def test_mpc_qp_input_box_small_matches_mpc_box(dev, dt, tol):
     assert y is None
     assert (batched.status_code(st1) == 0).all() and (batched.status_code(st2) == 0).all()
     assert float((z1 - z2).abs().max()) < tol
+
+
+def test_mpc_qp_f32_near_active_bound_stays_optimal(dev):
+    """A state bound that the fp32 active set leaves inside its tolerance but
+    the dynamics-refined values violate (between the tight re-scan
+    tolerance 1e-7 and the fp32 tolerance 1e-6): the re-scan round must fix
+    it without spurious additions -- status OPTIMAL, error below 1e-5."""
+    N, dt = 30, torch.float32
+    pb = _bicycle_problem(dev, 8, N, seed=9, dt=dt)
+    A, B, c = (pb[k].double().cpu().numpy() for k in ("A", "B", "c"))
+    X0 = pb["x0"].double().cpu().numpy()
+    r = lambda a: _rounded(a, dt)  # noqa: E731
+    xhi = np.tile(r(pb["xhi"]), (8, N))
+    for i in range(8):
+        zr, d = _oracle_state_box(A[i], B[i], c[i], X0[i], r(pb["Q"]), r(pb["R"]), r(pb["QN"]), N,
+                                  r(pb["xlo"]), r(pb["xhi"]), r(pb["lb"]), r(pb["ub"]))
+        xs = d["xbar"] + d["Gam"] @ zr
+        j = 4 * (N // 2)  # p_x at mid-horizon, far inside its box at the optimum
+        xhi[i, j] = float(np.float32(xs[j] - 5e-7 * (1 + abs(xs[j]))))
+    t = lambda a: torch.as_tensor(np.asarray(a, float), dtype=dt, device=dev)  # noqa: E731
+    xlo = np.tile(r(pb["xlo"]), (8, N))
+    z, y, st = batched.mpc_qp(pb["A"], pb["B"], t(pb["Q"]), t(pb["R"]), t(pb["QN"]), N, pb["x0"],
+                              xlo=t(xlo), xhi=t(xhi), lb=t(pb["lb"]), ub=t(pb["ub"]),
+                              c=pb["c"], tv=True)
+    torch.cuda.synchronize()
+    code = batched.status_code(st).cpu().numpy()
+    assert (code == 0).all(), code
+    err = 0.0
+    for i in range(8):
+        d = oc.condense(A[i], B[i], r(pb["Q"]), r(pb["R"]), r(pb["QN"]), N, x0=X0[i], c=c[i])
+        G = np.vstack([d["Gam"], -d["Gam"]])
+        h = np.concatenate([xhi[i] - d["xbar"], -(np.tile(r(pb["xlo"]), N) - d["xbar"])])
+        zr = oq.poly_qp(d["H"], d["f"], G, h, r(pb["lb"]), r(pb["ub"]))[0]
+        err = max(err, float(np.abs(z[i].double().cpu().numpy() - zr).max()))
+    assert err < TOL_F32, err

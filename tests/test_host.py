@@ -169,9 +169,13 @@ def test_mpc_controller_model_params_and_x_obs():
     bad = VehicleParameters(friction=0.8)
     with pytest.raises(ValueError):
         mpc.MPCController(10, 0.08, VehicleParameters(), model=bicycle.KinematicBicycle(bad))
-    with pytest.warns(UserWarning):
-        with pytest.raises(RuntimeError):  # no GPU here: the device check comes next
+    if torch.cuda.is_available():
+        with pytest.warns(UserWarning):
             mpc.MPCController(10, 0.08, x_obs=np.zeros(2))
+    else:
+        with pytest.warns(UserWarning):
+            with pytest.raises(RuntimeError):  # no GPU here: the device check comes next
+                mpc.MPCController(10, 0.08, x_obs=np.zeros(2))
     if not torch.cuda.is_available():
         with pytest.raises(RuntimeError):
             mpc.MPCController(10, 0.08, model=bicycle.KinematicBicycle(bad))
