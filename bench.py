@@ -230,8 +230,10 @@ class Config2:
         r_s = roof("box_quad_kernel<double,5>", "hbm", sb, t_s, HBM_PEAK_GBS, "GB/s",
                    traffic.get("solve_box"), {"bytes_per_launch": sb})
         # fused kernel: SURVEY.md 8(d) per-instance figure (22.0 kflop condense,
-        # config 2) against the fp64 peak; it moves only A, B, x0 in and z out.
-        r_f = roof("mpc_group_kernel<double,2,1,QSym<double,5>,16,2>", "mfma", fl, t_f, FP64_PEAK_TFS, "TFLOP/s",
+        # config 2) against the fp64 vector peak; it moves only A, B, x0 in and
+        # z out, and issues no MFMA: its roof is fp64 VALU issue
+        r_f = roof("mpc_group_kernel<double,2,1,QSym<double,5>,16,2>", "valu-fp64", fl, t_f,
+                   FP64_PEAK_TFS, "TFLOP/s",
                    traffic.get("mpc_box"), {"flops_per_launch": fl,
                                             "hbm_bytes_per_launch": (nx * nx + nx * nu + nx + n) * 8 * bsz + 4 * bsz})
         # split vs fused agreement on the same slot
@@ -410,29 +412,24 @@ class Config3:
         return float(max(errs)) if errs else None
 
     def cpu_baseline(self, seconds):
-        from oracle import condense as oc
-        from oracle import qp as oq
+        from oracle import parallel
 
         N = self.N
         A, B, c = self.A[0].double().cpu().numpy(), self.B[0].double().cpu().numpy(), \
             self.c[0].double().cpu().numpy()
         lb = np.tile([self.p.min_drive, -self.p.max_steer], N)
         ub = np.tile([self.p.max_drive, self.p.max_steer], N)
-        done = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < seconds and done < self.args.batch:
-            d = oc.condense(A[done], B[done], self.Qn, self.Rn, self.QNn, N, x0=self.X0[0, done], c=c[done])
-            G = np.vstack([d["Gam"], -d["Gam"]])
-            h = np.concatenate([np.tile(self.xmax, N) - d["xbar"], -(np.tile(self.xmin, N) - d["xbar"])])
-            try:
-                oq.poly_qp(d["H"], d["f"], G, h, lb, ub)
-            except ValueError:
-                pass
-            done += 1
-        dt = time.perf_counter() - t0
-        return {"value": round(done / dt, 2), "unit": "solves/s", "cores": 1, "kind": "port",
-                "sample": f"{done} config-3 instances: NumPy explicit condensing (oracle/condense.py) "
-                          f"+ Goldfarb-Idnani (oracle/qp.py) in {dt:.1f} s, 1 thread"}
+        cores = parallel.host_cores()
+        total = min(self.args.batch, 2000 * cores)
+        r = parallel.rate(parallel.cfg3_chunk, lambda lo, hi, dl: (
+            A[lo:hi], B[lo:hi], c[lo:hi], self.X0[0, lo:hi], self.Qn, self.Rn, self.QNn, N,
+            self.xmin, self.xmax, lb, ub, dl), total, seconds, cores)
+        return {"value": round(r["value"], 2), "unit": "solves/s", "cores": r["cores"],
+                "kind": "port",
+                "sample": f"{r['done']} config-3 instances: NumPy explicit condensing "
+                          f"(oracle/condense.py) + Goldfarb-Idnani (oracle/qp.py), per-x0 solves "
+                          f"over {r['cores']} spawned processes (oracle/parallel.py) in "
+                          f"{r['seconds']:.1f} s"}
 
 
 class Config4:
@@ -508,18 +505,18 @@ class Config4:
 
     def cpu_baseline(self, seconds):
         from oracle import condense as oc
-        from oracle import qp as oq
+        from oracle import parallel
 
         d = oc.condense(self.A, self.B, self.Qn, self.Rn, self.Qn, self.N)
-        done = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < seconds and done < self.args.batch:
-            oq.poly_qp(d["H"], d["F"] @ self.X0[0, done], self.G, self.h)
-            done += 1
-        dt = time.perf_counter() - t0
-        return {"value": round(done / dt, 2), "unit": "solves/s", "cores": 1, "kind": "port",
-                "sample": f"{done} config-4 instances: NumPy Goldfarb-Idnani (oracle/qp.py) on the "
-                          f"shared condensed QP in {dt:.1f} s, 1 thread"}
+        cores = parallel.host_cores()
+        total = min(self.args.batch, 4000 * cores)
+        r = parallel.rate(parallel.cfg4_chunk, lambda lo, hi, dl: (
+            d["H"], d["F"], self.G, self.h, self.X0[0, lo:hi], dl), total, seconds, cores)
+        return {"value": round(r["value"], 2), "unit": "solves/s", "cores": r["cores"],
+                "kind": "port",
+                "sample": f"{r['done']} config-4 instances: NumPy Goldfarb-Idnani (oracle/qp.py) "
+                          f"on the shared condensed QP, per-x0 solves over {r['cores']} spawned "
+                          f"processes in {r['seconds']:.1f} s"}
 
 
 class Config5:
@@ -628,25 +625,219 @@ class Config5:
         return float(max(errs))
 
     def cpu_baseline(self, seconds):
-        from oracle import condense as oc
-        from oracle import qp as oq
+        from oracle import parallel
 
         N = self.N
-        A, B = self.A[0].double().cpu().numpy(), self.B[0].double().cpu().numpy()
-        X0 = self.X0_t[0].double().cpu().numpy()
-        done = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < seconds and done < self.args.batch:
-            d = oc.condense(A[done], B[done], self.Qn, self.Rn, self.Qn, N, x0=X0[done])
-            oq.box_qp(d["H"], d["f"], np.full(self.n, self.lb), np.full(self.n, self.ub))
-            done += 1
-        dt = time.perf_counter() - t0
-        return {"value": round(done / dt, 2), "unit": "solves/s", "cores": 1, "kind": "port",
-                "sample": f"{done} config-5 instances: NumPy explicit condensing + primal active "
-                          f"set (oracle/) in {dt:.1f} s, 1 thread"}
+        cores = parallel.host_cores()
+        total = min(self.args.batch, 500 * cores)
+        A = self.A[0][:total].double().cpu().numpy()
+        B = self.B[0][:total].double().cpu().numpy()
+        X0 = self.X0_t[0][:total].double().cpu().numpy()
+        r = parallel.rate(parallel.cfg5_chunk, lambda lo, hi, dl: (
+            A[lo:hi], B[lo:hi], X0[lo:hi], self.Qn, self.Rn, N, self.lb, self.ub, dl),
+            total, seconds, cores)
+        return {"value": round(r["value"], 2), "unit": "solves/s", "cores": r["cores"],
+                "kind": "port",
+                "sample": f"{r['done']} config-5 instances: NumPy explicit condensing + primal "
+                          f"active set (oracle/), per-x0 solves over {r['cores']} spawned "
+                          f"processes in {r['seconds']:.1f} s"}
 
 
-CONFIGS = {2: Config2, 3: Config3, 4: Config4, 5: Config5}
+class ConfigNLP:
+    """Converged NLP solves of the session-4 MPC step (the controller of
+    main.py:241-251: N=30, ts=0.08, weights main.py:72-74, input + state box;
+    collision rows out of scope): MPCController's SQP (mpc.SqpSolver), a
+    fixed budget of --sqp-iters iterations per solve from a cold start
+    (U = 0), over a batch of x0.  One step = one batch of NLP solves."""
+
+    dtype = torch.float64
+    dname = "f64"
+    default_batch = 4096
+    default_slots = 2
+
+    def __init__(self, args, dev, rank):
+        from model_predictive_control_amd.mpc import MPCController, SqpSolver
+        from model_predictive_control_amd.parameters import VehicleParameters
+
+        self.args, self.dev = args, dev
+        self.N, self.ts = args.horizon or 30, 0.08
+        self.iters = args.sqp_iters
+        bsz, S = args.batch, args.slots
+        self.ctl = MPCController(self.N, self.ts, VehicleParameters(), tol=1e-9)
+        self.sqp = SqpSolver(self.ctl, bsz)
+        rng = np.random.default_rng(20261015 + 6 + 1000 * rank)
+        self.X0 = np.stack([rng.uniform(-.8, .8, (S, bsz)), rng.uniform(-.4, .4, (S, bsz)),
+                            rng.uniform(-.5, .5, (S, bsz)), rng.uniform(-.2, .2, (S, bsz))], -1)
+        self.X0_t = torch.as_tensor(self.X0, dtype=torch.float64, device=dev)
+        self.Z = torch.empty((S, bsz, 2 * self.N), dtype=torch.float64, device=dev)
+        self.ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
+        self.KKT = torch.empty((S, bsz), dtype=torch.float64, device=dev)
+
+    def workload(self):
+        return {"workload": f"nlp: converged MPCController.solve (main.py controller, N={self.N}, "
+                            f"ts=0.08, input + state box) by SQP on device, {self.iters} "
+                            f"iterations per solve from U=0 (Gauss-Newton, then damped exact "
+                            f"Hessian), x0 ~ U(+-.8, +-.4, +-.5, +-.2)",
+                "horizon": self.N, "nx": 4, "nu": 2, "sqp_iters": self.iters}
+
+    def step(self, s):
+        sqp = self.sqp
+        sqp.reset()
+        for _ in range(self.iters):
+            sqp.iterate(self.X0_t[s])
+        self.Z[s].copy_(sqp.U.view(self.args.batch, -1))
+        self.ST[s].copy_(sqp.status())
+        self.KKT[s].copy_(sqp.kkt)
+
+    def status(self):
+        return self.ST
+
+    def kernels(self, traffic):
+        """One SQP iteration's launches timed separately on the converged state
+        of slot 0 (the last step left it there)."""
+        R = self.args.reps
+        sqp, ctl, N, bsz = self.sqp, self.ctl, self.N, self.args.batch
+        x0 = self.X0_t[0]
+        A, B, c, Xr = batched.bicycle_rti(x0, sqp.U, ctl.params, ctl.ts, states=True)
+        t_r = time_kernel(lambda: batched.bicycle_rti(x0, sqp.U, ctl.params, ctl.ts, states=True), R,
+                          self.dev)
+        t_h = time_kernel(lambda: batched.bicycle_hessian(Xr, sqp.U, sqp.pi, ctl.params, ctl.ts,
+                                                          flags=None, mu=sqp.mu), R, self.dev)
+        H2, q2 = batched.bicycle_hessian(Xr, sqp.U, sqp.pi, ctl.params, ctl.ts, flags=None, mu=sqp.mu)
+        box = ctl._box()
+
+        def ipm():
+            sqp.qp = batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, lb=ctl.lbz, ub=ctl.ubz, c=c,
+                                     tv=True, H2=H2, q2=q2, out=sqp.qp, **box)
+        t_i = time_kernel(ipm, R, self.dev)
+        torch.cuda.synchronize()
+        it_ipm = float(((sqp.qp["status"] >> 8) & 0xFFFF).double().mean())
+        # algorithmic bytes of the interior point: A_k, B_k, c_k, H2_k, q2_k, x0 in;
+        # z, X, y, pi, lam_u, status out (its workspace traffic is overhead)
+        ib = (N * (16 + 8 + 4 + 36 + 6) + 4 + N * (2 + 4 + 4 + 4 + 2)) * 8 * bsz + 4 * bsz
+        r_i = roof("ipm_kernel<double,4,2>", "hbm", ib, t_i, HBM_PEAK_GBS, "GB/s",
+                   traffic.get("ipm"), {"bytes_per_launch": ib, "ipm_iters_mean": round(it_ipm, 2),
+                                        "note": "lane per instance; latency-bound sweeps over the "
+                                                "stages, workspace traffic not counted"})
+        extra = {"kernel_us": {"bicycle_rti": round(t_r * 1e3, 2),
+                               "bicycle_hessian": round(t_h * 1e3, 2),
+                               "mpc_ipm": round(t_i * 1e3, 2)},
+                 "kkt_max": float(self.KKT[0].max()),
+                 "converged_frac": float((batched.status_code(self.ST[0]) == 0).double().mean())}
+        return r_i, {}, extra
+
+    def check(self):
+        """max |u - u*| against the NLP oracle (oracle/nlp.py: SQP + Newton
+        polish, KKT-certified) on a few instances of slot 0."""
+        from oracle import nlp
+
+        g = self.ctl
+        xlo, lbu = g.lb_states, g.lb_inputs
+        ocp = nlp.OCP(self.N, self.ts, g.Q.cpu().numpy(), g.QN.cpu().numpy(), g.R.cpu().numpy(),
+                      xlo, -xlo, lbu, -lbu)
+        Z = self.Z[0].cpu().numpy()
+        errs = []
+        for i in range(min(self.args.check, 4, self.args.batch)):
+            U, _, k = ocp.solve(self.X0[0, i])
+            if k < 1e-10:
+                errs.append(np.abs(Z[i] - U).max())
+        return float(max(errs)) if errs else None
+
+    def cpu_baseline(self, seconds):
+        from oracle import parallel
+
+        g = self.ctl
+        cores = parallel.host_cores()
+        total = min(self.args.batch, 64 * cores)
+        Q, QN, R = (v.cpu().numpy() for v in (g.Q, g.QN, g.R))
+        r = parallel.rate(parallel.nlp_chunk, lambda lo, hi, dl: (
+            self.N, self.ts, Q, QN, R, g.lb_states, g.lb_inputs, self.X0[0, lo:hi], dl),
+            total, seconds, cores)
+        return {"value": round(r["value"], 3), "unit": "solves/s", "cores": r["cores"],
+                "kind": "port",
+                "sample": f"{r['done']} NLP solves (oracle/nlp.py: Gauss-Newton SQP on the "
+                          f"NumPy condensing + Goldfarb-Idnani QP, Newton polish to KKT 1e-9), "
+                          f"per-x0 over {r['cores']} spawned processes in {r['seconds']:.1f} s"}
+
+
+class ConfigLoop:
+    """The receding-horizon loop on device (closed_loop.ClosedLoop): the
+    main.py controller (converged SQP, --sqp-iters iterations per sample,
+    warm-started) on a forward-Euler bicycle plant for --loop-steps samples
+    (main.py:270-271 runs 100), batch of x0.  One bench step = one closed-loop
+    episode of the batch; value = closed-loop MPC steps (instance x sample)
+    per second."""
+
+    dtype = torch.float64
+    dname = "f64"
+    default_batch = 4096
+    default_slots = 2
+
+    def __init__(self, args, dev, rank):
+        from model_predictive_control_amd.closed_loop import ClosedLoop
+        from model_predictive_control_amd.mpc import MPCController
+        from model_predictive_control_amd.parameters import VehicleParameters
+
+        self.args, self.dev = args, dev
+        self.N, self.T = args.horizon or 30, args.loop_steps
+        self.units_per_step = self.T
+        bsz, S = args.batch, args.slots
+        self.ctl = MPCController(self.N, 0.08, VehicleParameters(), tol=1e-9)
+        self.loop = ClosedLoop(self.ctl, plant="fe", iters_per_step=args.sqp_iters, graph=False)
+        rng = np.random.default_rng(20261015 + 7 + 1000 * rank)
+        self.X0 = np.stack([rng.uniform(-.8, .8, (S, bsz)), rng.uniform(-.4, .4, (S, bsz)),
+                            rng.uniform(-.5, .5, (S, bsz)), rng.uniform(-.2, .2, (S, bsz))], -1)
+        self.X0_t = torch.as_tensor(self.X0, dtype=torch.float64, device=dev)
+        self.bufs = [self.loop._alloc(bsz, self.T) for _ in range(S)]
+        self.ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
+
+    def workload(self):
+        return {"workload": f"loop: on-device receding-horizon loop, main.py controller (N={self.N}, "
+                            f"ts=0.08, input + state box, converged SQP with {self.args.sqp_iters} "
+                            f"iterations per sample, warm-started) on a forward-Euler plant, "
+                            f"{self.T} samples per episode",
+                "horizon": self.N, "nx": 4, "nu": 2, "samples": self.T,
+                "sqp_iters_per_sample": self.args.sqp_iters}
+
+    def step(self, s):
+        b = self.bufs[s]
+        b["xs"][0].copy_(self.X0_t[s])
+        self.loop._reset(b)
+        for t in range(self.T):
+            self.loop._step(b, t)
+        self.ST[s].copy_(b["success"].all(0).logical_not().to(torch.int32))
+
+    def status(self):
+        return self.ST
+
+    def kernels(self, traffic):
+        b = self.bufs[0]
+        extra = {"success_frac_per_sample": float(b["success"].double().mean()),
+                 "iters_per_sample_mean": float(b["iters"].double().mean()),
+                 "iters_per_sample_max": int(b["iters"].max())}
+        return None, {}, extra
+
+    def check(self):
+        """Device episode of 2 instances against the host loop mpc.simulate
+        with the same converged controller (max state deviation)."""
+        from model_predictive_control_amd import bicycle, mpc
+        from model_predictive_control_amd.parameters import VehicleParameters
+
+        xs = self.bufs[0]["xs"].cpu().numpy()
+        fe = bicycle.fwd_euler(bicycle.KinematicBicycle(VehicleParameters()), 0.08)
+        err = 0.0
+        for i in range(2):
+            ctl = mpc.MPCController(self.N, 0.08, VehicleParameters(), tol=1e-9)
+            ref = mpc.simulate(self.X0[0, i], fe, min(self.T, 10), ctl)
+            err = max(err, float(np.abs(xs[:ref.shape[0], i] - ref).max()))
+        return err
+
+    def cpu_baseline(self, seconds):
+        return None
+
+
+CONFIGS = {"2": Config2, "3": Config3, "4": Config4, "5": Config5, "nlp": ConfigNLP,
+           "loop": ConfigLoop}
 
 
 def main():
@@ -654,7 +845,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="2", choices=sorted(CONFIGS),
+                    help="BASELINE configs 2-5 (2 = the headline), nlp (converged "
+                         "MPCController.solve), loop (on-device receding-horizon loop)")
+    ap.add_argument("--sqp-iters", type=int, default=40,
+                    help="nlp: SQP iterations per solve; loop: per sample")
+    ap.add_argument("--loop-steps", type=int, default=20, help="loop: samples per episode")
+    ap.add_argument("--gather", action="store_true",
+                    help="N>1: time the final all-gather of z (RCCL) after the timed loop")
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU per step (0 = config default)")
     ap.add_argument("--horizon", type=int, default=0, help="N (0 = config default)")
     ap.add_argument("--slots", type=int, default=0, help="distinct x0 batches cycled over")
@@ -763,7 +961,11 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = mdist.max_over_ranks(elapsed, dev if backend == "nccl" else torch.device("cpu"))
-    value = world * args.batch * args.steps / elapsed
+    units = getattr(wl, "units_per_step", 1)
+    value = world * args.batch * units * args.steps / elapsed
+    gather = None
+    if args.gather and world > 1:
+        gather = time_gather(wl, args, world, dev)
 
     # ---- correctness of what was timed: statuses + oracle spot check (rank 0)
     st = wl.status()
@@ -790,6 +992,9 @@ def main():
         cfg.update({"batch_per_gpu": args.batch, "parallelism": f"dp{world}",
                     "graph": graphs is not None, "graph_steps": S if chain is not None else 1,
                     "config": args.config})
+        if dom is None:
+            dom = {"note": "no single dominant kernel: see the nlp config for the per-kernel "
+                           "rooflines of one SQP iteration"}
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -814,12 +1019,36 @@ def main():
         }
         if e2e is not None:
             out["host_roundtrip"] = e2e
+        if gather is not None:
+            out["gather"] = gather
+        if units != 1:
+            out["unit"] = "closed-loop MPC steps/s"
         out.update(others)
         out.update(extra)
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
     return out
+
+
+def time_gather(wl, args, world, dev):
+    """The only collective of the multi-GPU path: all-gather
+    of every rank's solutions z (slot 0) into the whole batch on every rank,
+    timed with HIP events around the collective, outside the timed loop."""
+    z = wl.Z[0]
+    total = world * z.shape[0]
+    torch.distributed.barrier()
+    mdist.gather_shards(z, total)          # warm-up (communicator setup)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    full = mdist.gather_shards(z, total)
+    e1.record()
+    e1.synchronize()
+    ms = mdist.max_over_ranks(e0.elapsed_time(e1), dev)
+    nbytes = full.numel() * full.element_size()
+    return {"ms": round(ms, 4), "bytes": int(nbytes), "GBps": round(nbytes / (ms * 1e-3) / 1e9, 2),
+            "note": "all-gather of z over ranks (RCCL), after the timed loop"}
 
 
 def host_roundtrip(wl, graphs, args, reps=50):

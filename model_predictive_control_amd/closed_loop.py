@@ -24,7 +24,7 @@ import torch
 
 from . import _native as nat
 from . import batched
-from .mpc import MPCController
+from .mpc import MPCController, SqpSolver
 from .parameters import VehicleParameters
 
 PLANTS = {"fe": nat.PLANT_FE, "rk4": nat.PLANT_RK4, "exact": nat.PLANT_RK4_SUB}
@@ -58,67 +58,52 @@ class ClosedLoop:
         f64 = dict(dtype=torch.float64, device=dev)
         s = dict(
             xs=torch.zeros((T + 1, b, 4), **f64), us=torch.zeros((T, b, 2), **f64),
-            U=torch.zeros((b, N, 2), **f64), y=torch.zeros((b, N * 4), **f64),
-            pi=torch.zeros((b, N, 4), **f64), X=torch.zeros((b, N + 1, 4), **f64),
-            rho=torch.zeros(b, **f64), kkt=torch.full((b,), float("inf"), **f64),
-            mu=torch.full((b,), 0.1, **f64),
-            flags=torch.zeros(b, dtype=torch.int32, device=dev),
             success=torch.zeros((T, b), dtype=torch.bool, device=dev),
             iters=torch.zeros((T, b), dtype=torch.int32, device=dev),
             state_prediction=torch.zeros((T, b, N + 1, 4), **f64),
             input_prediction=torch.zeros((T, b, N, 2), **f64))
-        s["qp"] = None
+        s["sqp"] = SqpSolver(ctl, b)
         return s
 
     # ------------------------------------------------------------ one step
     def _mpc(self, s, t):
-        ctl, N = self.ctl, self.ctl.N
+        ctl, N, sqp = self.ctl, self.ctl.N, s["sqp"]
         x0 = s["xs"][t]
-        box = ctl._box()
         if ctl.mode == "rti":
-            U = s["U"]
             for _ in range(ctl.sqp_iters):
-                A, B, c = batched.bicycle_rti(x0, U, ctl.params, ctl.ts)
+                A, B, c = batched.bicycle_rti(x0, sqp.U, ctl.params, ctl.ts)
                 z, _, st, X = batched.mpc_qp(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, c=c, lb=ctl.lbz,
-                                             ub=ctl.ubz, tv=True, states=True, **box)
-                U.copy_(z.view_as(U))
-            s["X"][:, 0].copy_(x0)
-            s["X"][:, 1:].copy_(X)
+                                             ub=ctl.ubz, tv=True, states=True, **ctl._box())
+                sqp.U.copy_(z.view_as(sqp.U))
+            sqp.X[:, 0].copy_(x0)
+            sqp.X[:, 1:].copy_(X)
             s["success"][t].copy_(batched.status_code(st) == 0)
             return
         for _ in range(self.iters):
-            A, B, c, Xr = batched.bicycle_rti(x0, s["U"], ctl.params, ctl.ts, states=True)
-            H2 = q2 = None
-            if ctl.hessian == "exact":
-                H2, q2 = batched.bicycle_hessian(Xr, s["U"], s["pi"], ctl.params, ctl.ts,
-                                                 flags=s["flags"], mu=s["mu"])
-            s["qp"] = batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, lb=ctl.lbz, ub=ctl.ubz,
-                                      c=c, tv=True, H2=H2, q2=q2, out=s["qp"], **box)
-            batched.bicycle_sqp_step(x0, s["U"], s["qp"]["z"], s["qp"]["y"], s["qp"]["pi"],
-                                     s["y"], s["pi"], s["X"], s, ctl.params, ctl.ts, ctl.Q, ctl.R,
-                                     ctl.QN, xlo=box.get("xlo"), xhi=box.get("xhi"), lb=ctl.lbz,
-                                     ub=ctl.ubz, tol=ctl.tol, qp_status=s["qp"]["status"])
-        s["success"][t].copy_((s["flags"] & nat.SQP_DONE) != 0)
-        s["iters"][t].copy_((s["flags"] >> 8) & 0xFFFF)
+            sqp.iterate(x0)
+        s["success"][t].copy_(sqp.done())
+        s["iters"][t].copy_(sqp.iters())
 
     def _step(self, s, t):
         ctl = self.ctl
-        b = s["U"].shape[0]
+        b = s["sqp"].b
         self._mpc(s, t)
+        sqp = s["sqp"]
         # ControllerLog of the step: [x_t; predicted states], the input plan
-        s["state_prediction"][t].copy_(s["X"])
-        s["input_prediction"][t].copy_(s["U"])
+        s["state_prediction"][t].copy_(sqp.X)
+        s["input_prediction"][t].copy_(sqp.U)
         p = self.plant_params
         prm = batched._bike_params(p)
         lib = nat.load()
         rc = lib.mpcqp_bicycle_plant(nat.F64, b, float(ctl.ts), prm, self.plant, self.substeps,
-                                     s["xs"][t].data_ptr(), s["U"].data_ptr(), 2 * ctl.N,
+                                     s["xs"][t].data_ptr(), sqp.U.data_ptr(), 2 * ctl.N,
                                      s["xs"][t + 1].data_ptr(), s["us"][t].data_ptr(),
                                      batched._stream())
         nat.check(rc, "mpcqp_bicycle_plant")
-        rc = lib.mpcqp_sqp_shift(nat.F64, b, ctl.N, s["U"].data_ptr(), s["y"].data_ptr(),
-                                 s["pi"].data_ptr(), s["flags"].data_ptr(), s["rho"].data_ptr(),
-                                 s["mu"].data_ptr(), s["kkt"].data_ptr(), 0.1, batched._stream())
+        rc = lib.mpcqp_sqp_shift(nat.F64, b, ctl.N, sqp.U.data_ptr(), sqp.y.data_ptr(),
+                                 sqp.pi.data_ptr(), sqp.flags.data_ptr(), sqp.rho.data_ptr(),
+                                 sqp.mu.data_ptr(), sqp.kkt.data_ptr(), sqp.MU0,
+                                 batched._stream())
         nat.check(rc, "mpcqp_sqp_shift")
 
     # ---------------------------------------------------------------- run
@@ -158,10 +143,4 @@ class ClosedLoop:
                                   "input_prediction")}
 
     def _reset(self, s):
-        s["U"].zero_()
-        s["y"].zero_()
-        s["pi"].zero_()
-        s["flags"].zero_()
-        s["rho"].zero_()
-        s["mu"].fill_(0.1)
-        s["kkt"].fill_(float("inf"))
+        s["sqp"].reset()

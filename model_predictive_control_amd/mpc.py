@@ -153,41 +153,21 @@ class MPCController:
 
     def _solve_sqp(self, X0):
         """SQP to a first-order point of the NLP (module docstring)."""
-        N, nu, dev = self.N, self.nu, self.device
+        N, nu = self.N, self.nu
         b = X0.shape[0]
-        f64 = dict(dtype=torch.float64, device=dev)
-        U = self._warm_start(b)
-        y = torch.zeros((b, N * 4), **f64)
-        pi = torch.zeros((b, N, 4), **f64)
-        X = torch.empty((b, N + 1, 4), **f64)
-        state = dict(rho=torch.zeros(b, **f64), kkt=torch.full((b,), float("inf"), **f64),
-                     mu=torch.full((b,), 0.1, **f64),
-                     flags=torch.zeros(b, dtype=torch.int32, device=dev))
-        box = self._box()
-        exact = self.hessian == "exact"
-        qp_out = None
+        sqp = SqpSolver(self, b)
+        sqp.reset(self._warm_start(b))
         for _ in range(self.max_iter):
-            A, B, c, Xr = batched.bicycle_rti(X0, U, self.params, self.ts, states=True)
-            H2 = q2 = None
-            if exact:
-                H2, q2 = batched.bicycle_hessian(Xr, U, pi, self.params, self.ts,
-                                                 flags=state["flags"], mu=state["mu"])
-            qp_out = batched.mpc_ipm(A, B, self.Q, self.R, self.QN, N, X0, lb=self.lbz,
-                                     ub=self.ubz, c=c, tv=True, H2=H2, q2=q2, out=qp_out, **box)
-            batched.bicycle_sqp_step(X0, U, qp_out["z"], qp_out["y"], qp_out["pi"], y, pi, X,
-                                     state, self.params, self.ts, self.Q, self.R, self.QN,
-                                     xlo=box.get("xlo"), xhi=box.get("xhi"), lb=self.lbz,
-                                     ub=self.ubz, tol=self.tol, qp_status=qp_out["status"])
-            if bool((state["flags"] & SQP_DONE).all()):
+            sqp.iterate(X0)
+            if bool((sqp.flags & SQP_DONE).all()):
                 break
-        done = (state["flags"] & SQP_DONE) != 0
-        iters = (state["flags"] >> 8) & 0xFFFF
-        status = torch.where(done, STATUS_OPTIMAL, STATUS_MAXITER).to(torch.int32) | (iters << 8)
-        self.last_prediction = X[:, 1:]
-        self.last_lam_g = y
-        self.last_costates = pi
-        self.last_kkt = state["kkt"]
-        self.last_iters = iters
+        status = sqp.status()
+        self.last_prediction = sqp.X[:, 1:]
+        self.last_lam_g = sqp.y
+        self.last_costates = sqp.pi
+        self.last_kkt = sqp.kkt
+        self.last_iters = sqp.iters()
+        U = sqp.U
         self._warm = torch.cat([U[:, 1:], U[:, -1:]], 1).contiguous()
         self.last_status = status
         return U.reshape(b, N * nu), status
@@ -244,6 +224,78 @@ class MPCController:
     def __call__(self, y):
         """main.py:121-129: solve for measured state y, return u[0]."""
         return self.reshape_input(self.solve(y))[0]
+
+
+class SqpSolver:
+    """Device state of the batched SQP of ``MPCController`` (mode "sqp") for
+    a batch of b initial states, preallocated so that ``iterate`` -- one SQP
+    iteration, four libmpcqp launches, no host synchronisation -- can be
+    repeated or captured in a HIP graph:
+
+      mpcqp_bicycle_rti -> mpcqp_bicycle_hessian -> mpcqp_mpc_ipm
+      -> mpcqp_bicycle_sqp_step
+
+    Instances that reach the KKT tolerance are frozen by the step kernel
+    (flag SQP_DONE); the others keep iterating."""
+
+    MU0 = 0.1  # initial Levenberg-Marquardt damping of the exact-Hessian QPs
+
+    def __init__(self, ctl: "MPCController", b: int):
+        self.ctl, self.b = ctl, b
+        N, dev = ctl.N, ctl.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.U = torch.zeros((b, N, 2), **f64)
+        self.y = torch.zeros((b, N * 4), **f64)
+        self.pi = torch.zeros((b, N, 4), **f64)
+        self.X = torch.zeros((b, N + 1, 4), **f64)
+        self.rho = torch.zeros(b, **f64)
+        self.kkt = torch.full((b,), float("inf"), **f64)
+        self.mu = torch.full((b,), self.MU0, **f64)
+        self.flags = torch.zeros(b, dtype=torch.int32, device=dev)
+        self.qp = None
+        self.box = ctl._box()
+
+    def state(self) -> dict:
+        return dict(rho=self.rho, kkt=self.kkt, mu=self.mu, flags=self.flags)
+
+    def reset(self, U0=None):
+        """Cold (U0 None: zeros) or warm start; multipliers and state cleared."""
+        if U0 is None:
+            self.U.zero_()
+        else:
+            self.U.copy_(U0)
+        self.y.zero_()
+        self.pi.zero_()
+        self.rho.zero_()
+        self.kkt.fill_(float("inf"))
+        self.mu.fill_(self.MU0)
+        self.flags.zero_()
+
+    def iterate(self, X0):
+        ctl, N, box = self.ctl, self.ctl.N, self.box
+        A, B, c, Xr = batched.bicycle_rti(X0, self.U, ctl.params, ctl.ts, states=True)
+        H2 = q2 = None
+        if ctl.hessian == "exact":
+            H2, q2 = batched.bicycle_hessian(Xr, self.U, self.pi, ctl.params, ctl.ts,
+                                             flags=self.flags, mu=self.mu)
+        self.qp = batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, X0, lb=ctl.lbz, ub=ctl.ubz,
+                                  c=c, tv=True, H2=H2, q2=q2, out=self.qp, **box)
+        batched.bicycle_sqp_step(X0, self.U, self.qp["z"], self.qp["y"], self.qp["pi"], self.y,
+                                 self.pi, self.X, self.state(), ctl.params, ctl.ts, ctl.Q, ctl.R,
+                                 ctl.QN, xlo=box.get("xlo"), xhi=box.get("xhi"), lb=ctl.lbz,
+                                 ub=ctl.ubz, tol=ctl.tol, qp_status=self.qp["status"])
+
+    def done(self):
+        return (self.flags & SQP_DONE) != 0
+
+    def iters(self):
+        return (self.flags >> 8) & 0xFFFF
+
+    def status(self):
+        """MPCQP status words: OPTIMAL (KKT <= tol) or MAXITER, iterations in
+        bits 8..23."""
+        code = torch.where(self.done(), STATUS_OPTIMAL, STATUS_MAXITER).to(torch.int32)
+        return code | (self.iters() << 8)
 
 
 def _kinematic(p) -> tuple:

@@ -1,0 +1,121 @@
+"""Multi-core CPU baselines (TEST/BENCH INFRASTRUCTURE ONLY -- bench.py's
+cpu_baseline leg): the oracle's per-x0 solves spread over the host cores,
+as SURVEY.md 8(d) asks ("per-x0 solves are spread across all host cores with
+multiprocessing").  Workers are started with the 'spawn' method (fresh
+interpreters that never touch the GPU) and each runs its chunk of instances
+until a common deadline; the rate is instances done / wall time.
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import os
+import time
+
+import numpy as np
+
+
+def host_cores(cap: int = 16) -> int:
+    """CPU share of this process (a GPU box shares its host: at most ``cap``)."""
+    return max(1, min(cap, len(os.sched_getaffinity(0))))
+
+
+_BLAS_ENV = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
+
+
+def _noop(_):
+    return os.getpid()
+
+
+# ----------------------------------------------------------------- workers
+def cfg3_chunk(a):
+    from oracle import condense as oc
+    from oracle import qp as oq
+
+    A, B, c, X0, Q, R, QN, N, xmin, xmax, lb, ub, deadline = a
+    done = 0
+    for i in range(A.shape[0]):
+        if time.time() >= deadline:
+            break
+        d = oc.condense(A[i], B[i], Q, R, QN, N, x0=X0[i], c=c[i])
+        G = np.vstack([d["Gam"], -d["Gam"]])
+        h = np.concatenate([np.tile(xmax, N) - d["xbar"], -(np.tile(xmin, N) - d["xbar"])])
+        try:
+            oq.poly_qp(d["H"], d["f"], G, h, lb, ub)
+        except ValueError:
+            pass
+        done += 1
+    return done
+
+
+def cfg4_chunk(a):
+    from oracle import qp as oq
+
+    H, F, G, h, X0, deadline = a
+    done = 0
+    for i in range(X0.shape[0]):
+        if time.time() >= deadline:
+            break
+        oq.poly_qp(H, F @ X0[i], G, h)
+        done += 1
+    return done
+
+
+def cfg5_chunk(a):
+    from oracle import condense as oc
+    from oracle import qp as oq
+
+    A, B, X0, Q, R, N, lo, hi, deadline = a
+    n = N * B.shape[-1]
+    done = 0
+    for i in range(A.shape[0]):
+        if time.time() >= deadline:
+            break
+        d = oc.condense(A[i], B[i], Q, R, Q, N, x0=X0[i])
+        oq.box_qp(d["H"], d["f"], np.full(n, lo), np.full(n, hi))
+        done += 1
+    return done
+
+
+def nlp_chunk(a):
+    from oracle import nlp
+
+    N, ts, Q, QN, R, xlo, lbu, X0, deadline = a
+    ocp = nlp.OCP(N, ts, Q, QN, R, xlo, -xlo, lbu, -lbu)
+    done = 0
+    for i in range(X0.shape[0]):
+        if time.time() >= deadline:
+            break
+        ocp.solve(X0[i], tol=1e-9)
+        done += 1
+    return done
+
+
+def rate(worker, make_args, total: int, seconds: float, cores: int | None = None) -> dict:
+    """Run ``worker`` over ``cores`` spawned processes; ``make_args(lo, hi,
+    deadline)`` builds the argument of the chunk [lo, hi) of ``total``
+    instances.  Returns dict(value=instances/s, done, seconds, cores)."""
+    cores = cores or host_cores()
+    ctx = mp.get_context("spawn")
+    # one BLAS thread per worker (the workers ARE the parallelism); the
+    # spawned interpreters read these when they import NumPy
+    saved = {k: os.environ.get(k) for k in _BLAS_ENV}
+    os.environ.update({k: "1" for k in _BLAS_ENV})
+    try:
+        pool = ctx.Pool(cores)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    with pool:
+        pool.map(_noop, range(cores))          # every worker up before the clock
+        t0 = time.time()
+        deadline = t0 + seconds
+        per = -(-total // cores)
+        args = [make_args(k * per, min(total, (k + 1) * per), deadline) for k in range(cores)
+                if k * per < total]
+        counts = pool.map(worker, args)
+        dt = time.time() - t0
+    done = int(sum(counts))
+    return {"value": done / dt, "done": done, "seconds": dt, "cores": cores}
