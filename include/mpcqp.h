@@ -80,6 +80,10 @@ extern "C" {
 /* condense / MPC-step flags */
 #define MPCQP_TV 1  /* A, B are per-stage: N*nx*nx / N*nx*nu per instance */
 #define MPCQP_IPM 2 /* mpcqp_mpc_qp: solve on the stage-wise interior point (mpcqp_mpc_ipm) */
+/* mpcqp_mpc_ipm: a non-positive Riccati pivot ends the solve with
+   MPCQP_STATUS_NOT_CONVEX at once instead of regularising (an SQP caller
+   raises its own damping and retries) */
+#define MPCQP_STRICT 4
 
 /* status bit 24: the solution was polished to the exact active-set vertex */
 #define MPCQP_STATUS_POLISHED (1 << 24)
@@ -314,7 +318,11 @@ int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
  * (optional, N*nu): input-bound multipliers, > 0 at ub; pi (optional, N*nx):
  * costates of x_{k+1} = A_k x_k + B_k u_k + c_k; y (optional, N*nx):
  * state-bound multipliers, > 0 at xhi.  status: MPCQP_STATUS_NOT_CONVEX when
- * no inertia correction up to 1e12 makes the Newton system definite.
+ * no inertia correction up to 1e12 makes the Newton system definite (at the
+ * first non-positive pivot with flags & MPCQP_STRICT).  skip (optional, one
+ * int32 per instance): instances with (skip[b] & skip_mask) != 0 are not
+ * solved and their outputs and status are left as they are (an SQP passes
+ * its per-instance flags to freeze the converged instances).
  * Limits: nx <= 4, nu <= 2.  workspace: mpcqp_mpc_ipm_workspace() bytes
  * (N * ~100 doubles per instance).
  */
@@ -329,6 +337,7 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
                   const void* U0, int64_t strideU0, const void* H2, int64_t strideH2,
                   const void* q2, int64_t strideq2,
                   void* z, void* y, void* X, void* lam_u, void* pi, int32_t* status,
+                  const int32_t* skip, int32_t skip_mask,
                   int max_iter, double tol, void* ws, size_t ws_bytes, void* stream);
 
 /*
@@ -357,15 +366,31 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
  *   full step (to 0 below 1e-11), multiplied by 4 (at least 1e-3) after a
  *   step that needed backtracking or a failed QP.  rho, mu, kkt: one double
  *   per instance (rho initialised to 0).  Q, R, Qf shared (4x4, 2x2, 4x4);
- *   bounds as in mpcqp_mpc_qp (lb/ub stride strideLb).  fp64.
+ *   bounds as in mpcqp_mpc_qp (lb/ub stride strideLb).  integrator: the
+ *   prediction model of the NLP (MPCQP_MODEL_FE / MPCQP_MODEL_RK4; the
+ *   exact Hessian of mpcqp_bicycle_hessian is the FE model's).  fp64.
  */
 #define MPCQP_SQP_DONE 1
 #define MPCQP_SQP_EXACT 2
+/* prediction models (integrator argument) */
+#define MPCQP_MODEL_FE 0  /* fwd_euler, main.py:132-135 */
+#define MPCQP_MODEL_RK4 1 /* runge_kutta4, main.py:138-147 (template.py:141) */
+/*
+ * mpcqp_bicycle_linearise: the prediction model (FE or RK4) rolled out from
+ * x0 under U (N x 2) -> X ((N+1) x 4), and linearised along it:
+ * A_k = d x+/dx, B_k = d x+/du (RK4: forward sensitivities through the four
+ * stages), c_k = x_{k+1} - A_k x_k - B_k u_k, in the layout of
+ * mpcqp_condense(MPCQP_TV).  fp64.  (mpcqp_bicycle_rti is the FE case in
+ * fp32 or fp64.)
+ */
+int mpcqp_bicycle_linearise(int dtype, int batch, int N, double ts, const double* params,
+                            int integrator, const void* x0, int64_t strideX0, const void* U,
+                            int64_t strideU, void* X, void* A, void* B, void* c, void* stream);
 int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
                           const void* X, const void* U, const void* pi, const int32_t* flags,
                           const double* mu, void* H2, void* q2, void* stream);
 int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts, const double* params,
-                           const void* x0, int64_t strideX0, const void* Q, const void* R,
+                           int integrator, const void* x0, int64_t strideX0, const void* Q, const void* R,
                            const void* Qf, const void* xlo, const void* xhi, int64_t strideXb,
                            const void* lb, const void* ub, int64_t strideLb, void* U,
                            const void* Z, const void* yq, const void* piq,

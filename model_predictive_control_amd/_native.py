@@ -19,9 +19,12 @@ F64 = 0
 F32 = 1
 TV = 1
 IPM = 2
+STRICT = 4
 STATUS_POLISHED = 1 << 24
 SQP_DONE = 1
 SQP_EXACT = 2
+MODEL_FE = 0
+MODEL_RK4 = 1
 PLANT_FE = 0
 PLANT_RK4 = 1
 PLANT_RK4_SUB = 2
@@ -77,10 +80,13 @@ SIGNATURES = {
                            _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                            _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                            _vp, _i64, _vp, _i64,
-                           _vp, _vp, _vp, _vp, _vp, _vp, _i, _d, _vp, ctypes.c_size_t, _vp]),
+                           _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int32, _i, _d, _vp,
+                           ctypes.c_size_t, _vp]),
     "mpcqp_bicycle_hessian": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _vp]),
-    "mpcqp_bicycle_sqp_step": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _i64,
+    "mpcqp_bicycle_linearise": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp,
+                                     _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "mpcqp_bicycle_sqp_step": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp, _i64,
                                     _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _vp]),
     "mpcqp_bicycle_plant": (_i, [_i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _i, _vp, _vp,

@@ -25,7 +25,7 @@ from . import _native as nat
 
 __all__ = [
     "condense", "solve_box", "mpc_box", "mpc_qp", "mpc_ipm", "solve_poly", "solve_qp", "sweep", "riccati", "gemv",
-    "rollout", "bicycle_rti", "bicycle_hessian", "bicycle_sqp_step",
+    "rollout", "bicycle_rti", "bicycle_linearise", "bicycle_hessian", "bicycle_sqp_step",
     "pack_lower", "unpack_lower", "status_code", "status_iters", "workspace_bytes",
 ]
 
@@ -320,7 +320,8 @@ def mpc_qp(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=N
 
 def mpc_ipm(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=None, *,
             tv: bool = False, U0=None, H2=None, q2=None, max_iter: int = 0, tol: float = 0.0,
-            out: dict | None = None, ws: torch.Tensor | None = None):
+            strict: bool = False, skip=None, skip_mask: int = 0, out: dict | None = None,
+            ws: torch.Tensor | None = None):
     """The MPC step of ``mpc_qp`` on the stage-wise interior point, any horizon
     (include/mpcqp.h ``mpcqp_mpc_ipm``; nx <= 4, nu <= 2).  U0: optional
     starting inputs (b, N, nu) or (b, N*nu).  H2 (b, N, nx+nu, nx+nu), q2
@@ -328,7 +329,10 @@ def mpc_ipm(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=
     w = [x_k; u_k] (may be indefinite).  Returns a dict with z (b, N*nu),
     X (b, N, nx) = x_1..x_N, y (b, N*nx) state-bound and lam_u (b, N*nu)
     input-bound multipliers (> 0 at the upper bound), pi (b, N, nx) costates
-    of the dynamics, status (b,).  ``out``: a dict of preallocated outputs."""
+    of the dynamics, status (b,).  ``strict``: a non-positive pivot ends an
+    instance with STATUS_NOT_CONVEX instead of regularising.  ``skip`` (b,)
+    int32 with ``skip_mask``: instances with skip & skip_mask != 0 are left
+    untouched.  ``out``: a dict of preallocated outputs."""
     g = _mpc_step_args(A, B, Q, R, Qf, N, x0, xlo, xhi, lb, ub, c, tv)
     dt, dev, batch, n, m, nx = g["dt"], g["dev"], g["batch"], g["n"], g["m"], g["nx"]
     U0t = None if U0 is None else _dev(U0, dt, dev).reshape(batch, n)
@@ -344,11 +348,16 @@ def mpc_ipm(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=
     lib = _lib()
     wsb = int(lib.mpcqp_mpc_ipm_workspace(_code(dt), batch, nx, g["nu"], N))
     ws = _workspace(wsb, dev, ws)
-    rc = lib.mpcqp_mpc_ipm(_code(dt), batch, nx, g["nu"], N, nat.TV if tv else 0, *g["head"],
+    if skip is not None and (skip.dtype != torch.int32 or skip.shape != (batch,)
+                             or skip.device != dev):
+        raise ValueError("skip must be an int32 device tensor of shape (batch,)")
+    flags = (nat.TV if tv else 0) | (nat.STRICT if strict else 0)
+    rc = lib.mpcqp_mpc_ipm(_code(dt), batch, nx, g["nu"], N, flags, *g["head"],
                            _ptr(U0t), 0 if U0t is None else n, _ptr(H2t),
                            0 if H2t is None else N * n2 * n2, _ptr(q2t),
                            0 if q2t is None else N * n2, _ptr(o["z"]), _ptr(o["y"]), _ptr(o["X"]),
-                           _ptr(o["lam_u"]), _ptr(o["pi"]), _ptr(o["status"]), int(max_iter),
+                           _ptr(o["lam_u"]), _ptr(o["pi"]), _ptr(o["status"]), _ptr(skip),
+                           int(skip_mask) if skip is not None else 0, int(max_iter),
                            float(tol), _ptr(ws), wsb, _stream())
     nat.check(rc, "mpcqp_mpc_ipm")
     return o
@@ -680,7 +689,8 @@ def bicycle_hessian(X, U, pi, params, ts: float, flags=None, mu=None,
 
 
 def bicycle_sqp_step(x0, U, Z, yq, piq, y, pi, X, state: dict, params, ts: float, Q, R, Qf,
-                     xlo=None, xhi=None, lb=None, ub=None, tol: float = 1e-9, qp_status=None):
+                     xlo=None, xhi=None, lb=None, ub=None, tol: float = 1e-9, qp_status=None,
+                     integrator: int = 0):
     """Line search + update + NLP optimality residual (include/mpcqp.h
     ``mpcqp_bicycle_sqp_step``), in place on U, y, pi, X and ``state``
     (rho, kkt, mu float64 (b,), flags int32 (b,)).  Bounds: xlo/xhi (N*4,)
@@ -693,11 +703,35 @@ def bicycle_sqp_step(x0, U, Z, yq, piq, y, pi, X, state: dict, params, ts: float
     if ub is not None and ub.ndim == 2:
         slb = 2 * N
     rc = _lib().mpcqp_bicycle_sqp_step(
-        nat.F64, b, N, float(ts), _bike_params(params), _ptr(x0), 4, _ptr(Q), _ptr(R), _ptr(Qf),
+        nat.F64, b, N, float(ts), _bike_params(params), int(integrator), _ptr(x0), 4, _ptr(Q),
+        _ptr(R), _ptr(Qf),
         _ptr(xlo), _ptr(xhi), sxb, _ptr(lb), _ptr(ub), slb, _ptr(U), _ptr(Z), _ptr(yq), _ptr(piq),
         _ptr(qp_status), _ptr(y), _ptr(pi), _ptr(X), _ptr(state["rho"]), _ptr(state["kkt"]), _ptr(state["mu"]),
         _ptr(state["flags"]), float(tol), _stream())
     nat.check(rc, "mpcqp_bicycle_sqp_step")
+
+
+def bicycle_linearise(x0, U, params, ts: float, integrator: int = 0, out: tuple | None = None):
+    """Rollout + linearisation of the prediction model (include/mpcqp.h
+    ``mpcqp_bicycle_linearise``; integrator 0 = forward Euler, 1 = RK4):
+    x0 (b, 4), U (b, N, 2) fp64 -> A (b,N,4,4), B (b,N,4,2), c (b,N,4),
+    X (b,N+1,4)."""
+    b, N = int(U.shape[0]), int(U.shape[1])
+    dev = U.device
+    x0, U = x0.contiguous(), U.contiguous()
+    if out is None:
+        f64 = dict(dtype=torch.float64, device=dev)
+        A = torch.empty((b, N, 4, 4), **f64)
+        B = torch.empty((b, N, 4, 2), **f64)
+        c = torch.empty((b, N, 4), **f64)
+        X = torch.empty((b, N + 1, 4), **f64)
+    else:
+        A, B, c, X = out
+    rc = _lib().mpcqp_bicycle_linearise(nat.F64, b, N, float(ts), _bike_params(params),
+                                        int(integrator), _ptr(x0), 4, _ptr(U), 2 * N, _ptr(X),
+                                        _ptr(A), _ptr(B), _ptr(c), _stream())
+    nat.check(rc, "mpcqp_bicycle_linearise")
+    return A, B, c, X
 
 
 # --------------------------------------------------------------- rollout

@@ -71,7 +71,7 @@ class ClosedLoop:
         x0 = s["xs"][t]
         if ctl.mode == "rti":
             for _ in range(ctl.sqp_iters):
-                A, B, c = batched.bicycle_rti(x0, sqp.U, ctl.params, ctl.ts)
+                A, B, c = ctl._linearise(x0, sqp.U)
                 z, _, st, X = batched.mpc_qp(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, c=c, lb=ctl.lbz,
                                              ub=ctl.ubz, tv=True, states=True, **ctl._box())
                 sqp.U.copy_(z.view_as(sqp.U))

@@ -83,4 +83,102 @@ __device__ __forceinline__ void bike_lag_hess(const Bike& p, const BikePt& q, co
   H[5 * 6 + 5] = ts * hdd;
 }
 
+// f(x, u) and its Jacobians (continuous time)
+__device__ __forceinline__ void bike_f_jac(const Bike& p, const double* x, const double* u,
+                                           double* f, double (&Jx)[4][4], double (&Ju)[4][2]) {
+  const BikePt q = bike_pt(p, x, u);
+  const double v = x[3];
+  f[0] = v * q.ct;
+  f[1] = v * q.st;
+  f[2] = v / p.lr * q.sb;
+  f[3] = p.acc * u[0] - p.fric * v;
+  for (int i = 0; i < 4; ++i) {
+    for (int j = 0; j < 4; ++j) Jx[i][j] = 0.0;
+    Ju[i][0] = Ju[i][1] = 0.0;
+  }
+  Jx[0][2] = -v * q.st;  Jx[0][3] = q.ct;
+  Jx[1][2] = v * q.ct;   Jx[1][3] = q.st;
+  Jx[2][3] = q.sb / p.lr;
+  Jx[3][3] = -p.fric;
+  Ju[0][1] = -v * q.st * q.db;
+  Ju[1][1] = v * q.ct * q.db;
+  Ju[2][1] = v * q.cb * q.db / p.lr;
+  Ju[3][0] = p.acc;
+}
+
+// One RK4 step (runge_kutta4, main.py:138-147) and, when A != nullptr, its
+// Jacobians A = d x+ / dx, B = d x+ / du by forward sensitivities through
+// the four stages (tangent S = d(stage point)/d(x, u), 4 x 6).
+__device__ __forceinline__ void bike_rk4_step_jac(const Bike& p, const double* x,
+                                                  const double* u, double* xn,
+                                                  double (*A)[4], double (*B)[2]) {
+  const double h = p.ts;
+  const double cw[4] = {h / 6.0, h / 3.0, h / 3.0, h / 6.0};  // stage weights
+  const double cs[4] = {0.0, 0.5 * h, 0.5 * h, h};            // stage offsets
+  double k[4] = {0, 0, 0, 0}, dk[4][6];
+  double acc[4], dacc[4][6];
+  for (int i = 0; i < 4; ++i) {
+    acc[i] = x[i];
+    for (int j = 0; j < 6; ++j) { dk[i][j] = 0.0; dacc[i][j] = (j == i) ? 1.0 : 0.0; }
+  }
+  for (int s = 0; s < 4; ++s) {
+    double xs[4], S[4][6];
+    for (int i = 0; i < 4; ++i) {
+      xs[i] = x[i] + cs[s] * k[i];
+      for (int j = 0; j < 6; ++j) S[i][j] = ((j == i) ? 1.0 : 0.0) + cs[s] * dk[i][j];
+    }
+    double f[4], Jx[4][4], Ju[4][2];
+    bike_f_jac(p, xs, u, f, Jx, Ju);
+    for (int i = 0; i < 4; ++i) {
+      k[i] = f[i];
+      acc[i] += cw[s] * f[i];
+    }
+    if (A) {
+      double nk[4][6];
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 6; ++j) {
+          double t = j >= 4 ? Ju[i][j - 4] : 0.0;
+          for (int q2 = 0; q2 < 4; ++q2) t = fma(Jx[i][q2], S[q2][j], t);
+          nk[i][j] = t;
+        }
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 6; ++j) {
+          dk[i][j] = nk[i][j];
+          dacc[i][j] += cw[s] * nk[i][j];
+        }
+    }
+  }
+  for (int i = 0; i < 4; ++i) xn[i] = acc[i];
+  if (A)
+    for (int i = 0; i < 4; ++i) {
+      for (int j = 0; j < 4; ++j) A[i][j] = dacc[i][j];
+      B[i][0] = dacc[i][4];
+      B[i][1] = dacc[i][5];
+    }
+}
+
+// the prediction model of the OCP: 0 = forward Euler (main.py:132-135),
+// 1 = RK4 (main.py:138-147, the model template.py:141 builds on)
+__device__ __forceinline__ void model_step(const Bike& p, int integ, const double* x,
+                                           const double* u, double* xn) {
+  if (integ == 1) {
+    bike_rk4_step_jac(p, x, u, xn, nullptr, nullptr);
+  } else {
+    const BikePt q = bike_pt(p, x, u);
+    bike_step(p, q, x, u, xn);
+  }
+}
+
+__device__ __forceinline__ void model_step_jac(const Bike& p, int integ, const double* x,
+                                               const double* u, double* xn, double (&A)[4][4],
+                                               double (&B)[4][2]) {
+  if (integ == 1) {
+    bike_rk4_step_jac(p, x, u, xn, A, B);
+  } else {
+    const BikePt q = bike_pt(p, x, u);
+    bike_step(p, q, x, u, xn);
+    bike_jac(p, q, x, A, B);
+  }
+}
+
 }  // namespace mpcqp

@@ -15,6 +15,9 @@
 // runs the same sequence of operations on its own data (no divergence except
 // the iteration count, which the wave pays as its maximum), and every
 // workspace access is one fp64 per lane at consecutive addresses.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.hpp"
 
 #define MPCQP_HD __host__ __device__
@@ -29,7 +32,36 @@ __global__ __launch_bounds__(64) void ipm_kernel(ipm::Args<T> a) {
   ipm::solve_lane<T, NX, NU>(a, b);
 }
 
+// The same lane routine with the instance's workspace in LDS: G instances
+// per single-wave workgroup (lanes >= G idle), field stride G doubles so the
+// active lanes hit consecutive banks.  Every workspace access is then an LDS
+// round trip instead of an HBM one; it is the latency-bound small/medium-batch
+// variant (the per-stage sweeps are serial in each lane either way).
+template <typename T, int NX, int NU>
+__global__ __launch_bounds__(64) void ipm_lds_kernel(ipm::Args<T> a, int G) {
+  extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
+  const int lane = threadIdx.x;
+  const int b = blockIdx.x * G + lane;
+  if (lane >= G || b >= a.batch) return;
+  ipm::solve_lane<T, NX, NU>(a, b, ipm_lds + lane, G);
+}
+
 static int64_t ipm_ldb(int batch) { return ((int64_t)batch + 63) / 64 * 64; }
+
+// LDS variant: bytes of one instance's workspace, and instances per
+// workgroup (0 = does not fit).  MPCQP_IPM_LDS=0/1 forces the choice.
+static int ipm_lds_group(int batch, int F, int N) {
+  const size_t per = (size_t)N * F * sizeof(double);
+  const char* env = getenv("MPCQP_IPM_LDS");
+  if (env && atoi(env) == 0) return 0;
+  const size_t budget = 64 * 1024;
+  if (per > 160 * 1024) return 0;
+  int G = (int)std::max<size_t>(1, std::min<size_t>(64, budget / per));
+  // large batches: the global-workspace kernel keeps 64 lanes busy per wave
+  const bool small = (int64_t)batch <= (int64_t)256 * 3 * G;
+  if (!small && !(env && atoi(env) == 1)) return 0;
+  return G;
+}
 
 static bool ipm_dims(int nx, int nu, int& NX, int& NU) {
   if (nx <= 2 && nu <= 1) { NX = 2; NU = 1; return true; }
@@ -49,17 +81,34 @@ bool ipm_supported(int nx, int nu) {
   return ipm_dims(nx, nu, NX, NU);
 }
 
+template <typename T, int NX, int NU>
+static int ipm_launch_t(ipm::Args<T>& a, hipStream_t st) {
+  const int F = ipm::Layout<NX, NU>::F;
+  const int G = ipm_lds_group(a.batch, F, a.N);
+  const dim3 blk(64);
+  if (G > 0) {
+    const size_t bytes = (size_t)G * a.N * F * sizeof(double);
+    if (bytes > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)ipm_lds_kernel<T, NX, NU>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+      if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(ipm_lds)");
+    }
+    hipLaunchKernelGGL((ipm_lds_kernel<T, NX, NU>), dim3((unsigned)((a.batch + G - 1) / G)), blk,
+                       bytes, st, a, G);
+    MPCQP_CHECK_LAUNCH("ipm_lds_kernel");
+    return MPCQP_OK;
+  }
+  hipLaunchKernelGGL((ipm_kernel<T, NX, NU>), dim3((unsigned)((a.batch + 63) / 64)), blk, 0, st,
+                     a);
+  MPCQP_CHECK_LAUNCH("ipm_kernel");
+  return MPCQP_OK;
+}
+
 template <typename T>
 static int ipm_launch(ipm::Args<T>& a, hipStream_t st) {
   int NX, NU;
   ipm_dims(a.nx, a.nu, NX, NU);
-  const dim3 grid((unsigned)((a.batch + 63) / 64)), blk(64);
-  if (NX == 2)
-    hipLaunchKernelGGL((ipm_kernel<T, 2, 1>), grid, blk, 0, st, a);
-  else
-    hipLaunchKernelGGL((ipm_kernel<T, 4, 2>), grid, blk, 0, st, a);
-  MPCQP_CHECK_LAUNCH("ipm_kernel");
-  return MPCQP_OK;
+  return NX == 2 ? ipm_launch_t<T, 2, 1>(a, st) : ipm_launch_t<T, 4, 2>(a, st);
 }
 
 int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const void* A,
@@ -68,8 +117,9 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
                  const void* x0, int64_t sX0, const void* xlo, const void* xhi, int64_t sXb,
                  const void* lb, int64_t sLb, const void* ub, int64_t sUb, const void* U0,
                  int64_t sU0, const void* H2, int64_t sH2, const void* q2, int64_t sq2, void* z,
-                 void* y, void* X, void* lam_u, void* pi, int32_t* status, int max_iter,
-                 double tol, void* ws, size_t ws_bytes, hipStream_t st) {
+                 void* y, void* X, void* lam_u, void* pi, int32_t* status,
+                 const int32_t* skip, int32_t skip_mask, int max_iter, double tol, void* ws,
+                 size_t ws_bytes, hipStream_t st) {
   const size_t need = ipm_ws_bytes(batch, nx, nu, N);
   MPCQP_CHECK_ARG(ws && ws_bytes >= need, "mpcqp_mpc_ipm: workspace %zu bytes < %zu", ws_bytes,
                   need);
@@ -77,6 +127,7 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
     using T = decltype(tp);
     a.batch = batch; a.nx = nx; a.nu = nu; a.N = N; a.tv = (flags & MPCQP_TV) ? 1 : 0;
     a.max_iter = max_iter > 0 ? max_iter : 100;
+    a.strict = (flags & MPCQP_STRICT) ? 1 : 0;
     a.tol = tol > 0 ? tol : 1e-10;
     a.tol_mu = 1e-2 * a.tol;
     a.tol_polish = 1e-6;
@@ -89,6 +140,7 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
     a.U0 = (const T*)U0; a.sU0 = sU0;
     a.H2 = (const T*)H2; a.sH2 = sH2; a.q2 = (const T*)q2; a.sq2 = sq2;
     a.z = (T*)z; a.y = (T*)y; a.X = (T*)X; a.lam_u = (T*)lam_u; a.pi = (T*)pi; a.status = status;
+    a.skip = skip; a.skip_mask = skip_mask;
     a.ws = (double*)ws; a.ldb = ipm_ldb(batch);
   };
   if (dtype == MPCQP_F64) {
@@ -116,8 +168,9 @@ extern "C" int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int fl
                              int64_t strideXb, const void* lb, int64_t strideLb, const void* ub,
                              int64_t strideUb, const void* U0, int64_t strideU0, const void* H2,
                              int64_t strideH2, const void* q2, int64_t strideq2, void* z, void* y,
-                             void* X, void* lam_u, void* pi, int32_t* status, int max_iter,
-                             double tol, void* ws, size_t ws_bytes, void* stream) {
+                             void* X, void* lam_u, void* pi, int32_t* status,
+                             const int32_t* skip, int32_t skip_mask, int max_iter, double tol,
+                             void* ws, size_t ws_bytes, void* stream) {
   using namespace mpcqp;
   MPCQP_CHECK_ARG(dtype == MPCQP_F64 || dtype == MPCQP_F32, "mpcqp_mpc_ipm: bad dtype %d", dtype);
   MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "mpcqp_mpc_ipm: bad sizes (batch=%d, N=%d)", batch, N);
@@ -136,5 +189,6 @@ extern "C" int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int fl
   return mpc_ipm_impl(dtype, batch, nx, nu, N, flags, A, strideA, Bm, strideB, Q, strideQ, R,
                       strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi, strideXb, lb,
                       strideLb, ub, strideUb, U0, strideU0, H2, strideH2, q2, strideq2, z, y, X,
-                      lam_u, pi, status, max_iter, tol, ws, ws_bytes, (hipStream_t)stream);
+                      lam_u, pi, status, skip, skip_mask, max_iter, tol, ws, ws_bytes,
+                      (hipStream_t)stream);
 }

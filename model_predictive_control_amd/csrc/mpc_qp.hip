@@ -176,7 +176,7 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
     return mpc_ipm_impl(dtype, batch, nx, nu, N, flags, A, strideA, Bm, strideB, Q, strideQ, R,
                         strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi, strideXb, lb,
                         strideLb, ub, strideUb, nullptr, 0, nullptr, 0, nullptr, 0, z, y, X,
-                        nullptr, nullptr, status, max_iter, tol, ws, ws_bytes,
+                        nullptr, nullptr, status, nullptr, 0, max_iter, tol, ws, ws_bytes,
                         (hipStream_t)stream);
   }
   MPCQP_CHECK_ARG(n + m <= max_qp_size_dtype(dtype),

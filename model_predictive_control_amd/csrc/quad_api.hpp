@@ -70,8 +70,9 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
                  const void* x0, int64_t sX0, const void* xlo, const void* xhi, int64_t sXb,
                  const void* lb, int64_t sLb, const void* ub, int64_t sUb, const void* U0,
                  int64_t sU0, const void* H2, int64_t sH2, const void* q2, int64_t sq2, void* z,
-                 void* y, void* X, void* lam_u, void* pi, int32_t* status, int max_iter,
-                 double tol, void* ws, size_t ws_bytes, hipStream_t st);
+                 void* y, void* X, void* lam_u, void* pi, int32_t* status,
+                 const int32_t* skip, int32_t skip_mask, int max_iter, double tol, void* ws,
+                 size_t ws_bytes, hipStream_t st);
 size_t qp_ws_bytes(int dtype, int batch, int n, int m);
 struct PfDyn;
 // dyn != NULL: refine from the dynamics (pf.hpp); refine < 0: default steps

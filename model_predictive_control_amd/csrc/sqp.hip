@@ -16,6 +16,8 @@
 // damped Levenberg-Marquardt style by a proximal term mu/2 |w - w_k|^2 per
 // stage: a full step divides mu by 4 (down to 0), a step that needs
 // backtracking or a QP that fails multiplies it by 4 (at least 1e-3).
+#include <cstdlib>
+
 #include "bike.hpp"
 
 namespace mpcqp {
@@ -57,7 +59,7 @@ __global__ void bike_hess_kernel(int batch, int N, Bike p, const double* X, cons
 }
 
 struct SqpArgs {
-  int batch, N;
+  int batch, N, integ;  // integ: prediction model, 0 = forward Euler, 1 = RK4
   Bike p;
   const double* x0; int64_t sX0;
   const double *Q, *R, *Qf;
@@ -70,6 +72,7 @@ struct SqpArgs {
   double *rho, *kkt, *mu;
   int32_t* flags;
   double tol;
+  double sw, mu_floor, mu_dec;  // Hessian switch, damping after a failed step, decrease factor
 };
 
 // 1/2 J(U) and the l1 violation of the state box along a rollout
@@ -109,9 +112,8 @@ __device__ Merit merit_at(const SqpArgs& a, int64_t b, double alpha) {
     double u[2];
     for (int r = 0; r < 2; ++r) u[r] = fma(alpha, Z[k * 2 + r] - U[k * 2 + r], U[k * 2 + r]);
     m.J += 0.5 * (sq_form(a.Q, 4, x) + sq_form(a.R, 2, u));
-    const BikePt pt = bike_pt(a.p, x, u);
     double xn[4];
-    bike_step(a.p, pt, x, u, xn);
+    model_step(a.p, a.integ, x, u, xn);
     for (int i = 0; i < 4; ++i) x[i] = xn[i];
     m.viol += box_viol(a, b, k, x);
   }
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
     // converged): no step; an exact-Hessian iteration falls back to
     // Gauss-Newton (positive definite) until the residual drops 10x
     const int iters = ((fl >> 8) & 0xFFFF) + 1;
-    if (fl & kSqpExact) a.mu[b] = fmax(4.0 * a.mu[b], 1e-3);
+    if (fl & kSqpExact) a.mu[b] = fmax(4.0 * a.mu[b], a.mu_floor);
     a.flags[b] = (iters << 8) | (fl & kSqpExact);
     return;
   }
@@ -169,10 +171,8 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
         for (int q = 0; q < 2; ++q) t = fma(a.R[r * 2 + q], u[q], t);
         D = fma(t, d[r], D);
       }
-      const BikePt pt = bike_pt(a.p, x, u);
       double A[4][4], B[4][2], xn[4], dxn[4];
-      bike_jac(a.p, pt, x, A, B);
-      bike_step(a.p, pt, x, u, xn);
+      model_step_jac(a.p, a.integ, x, u, xn, A, B);
       for (int i = 0; i < 4; ++i) {
         double s = B[i][0] * d[0] + B[i][1] * d[1];
         for (int j = 0; j < 4; ++j) s = fma(A[i][j], dx[j], s);
@@ -222,9 +222,8 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
     for (int i = 0; i < 4; ++i) X[i] = x[i] = a.x0[b * a.sX0 + i];
     for (int k = 0; k < N; ++k) {
       const double u[2] = {U[2 * k], U[2 * k + 1]};
-      const BikePt pt = bike_pt(a.p, x, u);
       double xn[4];
-      bike_step(a.p, pt, x, u, xn);
+      model_step(a.p, a.integ, x, u, xn);
       for (int i = 0; i < 4; ++i) X[(k + 1) * 4 + i] = x[i] = xn[i];
     }
   }
@@ -240,9 +239,8 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
     for (int k = N - 1; k >= 0; --k) {
       const double* x = X + k * 4;
       const double u[2] = {U[2 * k], U[2 * k + 1]};
-      const BikePt pt = bike_pt(a.p, x, u);
-      double A[4][4], B[4][2];
-      bike_jac(a.p, pt, x, A, B);
+      double A[4][4], B[4][2], xn[4];
+      model_step_jac(a.p, a.integ, x, u, xn, A, B);
       for (int q = 0; q < 2; ++q) {
         double g = 0.0;
         for (int j = 0; j < 2; ++j) g = fma(a.R[q * 2 + j], u[j], g);
@@ -281,15 +279,58 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
   // ---------------------------------------------------- Hessian mode, flags
   if (fl & kSqpExact) {
     double mu = a.mu[b];
-    mu = alpha == 1.0 ? (mu > 4e-12 ? 0.25 * mu : 0.0) : fmax(4.0 * mu, 1e-3);
+    mu = alpha == 1.0 ? (mu > 4e-12 ? a.mu_dec * mu : 0.0) : fmax(4.0 * mu, a.mu_floor);
     a.mu[b] = mu;
   }
   const int iters = ((fl >> 8) & 0xFFFF) + 1;
-  const bool exact = (fl & kSqpExact) || r < kSqpSwitch;  // sticky
+  const bool exact = (fl & kSqpExact) || r < a.sw;  // sticky
   fl = (iters << 8) | (r <= a.tol ? kSqpDone : 0) | (exact ? kSqpExact : 0);
   a.flags[b] = fl;
   a.rho[b] = rho;
   a.kkt[b] = r;
+}
+
+// ------------------------------------------------------- linearisation
+// The prediction model linearised along the rollout of U (the RTI / SQP
+// linearisation, main.py:41-113 on fwd_euler or runge_kutta4,
+// main.py:132-147; template.py:141 builds its OCP on RK4): phase 1 (lane =
+// instance) rolls out X, phase 2 (lane = (instance, stage)) writes
+//   A_k = d x+/dx, B_k = d x+/du at (x_k, u_k), c_k = x_{k+1} - A_k x_k - B_k u_k
+// in the layout of mpcqp_condense(MPCQP_TV) and mpcqp_mpc_ipm.
+__global__ void model_rollout_kernel(int batch, int N, Bike p, int integ, const double* x0,
+                                     int64_t sX0, const double* U, int64_t sU, double* X) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  double x[4];
+  for (int i = 0; i < 4; ++i) X[(int64_t)b * (N + 1) * 4 + i] = x[i] = x0[(int64_t)b * sX0 + i];
+  for (int k = 0; k < N; ++k) {
+    const double u[2] = {U[(int64_t)b * sU + 2 * k], U[(int64_t)b * sU + 2 * k + 1]};
+    double xn[4];
+    model_step(p, integ, x, u, xn);
+    for (int i = 0; i < 4; ++i) X[((int64_t)b * (N + 1) + k + 1) * 4 + i] = x[i] = xn[i];
+  }
+}
+
+__global__ void model_jac_kernel(int batch, int N, Bike p, int integ, const double* U, int64_t sU,
+                                 const double* X, double* Ao, double* Bo, double* co) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)batch * N) return;
+  const int64_t b = e / N;
+  const int k = (int)(e - b * N);
+  const double* x = X + (b * (N + 1) + k) * 4;
+  const double u[2] = {U[b * sU + 2 * k], U[b * sU + 2 * k + 1]};
+  double A[4][4], B[4][2], xn[4];
+  model_step_jac(p, integ, x, u, xn, A, B);
+  for (int i = 0; i < 4; ++i) {
+    double s = xn[i] - B[i][0] * u[0] - B[i][1] * u[1];
+    for (int j = 0; j < 4; ++j) {
+      Ao[e * 16 + i * 4 + j] = A[i][j];
+      s -= A[i][j] * x[j];
+    }
+    Bo[e * 8 + i * 2] = B[i][0];
+    Bo[e * 8 + i * 2 + 1] = B[i][1];
+    co[e * 4 + i] = s;
+  }
 }
 
 // -------------------------------------------------- receding-horizon loop
@@ -404,7 +445,8 @@ extern "C" int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, con
 }
 
 extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,
-                                      const double* params, const void* x0, int64_t strideX0,
+                                      const double* params, int integrator, const void* x0,
+                                      int64_t strideX0,
                                       const void* Q, const void* R, const void* Qf,
                                       const void* xlo, const void* xhi, int64_t strideXb,
                                       const void* lb, const void* ub, int64_t strideLb, void* U,
@@ -422,9 +464,11 @@ extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,
                   "mpcqp_bicycle_sqp_step: bad axle lengths");
   MPCQP_CHECK_ARG(strideX0 >= 0 && strideXb >= 0 && strideLb >= 0,
                   "mpcqp_bicycle_sqp_step: negative stride");
+  MPCQP_CHECK_ARG(integrator == MPCQP_MODEL_FE || integrator == MPCQP_MODEL_RK4,
+                  "mpcqp_bicycle_sqp_step: integrator %d", integrator);
   if (batch == 0) return MPCQP_OK;
   SqpArgs a;
-  a.batch = batch; a.N = N; a.p = bike_of(ts, params);
+  a.batch = batch; a.N = N; a.p = bike_of(ts, params); a.integ = integrator;
   a.x0 = (const double*)x0; a.sX0 = strideX0;
   a.Q = (const double*)Q; a.R = (const double*)R; a.Qf = (const double*)Qf;
   a.xlo = (const double*)xlo; a.xhi = (const double*)xhi; a.sXb = strideXb;
@@ -433,6 +477,10 @@ extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,
   a.qp_status = qp_status;
   a.y = (double*)y; a.pi = (double*)pi; a.X = (double*)X;
   a.rho = rho; a.kkt = kkt; a.mu = mu; a.flags = flags; a.tol = tol > 0 ? tol : 1e-9;
+  auto envd = [](const char* k, double d) { const char* v = getenv(k); return v ? atof(v) : d; };
+  a.sw = envd("MPCQP_SQP_SWITCH", kSqpSwitch);
+  a.mu_floor = envd("MPCQP_SQP_MUFLOOR", 1e-3);
+  a.mu_dec = envd("MPCQP_SQP_MUDEC", 0.25);
   hipLaunchKernelGGL(sqp_step_kernel, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0,
                      (hipStream_t)stream, a);
   MPCQP_CHECK_LAUNCH("sqp_step_kernel");
@@ -469,5 +517,33 @@ extern "C" int mpcqp_sqp_shift(int dtype, int batch, int N, void* U, void* y, vo
                      (hipStream_t)stream, batch, N, (double*)U, (double*)y, (double*)pi, flags,
                      rho, mu, kkt, mu0);
   MPCQP_CHECK_LAUNCH("sqp_shift_kernel");
+  return MPCQP_OK;
+}
+
+extern "C" int mpcqp_bicycle_linearise(int dtype, int batch, int N, double ts,
+                                       const double* params, int integrator, const void* x0,
+                                       int64_t strideX0, const void* U, int64_t strideU, void* X,
+                                       void* A, void* B, void* c, void* stream) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_bicycle_linearise: MPCQP_F64 only");
+  MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "mpcqp_bicycle_linearise: bad sizes");
+  MPCQP_CHECK_ARG(integrator == MPCQP_MODEL_FE || integrator == MPCQP_MODEL_RK4,
+                  "mpcqp_bicycle_linearise: integrator %d", integrator);
+  MPCQP_CHECK_ARG(params && x0 && U && X && A && B && c, "mpcqp_bicycle_linearise: null pointer");
+  MPCQP_CHECK_ARG(params[1] > 0 && params[0] + params[1] > 0,
+                  "mpcqp_bicycle_linearise: bad axle lengths");
+  MPCQP_CHECK_ARG(strideX0 >= 4 && strideU >= 2 * N, "mpcqp_bicycle_linearise: bad strides");
+  if (batch == 0) return MPCQP_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const Bike p = bike_of(ts, params);
+  hipLaunchKernelGGL(model_rollout_kernel, dim3((batch + 63) / 64), dim3(64), 0, st, batch, N, p,
+                     integrator, (const double*)x0, strideX0, (const double*)U, strideU,
+                     (double*)X);
+  MPCQP_CHECK_LAUNCH("model_rollout_kernel");
+  const int64_t total = (int64_t)batch * N;
+  hipLaunchKernelGGL(model_jac_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     batch, N, p, integrator, (const double*)U, strideU, (const double*)X,
+                     (double*)A, (double*)B, (double*)c);
+  MPCQP_CHECK_LAUNCH("model_jac_kernel");
   return MPCQP_OK;
 }

@@ -37,6 +37,7 @@ import warnings
 import numpy as np
 import torch
 
+from . import _native as nat
 from . import batched
 from ._native import SQP_DONE, STATUS_MAXITER, STATUS_OPTIMAL
 from .bicycle import KinematicBicycle
@@ -51,6 +52,7 @@ class MPCController:
     def __init__(self, N: int, ts: float, params: VehicleParameters | None = None, model=None,
                  x_obs=None, *, Q=None, QN=None, R=None, mode: str = "sqp",
                  max_iter: int = 200, tol: float = 1e-9, hessian: str = "exact",
+                 integrator: str = "fe",
                  sqp_iters: int = 3, state_box: bool = True, dtype=torch.float64,
                  device=None) -> None:
         self.N = N
@@ -76,6 +78,15 @@ class MPCController:
             raise ValueError(f"mode must be 'sqp' or 'rti', got {mode!r}")
         if hessian not in ("exact", "gauss-newton"):
             raise ValueError(f"hessian must be 'exact' or 'gauss-newton', got {hessian!r}")
+        if integrator not in ("fe", "rk4"):
+            raise ValueError(f"integrator must be 'fe' or 'rk4', got {integrator!r}")
+        # the prediction model: fwd_euler (main.py:132-135, the model of
+        # main.py:76 and session4_sol.py:192) or runge_kutta4 (main.py:138-147,
+        # template.py:141); the exact Hessian is the FE model's, so an RK4
+        # controller iterates with Gauss-Newton
+        self.integrator = integrator
+        if integrator == "rk4":
+            hessian = "gauss-newton"
         self.mode, self.hessian = mode, hessian
         self.max_iter, self.tol = int(max_iter), float(tol)
         self.nx, self.nu = 4, 2
@@ -128,6 +139,14 @@ class MPCController:
             return self._warm.clone()
         return torch.zeros((b, self.N, self.nu), dtype=self.dtype, device=self.device)
 
+    def _linearise(self, X0, U):
+        """(A_k, B_k, c_k) along the rollout of U (the RTI linearisation)."""
+        if self.integrator == "rk4":
+            A, B, c, _ = batched.bicycle_linearise(X0.double(), U.double(), self.params, self.ts,
+                                                   nat.MODEL_RK4)
+            return A.to(self.dtype), B.to(self.dtype), c.to(self.dtype)
+        return batched.bicycle_rti(X0, U, self.params, self.ts)
+
     def _box(self):
         return dict(xlo=self.xmin, xhi=self.xmax) if self.state_box else {}
 
@@ -138,7 +157,7 @@ class MPCController:
         z = status = X = None
         for _ in range(self.sqp_iters):
             # FE rollout from x0 under U + per-stage (A_k, B_k, c_k): one launch
-            A, B, c = batched.bicycle_rti(X0, U, self.params, self.ts)
+            A, B, c = self._linearise(X0, U)
             # condense + QP (+ predicted states) in one libmpcqp call
             z, lam, status, X = batched.mpc_qp(A, B, self.Q, self.R, self.QN, N, X0, c=c,
                                                lb=self.lbz, ub=self.ubz, tv=True, states=True,
@@ -236,9 +255,14 @@ class SqpSolver:
       -> mpcqp_bicycle_sqp_step
 
     Instances that reach the KKT tolerance are frozen by the step kernel
-    (flag SQP_DONE); the others keep iterating."""
+    (flag SQP_DONE): the interior point skips them and the others keep
+    iterating."""
 
-    MU0 = 0.1  # initial Levenberg-Marquardt damping of the exact-Hessian QPs
+    MU0 = float(__import__("os").environ.get("MPCQP_SQP_MU0", 0.1))  # initial Levenberg-Marquardt damping of the exact-Hessian QPs
+    # interior-point budget of one QP: a convex one takes 6-10 iterations; one
+    # that is not (strict: first non-positive pivot) or stalls is abandoned
+    # and the step kernel raises the damping instead
+    QP_MAX_ITER = 40
 
     def __init__(self, ctl: "MPCController", b: int):
         self.ctl, self.b = ctl, b
@@ -273,17 +297,23 @@ class SqpSolver:
 
     def iterate(self, X0):
         ctl, N, box = self.ctl, self.ctl.N, self.box
-        A, B, c, Xr = batched.bicycle_rti(X0, self.U, ctl.params, ctl.ts, states=True)
+        if ctl.integrator == "rk4":
+            A, B, c, Xr = batched.bicycle_linearise(X0, self.U, ctl.params, ctl.ts, nat.MODEL_RK4)
+        else:
+            A, B, c, Xr = batched.bicycle_rti(X0, self.U, ctl.params, ctl.ts, states=True)
         H2 = q2 = None
         if ctl.hessian == "exact":
             H2, q2 = batched.bicycle_hessian(Xr, self.U, self.pi, ctl.params, ctl.ts,
                                              flags=self.flags, mu=self.mu)
         self.qp = batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, X0, lb=ctl.lbz, ub=ctl.ubz,
-                                  c=c, tv=True, H2=H2, q2=q2, out=self.qp, **box)
+                                  c=c, tv=True, H2=H2, q2=q2, strict=True, skip=self.flags,
+                                  skip_mask=SQP_DONE, max_iter=self.QP_MAX_ITER, out=self.qp,
+                                  **box)
         batched.bicycle_sqp_step(X0, self.U, self.qp["z"], self.qp["y"], self.qp["pi"], self.y,
                                  self.pi, self.X, self.state(), ctl.params, ctl.ts, ctl.Q, ctl.R,
                                  ctl.QN, xlo=box.get("xlo"), xhi=box.get("xhi"), lb=ctl.lbz,
-                                 ub=ctl.ubz, tol=ctl.tol, qp_status=self.qp["status"])
+                                 ub=ctl.ubz, tol=ctl.tol, qp_status=self.qp["status"],
+                                 integrator=nat.MODEL_RK4 if ctl.integrator == "rk4" else nat.MODEL_FE)
 
     def done(self):
         return (self.flags & SQP_DONE) != 0

@@ -43,22 +43,35 @@ def fe(x, u, ts, prm=PARAMS):
     return x + ts * f_ode(x, u, prm)
 
 
-def fe_jac(x, u, ts, prm=PARAMS, h=1e-30):
-    """A = d fe / dx, B = d fe / du by the complex step (exact to rounding)."""
+def rk4(x, u, ts, prm=PARAMS):
+    """main.py:138-147 (the model template.py:141 builds its OCP on)."""
+    s1 = f_ode(x, u, prm)
+    s2 = f_ode(x + ts / 2 * s1, u, prm)
+    s3 = f_ode(x + ts / 2 * s2, u, prm)
+    s4 = f_ode(x + ts * s3, u, prm)
+    return x + ts / 6 * (s1 + 2 * s2 + 2 * s3 + s4)
+
+
+STEPS = {"fe": fe, "rk4": rk4}
+
+
+def fe_jac(x, u, ts, prm=PARAMS, h=1e-30, step=fe):
+    """A = d step / dx, B = d step / du by the complex step (exact to
+    rounding); step = fe (default) or rk4."""
     x = np.asarray(x, complex)
     u = np.asarray(u, complex)
     A = np.zeros((4, 4))
     B = np.zeros((4, 2))
     for i in range(4):
         d = np.zeros(4, complex); d[i] = 1j * h
-        A[:, i] = fe(x + d, u, ts, prm).imag / h
+        A[:, i] = step(x + d, u, ts, prm).imag / h
     for i in range(2):
         d = np.zeros(2, complex); d[i] = 1j * h
-        B[:, i] = fe(x, u + d, ts, prm).imag / h
+        B[:, i] = step(x, u + d, ts, prm).imag / h
     return A, B
 
 
-def _stage_curvature(w, lam, ts, prm, e=1e-6):
+def _stage_curvature(w, lam, ts, prm, step=fe, e=1e-6):
     """sum_i lam_i d2 fe_i / dw2 at w = [x; u] (6 x 6): central differences of
     the complex-step gradient of lam' fe."""
     def grad(wv):
@@ -67,7 +80,7 @@ def _stage_curvature(w, lam, ts, prm, e=1e-6):
             d = np.zeros(6, complex)
             d[j] = 1e-30j
             ww = wv + d
-            out[j] = (lam @ fe(ww[:4], ww[4:], ts, prm)).imag / 1e-30
+            out[j] = (lam @ step(ww[:4], ww[4:], ts, prm)).imag / 1e-30
         return out
     H = np.zeros((6, 6))
     for j in range(6):
@@ -80,8 +93,9 @@ def _stage_curvature(w, lam, ts, prm, e=1e-6):
 class OCP:
     """The NLP of one MPC step; the cost is the reference's (not halved)."""
 
-    def __init__(self, N, ts, Q, QN, R, xlo, xhi, lbu, ubu, prm=PARAMS):
+    def __init__(self, N, ts, Q, QN, R, xlo, xhi, lbu, ubu, prm=PARAMS, model="fe"):
         self.N, self.ts = N, ts
+        self.step = STEPS[model]
         self.Q, self.QN, self.R = (np.asarray(v, float) for v in (Q, QN, R))
         self.xlo, self.xhi = np.asarray(xlo, float), np.asarray(xhi, float)
         self.lbu, self.ubu = np.asarray(lbu, float), np.asarray(ubu, float)
@@ -91,7 +105,7 @@ class OCP:
         U = np.asarray(U).reshape(self.N, 2)
         xs = [np.asarray(x0, U.dtype if np.iscomplexobj(U) else float)]
         for k in range(self.N):
-            xs.append(fe(xs[-1], U[k], self.ts, self.prm))
+            xs.append(self.step(xs[-1], U[k], self.ts, self.prm))
         return np.array(xs)
 
     def cost(self, x0, U):
@@ -105,7 +119,7 @@ class OCP:
         X = self.rollout(x0, U)
         A = np.zeros((self.N, 4, 4)); B = np.zeros((self.N, 4, 2)); c = np.zeros((self.N, 4))
         for k in range(self.N):
-            A[k], B[k] = fe_jac(X[k], U[k], self.ts, self.prm)
+            A[k], B[k] = fe_jac(X[k], U[k], self.ts, self.prm, step=self.step)
             c[k] = X[k + 1] - A[k] @ X[k] - B[k] @ U[k]
         return X, A, B, c
 
@@ -185,7 +199,7 @@ class OCP:
         HL = np.zeros((2 * N, 2 * N))
         for k in range(N):
             w = np.concatenate([X[k], Ur[k]])
-            L = _stage_curvature(w, lam[k + 1], self.ts, self.prm)
+            L = _stage_curvature(w, lam[k + 1], self.ts, self.prm, self.step)
             M = np.zeros((6, 2 * N))
             if k > 0:
                 M[:4] = d["Gam"][(k - 1) * 4:k * 4]

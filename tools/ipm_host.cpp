@@ -22,6 +22,7 @@ extern "C" int ipm_host_solve(int batch, int nx, int nu, int N, int tv, const do
   ipm::Args<double> a{};
   a.batch = batch; a.nx = nx; a.nu = nu; a.N = N; a.tv = tv;
   a.max_iter = max_iter; a.tol = tol; a.tol_mu = 1e-2 * tol; a.tol_polish = 1e-6; a.mu_polish = getenv("MUP") ? atof(getenv("MUP")) : 1e-6;
+  a.strict = getenv("STRICT") ? atoi(getenv("STRICT")) : 0;
   a.A = A; a.sA = sA; a.B = B; a.sB = sB; a.c = c; a.sC = sC;
   a.Q = Q; a.R = R; a.Qf = Qf; a.x0 = x0; a.sX0 = nx;
   a.xlo = xlo; a.xhi = xhi; a.sXb = 0; a.lb = lb; a.ub = ub;
