@@ -80,9 +80,9 @@ extern "C" {
 /* condense / MPC-step flags */
 #define MPCQP_TV 1  /* A, B are per-stage: N*nx*nx / N*nx*nu per instance */
 #define MPCQP_IPM 2 /* mpcqp_mpc_qp: solve on the stage-wise interior point (mpcqp_mpc_ipm) */
-/* mpcqp_mpc_ipm: a non-positive Riccati pivot ends the solve with
-   MPCQP_STATUS_NOT_CONVEX at once instead of regularising (an SQP caller
-   raises its own damping and retries) */
+/* mpcqp_mpc_ipm: after a few (6) inertia corrections of non-positive
+   Riccati pivots the solve ends with MPCQP_STATUS_NOT_CONVEX instead of
+   regularising further (an SQP caller raises its own damping and retries) */
 #define MPCQP_STRICT 4
 
 /* status bit 24: the solution was polished to the exact active-set vertex */
@@ -319,7 +319,7 @@ int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
  * costates of x_{k+1} = A_k x_k + B_k u_k + c_k; y (optional, N*nx):
  * state-bound multipliers, > 0 at xhi.  status: MPCQP_STATUS_NOT_CONVEX when
  * no inertia correction up to 1e12 makes the Newton system definite (at the
- * first non-positive pivot with flags & MPCQP_STRICT).  skip (optional, one
+ * sixth inertia correction with flags & MPCQP_STRICT).  skip (optional, one
  * int32 per instance): instances with (skip[b] & skip_mask) != 0 are not
  * solved and their outputs and status are left as they are (an SQP passes
  * its per-instance flags to freeze the converged instances).

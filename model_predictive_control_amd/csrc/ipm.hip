@@ -37,28 +37,28 @@ __global__ __launch_bounds__(64) void ipm_kernel(ipm::Args<T> a) {
 // active lanes hit consecutive banks.  Every workspace access is then an LDS
 // round trip instead of an HBM one; it is the latency-bound small/medium-batch
 // variant (the per-stage sweeps are serial in each lane either way).
-template <typename T, int NX, int NU>
-__global__ __launch_bounds__(64) void ipm_lds_kernel(ipm::Args<T> a, int G) {
+template <typename T, int NX, int NU, int G>
+__global__ __launch_bounds__(64) void ipm_lds_kernel(ipm::Args<T> a) {
   extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
   const int lane = threadIdx.x;
   const int b = blockIdx.x * G + lane;
   if (lane >= G || b >= a.batch) return;
-  ipm::solve_lane<T, NX, NU>(a, b, ipm_lds + lane, G);
+  ipm::solve_lane<T, NX, NU, G>(a, b, ipm_lds + lane);
 }
 
 static int64_t ipm_ldb(int batch) { return ((int64_t)batch + 63) / 64 * 64; }
 
-// LDS variant: bytes of one instance's workspace, and instances per
-// workgroup (0 = does not fit).  MPCQP_IPM_LDS=0/1 forces the choice.
+// LDS variant: instances per workgroup (1, 2 or 4; 0 = the global-workspace
+// kernel), within the 160 KB of one CU.  MPCQP_IPM_LDS=0/1 forces the choice.
 static int ipm_lds_group(int batch, int F, int N) {
   const size_t per = (size_t)N * F * sizeof(double);
   const char* env = getenv("MPCQP_IPM_LDS");
   if (env && atoi(env) == 0) return 0;
-  const size_t budget = 64 * 1024;
-  if (per > 160 * 1024) return 0;
-  int G = (int)std::max<size_t>(1, std::min<size_t>(64, budget / per));
+  const size_t budget = 160 * 1024;
+  if (per > budget) return 0;
+  const int G = per * 4 <= budget ? 4 : (per * 2 <= budget ? 2 : 1);
   // large batches: the global-workspace kernel keeps 64 lanes busy per wave
-  const bool small = (int64_t)batch <= (int64_t)256 * 3 * G;
+  const bool small = (int64_t)batch <= (int64_t)256 * 4 * G;
   if (!small && !(env && atoi(env) == 1)) return 0;
   return G;
 }
@@ -88,15 +88,19 @@ static int ipm_launch_t(ipm::Args<T>& a, hipStream_t st) {
   const dim3 blk(64);
   if (G > 0) {
     const size_t bytes = (size_t)G * a.N * F * sizeof(double);
-    if (bytes > 64 * 1024) {
-      hipError_t e = hipFuncSetAttribute((const void*)ipm_lds_kernel<T, NX, NU>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-      if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(ipm_lds)");
-    }
-    hipLaunchKernelGGL((ipm_lds_kernel<T, NX, NU>), dim3((unsigned)((a.batch + G - 1) / G)), blk,
-                       bytes, st, a, G);
-    MPCQP_CHECK_LAUNCH("ipm_lds_kernel");
-    return MPCQP_OK;
+    auto launch = [&](auto kern) -> int {
+      if (bytes > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(ipm_lds)");
+      }
+      hipLaunchKernelGGL(kern, dim3((unsigned)((a.batch + G - 1) / G)), blk, bytes, st, a);
+      MPCQP_CHECK_LAUNCH("ipm_lds_kernel");
+      return MPCQP_OK;
+    };
+    if (G == 4) return launch(ipm_lds_kernel<T, NX, NU, 4>);
+    if (G == 2) return launch(ipm_lds_kernel<T, NX, NU, 2>);
+    return launch(ipm_lds_kernel<T, NX, NU, 1>);
   }
   hipLaunchKernelGGL((ipm_kernel<T, NX, NU>), dim3((unsigned)((a.batch + 63) / 64)), blk, 0, st,
                      a);
@@ -127,7 +131,7 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
     using T = decltype(tp);
     a.batch = batch; a.nx = nx; a.nu = nu; a.N = N; a.tv = (flags & MPCQP_TV) ? 1 : 0;
     a.max_iter = max_iter > 0 ? max_iter : 100;
-    a.strict = (flags & MPCQP_STRICT) ? 1 : 0;
+    a.strict = (flags & MPCQP_STRICT) ? 6 : 0;  // inertia corrections before NOT_CONVEX
     a.tol = tol > 0 ? tol : 1e-10;
     a.tol_mu = 1e-2 * a.tol;
     a.tol_polish = 1e-6;
@@ -141,7 +145,7 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
     a.H2 = (const T*)H2; a.sH2 = sH2; a.q2 = (const T*)q2; a.sq2 = sq2;
     a.z = (T*)z; a.y = (T*)y; a.X = (T*)X; a.lam_u = (T*)lam_u; a.pi = (T*)pi; a.status = status;
     a.skip = skip; a.skip_mask = skip_mask;
-    a.ws = (double*)ws; a.ldb = ipm_ldb(batch);
+    a.ws = (double*)ws;
   };
   if (dtype == MPCQP_F64) {
     ipm::Args<double> a;

@@ -72,15 +72,22 @@ struct Layout {
   static constexpr int KV = E + NX;     // k_k: feed-forward
   static constexpr int PV = KV + NU;    // p_{k+1}
   static constexpr int GA = PV + NX;    // gradient without bound duals
-  // the stage data, converted to fp64
+  // the stage data, converted to fp64 and padded once at the start: the
+  // sweeps read nothing else (no runtime nx/nu tests, no per-lane pointers)
   static constexpr int DA = GA + NB, DB = DA + NX * NX, DC = DB + NX * NU;
-  static constexpr int F = DC + NX;
+  static constexpr int WXX = DC + NX;     // Q (Qf at k = N-1) + H2xx_{k+1}: cost of x_{k+1}, packed
+  static constexpr int WUU = WXX + SX;    // R + H2uu_k, packed
+  static constexpr int WXU = WUU + SU;    // H2xu_k (NX x NU): coupling of x_k and u_k
+  static constexpr int QX = WXU + NX * NU;  // q2x_{k+1}
+  static constexpr int QU = QX + NX;      // q2u_k
+  static constexpr int LO = QU + NU, HI = LO + NB;  // bounds of u_k, x_{k+1} (+-inf: none)
+  static constexpr int F = HI + NB;
 };
 
 template <typename T>
 struct Args {
   int batch, nx, nu, N, tv, max_iter;
-  int strict;                    // 1: a non-positive pivot ends the solve (NOT_CONVEX)
+  int strict;                    // > 0: at most this many inertia corrections, then NOT_CONVEX
   double tol, tol_mu;            // convergence of the interior-point iteration
   double tol_polish, mu_polish;  // first polish attempt: residuals and mu below these
   const T* A; int64_t sA;
@@ -109,7 +116,6 @@ struct Args {
   // (outputs and status keep their values; e.g. the SQP's converged ones)
   const int32_t* skip; int32_t skip_mask;
   double* ws;
-  int64_t ldb;               // instance stride of one field (>= batch)
 };
 
 constexpr double kInf = __builtin_huge_val();
@@ -119,12 +125,13 @@ MPCQP_IL constexpr int pk(int i, int j) {
   return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i;
 }
 
-// Workspace accessor: field f of stage k of this lane's instance.
-template <int F>
+// Workspace accessor: field f of stage k of this lane's instance, LD
+// instances interleaved (a compile-time stride, so every field offset is an
+// immediate of the load instead of a hoisted per-field register).
+template <int F, int LD>
 struct Ws {
   double* W;
-  int64_t ld;
-  MPCQP_IL double& operator()(int k, int f) const { return W[((int64_t)k * F + f) * ld]; }
+  MPCQP_IL double& operator()(int k, int f) const { return W[(k * F + f) * LD]; }
 };
 
 // Stage bounds of the NB components (u_k then x_{k+1}); +-inf where absent.
@@ -140,6 +147,16 @@ MPCQP_IL void load_bounds(const Args<T>& a, int b, int k, double* lo, double* hi
     const int64_t o = (int64_t)b * a.sXb + (int64_t)k * a.nx + i;
     lo[NU + i] = (on && a.xlo) ? (double)a.xlo[o] : -kInf;
     hi[NU + i] = (on && a.xhi) ? (double)a.xhi[o] : kInf;
+  }
+}
+
+// Bounds of stage k from the workspace.
+template <int NX, int NU, class W>
+MPCQP_IL void ws_bounds(const W& at, int k, double* lo, double* hi) {
+  using L = Layout<NX, NU>;
+  for (int j = 0; j < L::NB; ++j) {
+    lo[j] = at(k, L::LO + j);
+    hi[j] = at(k, L::HI + j);
   }
 }
 
@@ -202,36 +219,36 @@ MPCQP_IL void load_ab(const W& at, int k, double (&Am)[NX][NX], double (&Bm)[NX]
 
 // Gradient of the cost plus the dynamics terms (no bound duals) for u_k
 // (g[0..NU)) and x_{k+1} (g[NU..NB)): v = [u_k; x_{k+1}], pi = pi_{k+1},
-// xk = x_k, gx1 = A_{k+1}'pi_{k+2} + H2xu_{k+1} u_{k+1} + q2x_{k+1} (from the
-// later stage; 0 at k = N-1).
-template <typename T, int NX, int NU>
-MPCQP_IL void stage_grad(const Args<T>& a, int b, int k, const double (&Bm)[NX][NU],
-                         const double* v, const double (&pi)[NX], const double (&xk)[NX],
-                         const double (&gx1)[NX], double* g) {
-  const bool term = (k == a.N - 1);
+// xk = x_k, gx1 = A_{k+1}'pi_{k+2} + H2xu_{k+1} u_{k+1} (from the later
+// stage; 0 at k = N-1).
+template <int NX, int NU, class W>
+MPCQP_IL void stage_grad(const W& at, int k, const double (&Bm)[NX][NU], const double* v,
+                         const double (&pi)[NX], const double (&xk)[NX], const double (&gx1)[NX],
+                         double* g) {
+  using L = Layout<NX, NU>;
   for (int j = 0; j < NU; ++j) {
-    double s = q2u(a, b, k, j);
-    for (int q = 0; q < NU; ++q) s = fma(wr(a, b, j, q) + h2uu(a, b, k, j, q), v[q], s);
-    for (int i = 0; i < NX; ++i) s = fma(h2xu(a, b, k, i, j), xk[i], s);
+    double s = at(k, L::QU + j);
+    for (int q = 0; q < NU; ++q) s = fma(at(k, L::WUU + pk(j, q)), v[q], s);
+    for (int i = 0; i < NX; ++i) s = fma(at(k, L::WXU + i * NU + j), xk[i], s);
     for (int i = 0; i < NX; ++i) s = fma(Bm[i][j], pi[i], s);
     g[j] = s;
   }
   for (int i = 0; i < NX; ++i) {
-    double s = gx1[i] - pi[i];
-    for (int q = 0; q < NX; ++q)
-      s = fma(wq(a, b, term, i, q) + h2xx(a, b, k + 1, i, q), v[NU + q], s);
+    double s = gx1[i] - pi[i] + at(k, L::QX + i);
+    for (int q = 0; q < NX; ++q) s = fma(at(k, L::WXX + pk(i, q)), v[NU + q], s);
     g[NU + i] = s;
   }
 }
 
-// gx1 for the stage before k: A_k'pi_{k+1} + H2xu_k u_k + q2x_k.
-template <typename T, int NX, int NU>
-MPCQP_IL void next_gx1(const Args<T>& a, int b, int k, const double (&Am)[NX][NX],
-                       const double (&pi)[NX], const double* u, double (&gx1)[NX]) {
+// gx1 for the stage before k: A_k'pi_{k+1} + H2xu_k u_k.
+template <int NX, int NU, class W>
+MPCQP_IL void next_gx1(const W& at, int k, const double (&Am)[NX][NX], const double (&pi)[NX],
+                       const double* u, double (&gx1)[NX]) {
+  using L = Layout<NX, NU>;
   for (int i = 0; i < NX; ++i) {
-    double s = q2x(a, b, k, i);
+    double s = 0.0;
     for (int q = 0; q < NX; ++q) s = fma(Am[q][i], pi[q], s);
-    for (int r = 0; r < NU; ++r) s = fma(h2xu(a, b, k, i, r), u[r], s);
+    for (int r = 0; r < NU; ++r) s = fma(at(k, L::WXU + i * NU + r), u[r], s);
     gx1[i] = s;
   }
 }
@@ -264,19 +281,17 @@ MPCQP_IL bool spd_inv(const double* G, double* Gi) {
 // x_k.  dreg is added to every Hessian diagonal (inertia correction of a
 // non-convex stage cost, H2).  False on a non-positive pivot of
 // G = R + Sigma_u + B'P B: the reduced Hessian is not positive definite.
-template <typename T, int NX, int NU>
-MPCQP_IL bool riccati_stage(const Args<T>& a, int b, int k, const double (&Am)[NX][NX],
+template <int NX, int NU, class W>
+MPCQP_IL bool riccati_stage(const W& at, int k, const double (&Am)[NX][NX],
                             const double (&Bm)[NX][NU], const double (&e)[NX], const double* g,
                             const double* sig, double* Ph, double (&ph)[NX], double* P,
                             double (&p)[NX], double (&K)[NU][NX], double (&kk)[NU], double* Gi,
                             double dreg) {
-  constexpr int SX = NX * (NX + 1) / 2;
-  const bool term = (k == a.N - 1);
+  using L = Layout<NX, NU>;
   // P_{k+1} = Q' + H2xx_{k+1} + Sigma_x + Ph,  p_{k+1} = g_x + ph
   for (int i = 0; i < NX; ++i) {
     for (int j = 0; j <= i; ++j)
-      P[pk(i, j)] = wq(a, b, term, i, j) + h2xx(a, b, k + 1, i, j) + Ph[pk(i, j)] +
-                    (i == j ? sig[NU + i] + dreg : 0.0);
+      P[pk(i, j)] = at(k, L::WXX + pk(i, j)) + Ph[pk(i, j)] + (i == j ? sig[NU + i] + dreg : 0.0);
     p[i] = g[NU + i] + ph[i];
   }
   // Pe = P e + p
@@ -298,7 +313,7 @@ MPCQP_IL bool riccati_stage(const Args<T>& a, int b, int k, const double (&Am)[N
       }
     for (int r = 0; r < NU; ++r) {
       for (int q = 0; q <= r; ++q) {
-        double s = wr(a, b, r, q) + h2uu(a, b, k, r, q) + (r == q ? sig[r] + dreg : 0.0);
+        double s = at(k, L::WUU + pk(r, q)) + (r == q ? sig[r] + dreg : 0.0);
         for (int i = 0; i < NX; ++i) s = fma(Bm[i][r], PB[i][q], s);
         G[pk(r, q)] = s;
       }
@@ -319,7 +334,7 @@ MPCQP_IL bool riccati_stage(const Args<T>& a, int b, int k, const double (&Am)[N
       }
     for (int r = 0; r < NU; ++r)
       for (int j = 0; j < NX; ++j) {
-        double s = h2xu(a, b, k, j, r);
+        double s = at(k, L::WXU + j * NU + r);
         for (int i = 0; i < NX; ++i) s = fma(Bm[i][r], PA[i][j], s);
         Hx[r][j] = s;
       }
@@ -355,7 +370,6 @@ MPCQP_IL bool riccati_stage(const Args<T>& a, int b, int k, const double (&Am)[N
     for (int r = 0; r < NU; ++r) s = fma(Hx[r][i], kk[r], s);
     ph[i] = s;
   }
-  (void)SX;
   return ok;
 }
 
@@ -430,7 +444,7 @@ MPCQP_IL bool polish(const Args<T>& a, int b, const W& at, const double (&x0)[NX
   const int N = a.N;
   for (int k = 0; k < N; ++k) {
     double lo[NB], hi[NB];
-    load_bounds<T, NX, NU>(a, b, k, lo, hi);
+    ws_bounds<NX, NU>(at, k, lo, hi);
     for (int j = 0; j < NB; ++j) {
       const double vj = j < NU ? at(k, L::U + j) : at(k, L::X + j - NU);
       const double l = at(k, L::LL + j), u = at(k, L::LU + j);
@@ -466,7 +480,7 @@ MPCQP_IL bool polish(const Args<T>& a, int b, const W& at, const double (&x0)[NX
         for (int j = 0; j < NU; ++j) v[j] = at(k, L::DU + j);
         for (int i = 0; i < NX; ++i) { v[NU + i] = at(k, L::DX + i); pi[i] = at(k, L::DPI + i); }
         for (int i = 0; i < NX; ++i) xk[i] = k == 0 ? x0[i] : at(k - 1, L::DX + i);
-        load_bounds<T, NX, NU>(a, b, k, lo, hi);
+        ws_bounds<NX, NU>(at, k, lo, hi);
         double Am[NX][NX], Bm[NX][NU], e[NX];
         load_ab<NX, NU>(at, k, Am, Bm);
         for (int i = 0; i < NX; ++i) {
@@ -476,7 +490,7 @@ MPCQP_IL bool polish(const Args<T>& a, int b, const W& at, const double (&x0)[NX
           e[i] = s;
         }
         double g[NB], sig[NB];
-        stage_grad<T, NX, NU>(a, b, k, Bm, v, pi, xk, gx1, g);
+        stage_grad<NX, NU>(at, k, Bm, v, pi, xk, gx1, g);
         for (int j = 0; j < NB; ++j) {
           const double act = at(k, L::GA + j);
           const double y = j < NU ? at(k, L::DUA + j) : at(k, L::DXA + j - NU);
@@ -484,11 +498,10 @@ MPCQP_IL bool polish(const Args<T>& a, int b, const W& at, const double (&x0)[NX
           if (act != 0.0) g[j] += y + rho * (v[j] - (act > 0.0 ? hi[j] : lo[j]));
         }
         double P[L::SX], p[NX], K[NU][NX], kk[NU], Gi[L::SU];
-        good = riccati_stage<T, NX, NU>(a, b, k, Am, Bm, e, g, sig, Ph, ph, P, p, K, kk, Gi,
-                                        0.0) &&
+        good = riccati_stage<NX, NU>(at, k, Am, Bm, e, g, sig, Ph, ph, P, p, K, kk, Gi, 0.0) &&
                good;
         store_factor<NX, NU>(at, k, P, p, K, kk, Gi, e);
-        next_gx1<T, NX, NU>(a, b, k, Am, pi, v, gx1);
+        next_gx1<NX, NU>(at, k, Am, pi, v, gx1);
       }
       // forward: full Newton step, then the multiplier update
       const bool last = step == kSteps - 1;
@@ -499,7 +512,7 @@ MPCQP_IL bool polish(const Args<T>& a, int b, const W& at, const double (&x0)[NX
           at(k, L::DPI + i) += s;
         }
         double lo[NB], hi[NB];
-        load_bounds<T, NX, NU>(a, b, k, lo, hi);
+        ws_bounds<NX, NU>(at, k, lo, hi);
         for (int j = 0; j < NB; ++j) {
           double& vr = j < NU ? at(k, L::DU + j) : at(k, L::DX + j - NU);
           const double vj = vr + (j < NU ? du[j] : dxn[j - NU]);
@@ -564,14 +577,15 @@ MPCQP_IL void emit(const Args<T>& a, int b, const W& at, bool polished, int code
   a.status[b] = code | ((it & 0xFFFF) << 8) | (polished ? (1 << 24) : 0);
 }
 
-// One instance; its workspace rows start at W (field stride ld doubles): the
-// global workspace (W = ws + b, ld = ldb) or a slice of LDS.
-template <typename T, int NX, int NU>
-MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
+// One instance; its workspace rows start at W, LD instances interleaved: a
+// block of the global workspace (LD = 64, one block per wave) or a slice of
+// LDS.
+template <typename T, int NX, int NU, int LD>
+MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W) {
   using L = Layout<NX, NU>;
   constexpr int NB = L::NB;
   const int N = a.N, nx = a.nx, nu = a.nu;
-  const Ws<L::F> at{W, ld};
+  const Ws<L::F, LD> at{W};
   if (a.skip && (a.skip[b] & a.skip_mask)) return;
 
   double x0[NX];
@@ -590,6 +604,23 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
       const T* ck = a.c ? a.c + (int64_t)b * a.sC + (int64_t)k * nx : nullptr;
       double lo[NB], hi[NB], u[NU], xn[NX];
       load_bounds<T, NX, NU>(a, b, k, lo, hi);
+      for (int j = 0; j < NB; ++j) {
+        at(k, L::LO + j) = lo[j];
+        at(k, L::HI + j) = hi[j];
+      }
+      // stage cost: x_{k+1} (Q or Qf, H2xx_{k+1}, q2x_{k+1}); u_k (R, H2uu_k,
+      // q2u_k); the x_k-u_k coupling H2xu_k
+      const bool term = (k == N - 1);
+      for (int i = 0; i < NX; ++i) {
+        for (int j = 0; j <= i; ++j)
+          at(k, L::WXX + pk(i, j)) = wq(a, b, term, i, j) + h2xx(a, b, k + 1, i, j);
+        for (int r = 0; r < NU; ++r) at(k, L::WXU + i * NU + r) = h2xu(a, b, k, i, r);
+        at(k, L::QX + i) = q2x(a, b, k + 1, i);
+      }
+      for (int r = 0; r < NU; ++r) {
+        for (int q = 0; q <= r; ++q) at(k, L::WUU + pk(r, q)) = wr(a, b, r, q) + h2uu(a, b, k, r, q);
+        at(k, L::QU + r) = q2u(a, b, k, r);
+      }
       for (int j = 0; j < NU; ++j) {
         const double u0 =
             (a.U0 && j < nu) ? (double)a.U0[(int64_t)b * a.sU0 + (int64_t)k * nu + j] : 0.0;
@@ -628,12 +659,17 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
   // every exit writes the outputs and returns from inside the loop
   double alpha = 0.0, sigmu = 0.0;  // step and sigma*mu of the last corrector
   double mu_pol = a.mu_polish;      // next polish attempt below this mu
-  // inertia correction (only a non-convex H2 needs it; not in strict mode):
-  // on a non-positive pivot pass 1 runs again with a growing dreg; each
-  // iteration starts a third below the last one that worked (0 once it falls
-  // below 1e-12).  It changes the Newton direction, not the residuals, so
-  // the iterate still converges to a KKT point of the QP.
+  // inertia correction (only a non-convex H2 needs it): on a non-positive
+  // pivot pass 1 runs again with a growing dreg; each iteration starts a third
+  // below the last one that worked (0 once it falls below 1e-12).  It changes
+  // the Newton direction, not the residuals, so the iterate still converges
+  // to a KKT point of the QP.  Strict mode (an SQP's QP, whose caller can
+  // damp the Hessian instead) gives up after a.strict corrections: a QP that
+  // is non-convex only away from its active face needs a few while the
+  // barrier terms of the active bounds grow; one that keeps needing them is
+  // handed back to the caller.
   double dreg = 0.0, dlast = 0.0;
+  int ncorr = 0;
   const int max_iter = a.max_iter;
   for (int it = 0;; ++it) {
     // ======================================== pass 1: backward factorisation
@@ -652,7 +688,7 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
         xk[i] = k == 0 ? x0[i] : at(k - 1, L::X + i);
         if (alpha > 0.0 && k > 0) xk[i] += alpha * at(k - 1, L::DX + i);
       }
-      load_bounds<T, NX, NU>(a, b, k, lo, hi);
+      ws_bounds<NX, NU>(at, k, lo, hi);
       if (alpha > 0.0) {  // apply the corrector step of the previous iteration
         for (int j = 0; j < NB; ++j) {
           const double dv = j < NU ? at(k, L::DU + j) : at(k, L::DX + j - NU);
@@ -688,7 +724,7 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
       }
       // gradients without the bound duals
       double g[NB];
-      stage_grad<T, NX, NU>(a, b, k, Bm, v, pi, xk, gx1, g);
+      stage_grad<NX, NU>(at, k, Bm, v, pi, xk, gx1, g);
       // stationarity residual, complementarity, Sigma
       double sig[NB];
       for (int j = 0; j < NB; ++j) {
@@ -711,11 +747,10 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
       }
       for (int j = 0; j < NB; ++j) at(k, L::GA + j) = g[j];
       double P[L::SX], p[NX], K[NU][NX], kk[NU], Gi[L::SU];
-      const bool ok =
-          riccati_stage<T, NX, NU>(a, b, k, Am, Bm, e, g, sig, Ph, ph, P, p, K, kk, Gi, dreg);
+      const bool ok = riccati_stage<NX, NU>(at, k, Am, Bm, e, g, sig, Ph, ph, P, p, K, kk, Gi, dreg);
       pd = pd && ok;
       store_factor<NX, NU>(at, k, P, p, K, kk, Gi, e);
-      next_gx1<T, NX, NU>(a, b, k, Am, pi, v, gx1);
+      next_gx1<NX, NU>(at, k, Am, pi, v, gx1);
     }
     const double mu = mcount ? musum / mcount : 0.0;
 #ifdef MPCQP_IPM_TRACE  // host build of tools/ipm_host.cpp only
@@ -728,7 +763,7 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
     }
     if (!pd) {
       dreg = dreg > 0.0 ? 8.0 * dreg : (dlast > 0.0 ? dlast : 1e-4);
-      if (a.strict || dreg > 1e12 || it >= max_iter) {
+      if ((a.strict > 0 && ++ncorr > a.strict) || dreg > 1e12 || it >= max_iter) {
         emit<T, NX, NU>(a, b, at, false, MPCQP_STATUS_NOT_CONVEX, it);
         return;
       }
@@ -767,7 +802,7 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
       for (int r = 0; r < NU; ++r) at(k, L::DUA + r) = du[r];
       for (int i = 0; i < NX; ++i) at(k, L::DXA + i) = dxn[i];
       double lo[NB], hi[NB];
-      load_bounds<T, NX, NU>(a, b, k, lo, hi);
+      ws_bounds<NX, NU>(at, k, lo, hi);
       for (int j = 0; j < NB; ++j) {
         const double vj = j < NU ? at(k, L::U + j) : at(k, L::X + j - NU);
         const double dv = j < NU ? du[j] : dxn[j - NU];
@@ -805,7 +840,7 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
       for (int i = 0; i < NX; ++i) phc[i] = 0.0;
       for (int k = N - 1; k >= 0; --k) {
         double lo[NB], hi[NB], g[NB];
-        load_bounds<T, NX, NU>(a, b, k, lo, hi);
+        ws_bounds<NX, NU>(at, k, lo, hi);
         for (int j = 0; j < NB; ++j) {
           const double vj = j < NU ? at(k, L::U + j) : at(k, L::X + j - NU);
           const double dva = j < NU ? at(k, L::DUA + j) : at(k, L::DXA + j - NU);
@@ -861,7 +896,7 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
       for (int r = 0; r < NU; ++r) at(k, L::DU + r) = du[r];
       for (int i = 0; i < NX; ++i) at(k, L::DX + i) = dxn[i];
       double lo[NB], hi[NB];
-      load_bounds<T, NX, NU>(a, b, k, lo, hi);
+      ws_bounds<NX, NU>(at, k, lo, hi);
       for (int j = 0; j < NB; ++j) {
         const double vj = j < NU ? at(k, L::U + j) : at(k, L::X + j - NU);
         const double dv = j < NU ? du[j] : dxn[j - NU];
@@ -889,9 +924,11 @@ MPCQP_IL void solve_lane(const Args<T>& a, int b, double* W, int64_t ld) {
   }
 }
 
+// Global workspace: blocks of 64 instances, [block][stage][field][64].
 template <typename T, int NX, int NU>
 MPCQP_IL void solve_lane(const Args<T>& a, int b) {
-  solve_lane<T, NX, NU>(a, b, a.ws + b, a.ldb);
+  constexpr int F = Layout<NX, NU>::F;
+  solve_lane<T, NX, NU, 64>(a, b, a.ws + (int64_t)(b / 64) * a.N * F * 64 + (b % 64));
 }
 
 }  // namespace ipm

@@ -16,14 +16,17 @@
 // damped Levenberg-Marquardt style by a proximal term mu/2 |w - w_k|^2 per
 // stage: a full step divides mu by 4 (down to 0), a step that needs
 // backtracking or a QP that fails multiplies it by 4 (at least 1e-3).
-#include <cstdlib>
-
 #include "bike.hpp"
 
 namespace mpcqp {
 
 constexpr int kSqpDone = 1, kSqpExact = 2;
-constexpr double kSqpSwitch = 1e-2;  // KKT residual below which the exact Hessian is used
+// KKT residual below which the exact Hessian is used (Gauss-Newton before:
+// far from a solution the costates that weight the curvature are poor)
+constexpr double kSqpSwitch = 1.0;
+// Levenberg-Marquardt damping of the exact-Hessian QPs: x4 after a failed QP
+// or a shortened step (at least kMuFloor), x1/4 after a full step
+constexpr double kMuFloor = 1e-4, kMuDec = 0.25;
 
 __global__ void bike_hess_kernel(int batch, int N, Bike p, const double* X, const double* U,
                                  const double* pi, const int32_t* flags, const double* mu,
@@ -72,7 +75,6 @@ struct SqpArgs {
   double *rho, *kkt, *mu;
   int32_t* flags;
   double tol;
-  double sw, mu_floor, mu_dec;  // Hessian switch, damping after a failed step, decrease factor
 };
 
 // 1/2 J(U) and the l1 violation of the state box along a rollout
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
     // converged): no step; an exact-Hessian iteration falls back to
     // Gauss-Newton (positive definite) until the residual drops 10x
     const int iters = ((fl >> 8) & 0xFFFF) + 1;
-    if (fl & kSqpExact) a.mu[b] = fmax(4.0 * a.mu[b], a.mu_floor);
+    if (fl & kSqpExact) a.mu[b] = fmax(4.0 * a.mu[b], kMuFloor);
     a.flags[b] = (iters << 8) | (fl & kSqpExact);
     return;
   }
@@ -279,11 +281,11 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
   // ---------------------------------------------------- Hessian mode, flags
   if (fl & kSqpExact) {
     double mu = a.mu[b];
-    mu = alpha == 1.0 ? (mu > 4e-12 ? a.mu_dec * mu : 0.0) : fmax(4.0 * mu, a.mu_floor);
+    mu = alpha == 1.0 ? (mu > 4e-12 ? kMuDec * mu : 0.0) : fmax(4.0 * mu, kMuFloor);
     a.mu[b] = mu;
   }
   const int iters = ((fl >> 8) & 0xFFFF) + 1;
-  const bool exact = (fl & kSqpExact) || r < a.sw;  // sticky
+  const bool exact = (fl & kSqpExact) || r < kSqpSwitch;  // sticky
   fl = (iters << 8) | (r <= a.tol ? kSqpDone : 0) | (exact ? kSqpExact : 0);
   a.flags[b] = fl;
   a.rho[b] = rho;
@@ -477,10 +479,6 @@ extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,
   a.qp_status = qp_status;
   a.y = (double*)y; a.pi = (double*)pi; a.X = (double*)X;
   a.rho = rho; a.kkt = kkt; a.mu = mu; a.flags = flags; a.tol = tol > 0 ? tol : 1e-9;
-  auto envd = [](const char* k, double d) { const char* v = getenv(k); return v ? atof(v) : d; };
-  a.sw = envd("MPCQP_SQP_SWITCH", kSqpSwitch);
-  a.mu_floor = envd("MPCQP_SQP_MUFLOOR", 1e-3);
-  a.mu_dec = envd("MPCQP_SQP_MUDEC", 0.25);
   hipLaunchKernelGGL(sqp_step_kernel, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0,
                      (hipStream_t)stream, a);
   MPCQP_CHECK_LAUNCH("sqp_step_kernel");

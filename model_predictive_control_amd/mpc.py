@@ -258,7 +258,7 @@ class SqpSolver:
     (flag SQP_DONE): the interior point skips them and the others keep
     iterating."""
 
-    MU0 = float(__import__("os").environ.get("MPCQP_SQP_MU0", 0.1))  # initial Levenberg-Marquardt damping of the exact-Hessian QPs
+    MU0 = 1e-3  # initial Levenberg-Marquardt damping of the exact-Hessian QPs
     # interior-point budget of one QP: a convex one takes 6-10 iterations; one
     # that is not (strict: first non-positive pivot) or stalls is abandoned
     # and the step kernel raises the damping instead

@@ -31,10 +31,10 @@ extern "C" int ipm_host_solve(int batch, int nx, int nu, int N, int tv, const do
   const bool small = nx <= 2 && nu <= 1;
   const int F = small ? ipm::Layout<2, 1>::F : ipm::Layout<4, 2>::F;
   std::vector<double> ws((size_t)N * F * batch);
-  a.ws = ws.data(); a.ldb = batch;
+  a.ws = ws.data();
   for (int b = 0; b < batch; ++b) {
-    if (small) ipm::solve_lane<double, 2, 1>(a, b);
-    else ipm::solve_lane<double, 4, 2>(a, b);
+    if (small) ipm::solve_lane<double, 2, 1, 1>(a, b, ws.data() + (size_t)b * N * F);
+    else ipm::solve_lane<double, 4, 2, 1>(a, b, ws.data() + (size_t)b * N * F);
   }
   return 0;
 }
