@@ -654,6 +654,8 @@ class ConfigNLP:
     dname = "f64"
     default_batch = 4096
     default_slots = 2
+    default_sqp_iters = 30
+    default_steps = (5, 1)  # (steps, warmup) when not given: one step is ~30 SQP iterations
 
     def __init__(self, args, dev, rank):
         from model_predictive_control_amd.mpc import MPCController, SqpSolver
@@ -770,8 +772,10 @@ class ConfigLoop:
 
     dtype = torch.float64
     dname = "f64"
-    default_batch = 4096
+    default_batch = 1024
     default_slots = 2
+    default_sqp_iters = 8   # per sample, warm-started from the shifted solution
+    default_steps = (3, 1)  # one step is a whole episode
 
     def __init__(self, args, dev, rank):
         from model_predictive_control_amd.closed_loop import ClosedLoop
@@ -843,13 +847,13 @@ CONFIGS = {"2": Config2, "3": Config3, "4": Config4, "5": Config5, "nlp": Config
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=0, help="timed steps (0 = config default: 200)")
+    ap.add_argument("--warmup", type=int, default=-1, help="untimed steps (-1 = config default: 20)")
     ap.add_argument("--config", default="2", choices=sorted(CONFIGS),
                     help="BASELINE configs 2-5 (2 = the headline), nlp (converged "
                          "MPCController.solve), loop (on-device receding-horizon loop)")
-    ap.add_argument("--sqp-iters", type=int, default=40,
-                    help="nlp: SQP iterations per solve; loop: per sample")
+    ap.add_argument("--sqp-iters", type=int, default=0,
+                    help="nlp: SQP iterations per solve (default 30); loop: per sample (8)")
     ap.add_argument("--loop-steps", type=int, default=20, help="loop: samples per episode")
     ap.add_argument("--gather", action="store_true",
                     help="N>1: time the final all-gather of z (RCCL) after the timed loop")
@@ -871,6 +875,10 @@ def main():
     C = CONFIGS[args.config]
     args.batch = args.batch or C.default_batch
     args.slots = args.slots or C.default_slots
+    args.sqp_iters = args.sqp_iters or getattr(C, "default_sqp_iters", 0)
+    dsteps, dwarm = getattr(C, "default_steps", (200, 20))
+    args.steps = args.steps or dsteps
+    args.warmup = dwarm if args.warmup < 0 else args.warmup
 
     rank, world, local = mdist.env_rank_world()
     # rehearsal knobs (one-GPU box): MPCQP_BENCH_DEVICE pins every rank to one

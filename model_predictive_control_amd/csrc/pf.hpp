@@ -10,6 +10,11 @@ constexpr int kKChunk = 1536;  // floats of K rows per refinement chunk (6 KB of
 constexpr int kStatusRetry = 0x7f;  // internal: hand the instance to qp_wg_kernel
 // refinement scratch (doubles): K-pass = red (8*64) + rsum (3*64) + kbuf
 constexpr int kPool = 8 * kWave + 3 * kWave + kKChunk / 2;
+// doubles added to the pool for the M0 row cache of qp_pf_kernel (NXP <= 4):
+// 20 rows at n + m = 180, within the LDS of 8 waves per CU (2 per SIMD, the
+// occupancy the kernel is latency-bound at: 47 rows at 4 waves per CU cut
+// the traffic by 3x and doubled the time)
+constexpr int kPoolCacheExtra = 400;
 // DYN layout inside the pool (doubles): xd (3*64: u, then mu of the state
 // rows; g overwrites u) | lam (2 x 16) | X ((N+1) nx) | Q, Qf, R (floats) |
 // stage chunk (floats): [A_s | B_s | c_s] for a run of stages

@@ -338,7 +338,12 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
   __shared__ float s_lo[NR * kWave], s_hi[NR * kWave], s_sl[NR * kWave], s_su[NR * kWave],
       s_scl[NR * kWave];
   __shared__ __attribute__((aligned(16))) float sx[kSlots];  // slot-vector broadcast
-  __shared__ double pool[kPool];   // refinement scratch (K-pass or DYN layout)
+  // refinement scratch (K-pass or DYN layout); during the active set, the
+  // M0 row cache (below), extended past the refinement's needs where the row
+  // cache is on: 34 KB of LDS per wave, 4 waves per CU
+  constexpr bool kCache = NXP <= 4;
+  constexpr int kPoolX = kCache ? kPool + kPoolCacheExtra : kPool;
+  __shared__ double pool[kPoolX];
   double* red = pool;
   double* rsum = pool + 8 * kWave;
   float* kbuf = reinterpret_cast<float*>(pool + 11 * kWave);  // rows of K staged per chunk
@@ -401,9 +406,8 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
   // the refinement's residual reuses the pool and clears it.
   // (measured: pays at config 3; with the wide-state DYN residual (NXP >= 8,
   // config 5) the extra registers spill and it costs more than it saves)
-  constexpr bool kCache = NXP <= 4;
   float* cache = reinterpret_cast<float*>(pool);
-  const int ncache = !kCache ? 0 : ((2 * kPool) / nt < 16 ? (2 * kPool) / nt : 16);
+  const int ncache = !kCache ? 0 : ((2 * kPoolX) / nt < kSlots ? (2 * kPoolX) / nt : kSlots);
   uint64_t cmask = 0;
 
   int code = MPCQP_STATUS_OPTIMAL, iters = 0;
@@ -475,19 +479,32 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
     // out += sign * M0[:, P] q  (rows a_j of the symmetric M0); fixed_z_f:
     // coefficient -f_a on the fixed z instead (rows contribute nothing)
     // cached slots: the row from LDS, no memory round trip
+    // (kCB slots per LDS round trip: all their reads issued before the FMAs)
     auto ccols = [&](float q, float (&out)[NR], float sign, bool fixed_z_f, uint64_t mm) {
       if constexpr (!kCache) return;
+      constexpr int kCB = 4;
       while (mm) {
-        const int j = __builtin_ctzll(mm);
-        mm &= mm - 1;
-        const int aj = readlane(aidx, j);
-        const float c = fixed_z_f ? (aj < n ? -fb[aj] : 0.f) : sign * readlane(q, j);
+        float c[kCB], v[kCB][NR];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-          const int i = l + kWave * r;
-          const float v = cache[j * nt + (i < nt ? i : 0)];
-          out[r] = fmaf(c, i < nt ? v : 0.f, out[r]);
+        for (int t = 0; t < kCB; ++t) {
+          int j = 0;
+          c[t] = 0.f;
+          if (mm) {
+            j = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            const int aj = readlane(aidx, j);
+            c[t] = fixed_z_f ? (aj < n ? -fb[aj] : 0.f) : sign * readlane(q, j);
+          }
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            v[t][r] = cache[j * nt + (i < nt ? i : 0)];
+          }
         }
+#pragma unroll
+        for (int t = 0; t < kCB; ++t)
+#pragma unroll
+          for (int r = 0; r < NR; ++r) out[r] = fmaf(c[t], l + kWave * r < nt ? v[t][r] : 0.f, out[r]);
       }
     };
     auto pcols = [&](float q, float (&out)[NR], float sign, bool fixed_z_f, uint64_t mm) {
