@@ -695,37 +695,50 @@ class ConfigNLP:
         return self.ST
 
     def kernels(self, traffic):
-        """One SQP iteration's launches timed separately on the converged state
-        of slot 0 (the last step left it there)."""
+        """One SQP iteration's launches timed separately, on the state of slot
+        0 after 3 iterations from U = 0 (every instance still iterating): the
+        interior point as SqpSolver runs it (strict, QP_MAX_ITER), no skip."""
+        from model_predictive_control_amd.mpc import SqpSolver
+
         R = self.args.reps
         sqp, ctl, N, bsz = self.sqp, self.ctl, self.N, self.args.batch
         x0 = self.X0_t[0]
+        kkt_final, done_final = float(self.KKT[0].max()), self.ST[0].clone()
+        sqp.reset()
+        for _ in range(3):
+            sqp.iterate(x0)
         A, B, c, Xr = batched.bicycle_rti(x0, sqp.U, ctl.params, ctl.ts, states=True)
         t_r = time_kernel(lambda: batched.bicycle_rti(x0, sqp.U, ctl.params, ctl.ts, states=True), R,
                           self.dev)
         t_h = time_kernel(lambda: batched.bicycle_hessian(Xr, sqp.U, sqp.pi, ctl.params, ctl.ts,
-                                                          flags=None, mu=sqp.mu), R, self.dev)
-        H2, q2 = batched.bicycle_hessian(Xr, sqp.U, sqp.pi, ctl.params, ctl.ts, flags=None, mu=sqp.mu)
+                                                          flags=sqp.flags, mu=sqp.mu), R, self.dev)
+        H2, q2 = batched.bicycle_hessian(Xr, sqp.U, sqp.pi, ctl.params, ctl.ts, flags=sqp.flags,
+                                         mu=sqp.mu)
         box = ctl._box()
+        qp = {}
 
         def ipm():
-            sqp.qp = batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, lb=ctl.lbz, ub=ctl.ubz, c=c,
-                                     tv=True, H2=H2, q2=q2, out=sqp.qp, **box)
+            batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, lb=ctl.lbz, ub=ctl.ubz, c=c, tv=True,
+                            H2=H2, q2=q2, strict=True, max_iter=SqpSolver.QP_MAX_ITER, out=qp, **box)
         t_i = time_kernel(ipm, R, self.dev)
         torch.cuda.synchronize()
-        it_ipm = float(((sqp.qp["status"] >> 8) & 0xFFFF).double().mean())
-        # algorithmic bytes of the interior point: A_k, B_k, c_k, H2_k, q2_k, x0 in;
-        # z, X, y, pi, lam_u, status out (its workspace traffic is overhead)
-        ib = (N * (16 + 8 + 4 + 36 + 6) + 4 + N * (2 + 4 + 4 + 4 + 2)) * 8 * bsz + 4 * bsz
-        r_i = roof("ipm_kernel<double,4,2>", "hbm", ib, t_i, HBM_PEAK_GBS, "GB/s",
-                   traffic.get("ipm"), {"bytes_per_launch": ib, "ipm_iters_mean": round(it_ipm, 2),
-                                        "note": "lane per instance; latency-bound sweeps over the "
-                                                "stages, workspace traffic not counted"})
+        its = ((qp["status"] >> 8) & 0xFFFF).double()
+        # algorithmic fp64 flops of one interior-point iteration per stage
+        # (nx = 4, nu = 2): Riccati factorisation ~270 FMA, residuals and
+        # gradients ~90, predictor / corrector sweeps ~180 -> ~540 FMA
+        flops = 2 * 540 * N * float(its.sum())
+        r_i = roof("ipm_kernel<double,4,2> / ipm_lds_kernel", "valu-fp64", flops, t_i,
+                   FP64_PEAK_TFS, "TFLOP/s", traffic.get("ipm"),
+                   {"flops_per_launch": flops, "ipm_iters_mean": round(float(its.mean()), 2),
+                    "ipm_iters_max": int(its.max()),
+                    "note": "lane per instance, serial over the stages: latency/issue-bound "
+                            "(one wave per SIMD); flops = 1080 per stage per IPM iteration "
+                            "summed over the instances' own iteration counts, polish not counted"})
         extra = {"kernel_us": {"bicycle_rti": round(t_r * 1e3, 2),
                                "bicycle_hessian": round(t_h * 1e3, 2),
                                "mpc_ipm": round(t_i * 1e3, 2)},
-                 "kkt_max": float(self.KKT[0].max()),
-                 "converged_frac": float((batched.status_code(self.ST[0]) == 0).double().mean())}
+                 "kkt_max": kkt_final,
+                 "converged_frac": float((batched.status_code(done_final) == 0).double().mean())}
         return r_i, {}, extra
 
     def check(self):
