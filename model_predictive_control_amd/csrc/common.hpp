@@ -186,6 +186,17 @@ __device__ __forceinline__ T wave_max(T v) {
 }
 
 template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+  v = fmin(v, lane_step<1>(v));
+  v = fmin(v, lane_step<2>(v));
+  v = fmin(v, lane_step<4>(v));
+  v = fmin(v, lane_step<8>(v));
+  v = fmin(v, lane_step<16>(v));
+  v = fmin(v, lane_step<32>(v));
+  return v;
+}
+
+template <typename T>
 struct Lim {
   static __device__ __forceinline__ T inf() { return __builtin_huge_val(); }
 };

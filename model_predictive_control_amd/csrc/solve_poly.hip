@@ -28,6 +28,8 @@
 // pivot W_pp (its Schur complement -- zero when p depends on the active rows,
 // in which case a pure dual step drops rows first), dropping row k is a
 // reverse sweep.  Same register-resident sweep machinery as solve_box.hip.
+#include <cstdlib>
+
 #include "sym2d.hpp"
 
 namespace mpcqp {
@@ -54,20 +56,21 @@ struct DualArgs {
   T tol;
 };
 
-// st: 0 inactive, 1 at lower, 2 at upper, 3 padding row
-template <typename T, int BS>
-__global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
+// st: 0 inactive, 1 at lower, 2 at upper, 3 padding row.
+// Layout: the swept matrix W on the 8 x 8 block grid (Sym2D); every
+// row-indexed vector (s0, bounds, scales, y, s, st) one row per lane (lane i =
+// row i, mt <= 64), so the scan and the ratio test run once per row instead
+// of once per row-block replica, with full-wave DPP arg-max / arg-min.
+template <typename T, int BS, int WPS>
+__global__ __launch_bounds__(64, WPS) void dual_range_kernel(DualArgs<T> a) {
   using S2 = Sym2D<T, BS>;
   constexpr int NMAX = S2::NMAX;
+  static_assert(NMAX <= kWave, "one row per lane");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   T* buf = reinterpret_cast<T*>(smem_raw);
-  T* lis = buf + S2::BUF;
-  T* uis = lis + NMAX;
-  T* mds = uis + NMAX;
-  T* ss = mds + NMAX;
-  T* s0s = ss + NMAX;          // NMAX: unconstrained row values
-  T* xs = s0s + NMAX;          // 16: x0
-  T* Ps = xs + 16;
+  T* xs = buf + S2::BUF;       // 16: x0
+  T* part = xs + 16;           // 8 * NMAX: partial row sums of the mat-vec
+  T* Ps = part + 8 * NMAX;
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = a.mt;
@@ -78,59 +81,38 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
   stage_packed<T, NMAX*(NMAX + 1) / 2>(a.M + (int64_t)b * a.sM, Ps, P, lane);
   if (x0 && lane < nx) xs[lane] = x0[lane];
   __syncthreads();
-  // prologue: s0 = L x0 - Ut f1 (one row per lane)
-  if (lane < n) {
+  // row `lane`: unconstrained value s0 = L x0 - Ut f1, bounds, scales, M_ii
+  const bool row = lane < n;
+  T s0 = T(0), li = -Lim<T>::inf(), ui = Lim<T>::inf(), md = T(1);
+  if (row) {
     T acc = T(0);
     if (x0)
       for (int k = 0; k < nx; ++k) acc = fma(a.L[lane * nx + k], xs[k], acc);
     if (f1)
       for (int j = 0; j < nz; ++j) acc = fma(-a.Ut[(int64_t)lane * nz + j], f1[j], acc);
-    s0s[lane] = acc;
-  }
-  __syncthreads();
-
-  Sym2D<T, BS> W;
-  W.init(lane);
-  T s0[BS], li[BS], ui[BS], yi[BS], si[BS];
-  int st[BS];
-  bool nonfinite = false, badbox = false;
-#pragma unroll
-  for (int r = 0; r < BS; ++r) {
-    const int i = W.bi * BS + r;
-    const bool v = i < n;
-    s0[r] = v ? s0s[i] : T(0);
-    li[r] = -Lim<T>::inf();
-    ui[r] = Lim<T>::inf();
-    if (v) {
-      if (i < a.m1) {
-        if (a.l1) li[r] = a.l1[(int64_t)b * a.s1 + i];
-        if (a.u1) ui[r] = a.u1[(int64_t)b * a.s1 + i];
-      } else {
-        if (a.l2) li[r] = a.l2[i - a.m1];
-        if (a.u2) ui[r] = a.u2[i - a.m1];
-      }
+    s0 = acc;
+    if (lane < a.m1) {
+      if (a.l1) li = a.l1[(int64_t)b * a.s1 + lane];
+      if (a.u1) ui = a.u1[(int64_t)b * a.s1 + lane];
+    } else {
+      if (a.l2) li = a.l2[lane - a.m1];
+      if (a.u2) ui = a.u2[lane - a.m1];
     }
-    st[r] = v ? 0 : 3;
-    yi[r] = T(0);
-    si[r] = s0[r];
-    nonfinite |= v && !finite(s0[r]);
-    badbox |= v && (!(li[r] <= ui[r]) || li[r] == Lim<T>::inf() || ui[r] == -Lim<T>::inf());
+    md = Ps[lane * (lane + 1) / 2 + lane];
   }
+  int st = row ? 0 : 3;
+  T yi = T(0), si = s0;
+  bool nonfinite = row && !finite(s0);
+  const bool badbox =
+      row && (!(li <= ui) || li == Lim<T>::inf() || ui == -Lim<T>::inf());
   // relative-violation scales 1/(1+|bound|), NaN for an infinite bound (a NaN
   // violation never wins the arg-max): the per-iteration scan only multiplies
-  T sl[BS], su[BS];
-#pragma unroll
-  for (int r = 0; r < BS; ++r) {
-    sl[r] = finite(li[r]) ? T(1) / (T(1) + fabs(li[r])) : T(__builtin_nan(""));
-    su[r] = finite(ui[r]) ? T(1) / (T(1) + fabs(ui[r])) : T(__builtin_nan(""));
-  }
-  publish<T, BS>(li, lis, W.bi, W.bj);
-  publish<T, BS>(ui, uis, W.bi, W.bj);
-  __syncthreads();
+  const T sl = finite(li) ? T(1) / (T(1) + fabs(li)) : T(__builtin_nan(""));
+  const T su = finite(ui) ? T(1) / (T(1) + fabs(ui)) : T(__builtin_nan(""));
+
+  S2 W;
+  W.init(lane);
   W.load_packed(Ps, n, nonfinite);
-  // diagonal of M by row (dependency test scale)
-  for (int i = lane; i < n; i += kWave) mds[i] = Ps[i * (i + 1) / 2 + i];
-  __syncthreads();
   int code = MPCQP_STATUS_MAXITER;
   int iters = 0;
   const T tol = a.tol;
@@ -152,46 +134,27 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
     // w = (s0 - b on active rows, 0 elsewhere);  v = W w;
     // active: y = -v, s = bound;  inactive: s = s0 - v
     auto refresh = [&]() {
-      T w[BS], v[BS];
-#pragma unroll
-      for (int r = 0; r < BS; ++r) {
-        const bool act = st[r] == 1 || st[r] == 2;
-        const T bnd = (st[r] == 1) ? li[r] : ui[r];
-        w[r] = act ? s0[r] - bnd : T(0);
-      }
-      W.matvec(w, buf, v);
-#pragma unroll
-      for (int r = 0; r < BS; ++r) {
-        const bool act = st[r] == 1 || st[r] == 2;
-        const T bnd = (st[r] == 1) ? li[r] : ui[r];
-        yi[r] = act ? -v[r] : T(0);
-        si[r] = act ? bnd : s0[r] - v[r];
-      }
+      const bool act = st == 1 || st == 2;
+      const T bnd = (st == 1) ? li : ui;
+      const T v = matvec_lane_lds<T, BS>(W, act ? s0 - bnd : T(0), buf, part);
+      yi = act ? -v : T(0);
+      si = act ? bnd : s0 - v;
     };
     while (true) {
-      T viol = -Lim<T>::inf();
-      int p = 0;
-      T spv = T(0);  // the winner's row value rides along as the arg-max payload
-#pragma unroll
-      for (int r = 0; r < BS; ++r) {
-        const T vl = (li[r] - si[r]) * sl[r];
-        const T vu = (si[r] - ui[r]) * su[r];
-        const T vv = (st[r] == 0) ? fmax(vl, vu) : -Lim<T>::inf();
-        const bool take = vv > viol;
-        viol = take ? vv : viol;
-        p = take ? W.bi * BS + r : p;
-        spv = take ? si[r] : spv;
-      }
-      blocks_argmax(viol, p, spv);
-      p = uniform(p);
-      if (!(readlane(viol, 0) > tol)) {
+      const T vl = (li - si) * sl;
+      const T vu = (si - ui) * su;
+      // arg-max as a wave max (3 VALU per step) and a ballot of the lanes
+      // holding it: the smallest such lane wins, as in an (value, index) reduction
+      const T viol = (st == 0) ? fmax(vl, vu) : -Lim<T>::inf();
+      const T vmax = wave_max(viol);
+      if (!(readlane(vmax, 0) > tol)) {
         code = MPCQP_STATUS_OPTIMAL;
         break;
       }
-      // lis/uis/mds are read-only after the set-up barrier: no publish needed
-      const T sp0 = readlane(spv, 0);
-      const T lp = lis[p], up = uis[p];
-      const T mpp = mds[p];
+      const int p = uniform(__builtin_ctzll(__builtin_amdgcn_ballot_w64(viol == vmax)));
+      const T sp0 = readlane(si, p);
+      const T lp = readlane(li, p), up = readlane(ui, p);
+      const T mpp = readlane(md, p);
       const int side = (sp0 < lp) ? 1 : 2;
       const T tgt = (side == 1) ? lp : up;
       const T ysgn = (side == 1) ? T(-1) : T(1);
@@ -199,52 +162,37 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
       bool added = false;
       while (!added) {
         if (++iters > max_iter) goto done;
-        T c[BS], cc[BS];
-        const T wpp = W.column(p, buf, c, cc);  // c[r] = W_ip
+        T c[BS], cc[BS], cl;
+        const T wpp = W.template column<true>(p, buf, c, cc, cl);  // cl = W_lane,p
         const bool dep = !(wpp > dep_tol * fmax(mpp, T(1e-300)));
-        T ti = Lim<T>::inf();
-        int k = 0;
-        T dy[BS];
-#pragma unroll
-        for (int r = 0; r < BS; ++r) {
-          dy[r] = -c[r] * ysgn;
-          // an active row's multiplier moves toward 0: t = -y / dy (>= 0)
-          const bool cand = (st[r] == 2 && dy[r] < T(0)) || (st[r] == 1 && dy[r] > T(0));
-          const T t = cand ? -yi[r] * fast_rcp(dy[r]) : Lim<T>::inf();
-          const bool take = t < ti;
-          ti = take ? t : ti;
-          k = take ? W.bi * BS + r : k;
-        }
-        blocks_argmin(ti, k);
-        k = uniform(k);
-        ti = readlane(ti, 0);
+        // an active row's multiplier moves toward 0: t = -y / dy (>= 0)
+        const T dy = -cl * ysgn;
+        const bool cand = (st == 2 && dy < T(0)) || (st == 1 && dy > T(0));
+        const T tl = cand ? -yi * fast_rcp(dy) : Lim<T>::inf();
+        const T ti = readlane(wave_min(tl), 0);
+        const uint64_t kb = __builtin_amdgcn_ballot_w64(tl == ti);
+        const int k = kb ? uniform(__builtin_ctzll(kb)) : 0;
         const T t2 = dep ? Lim<T>::inf() : fabs(sp - tgt) / wpp;
         if (!(ti < Lim<T>::inf()) && !(t2 < Lim<T>::inf())) {
           code = MPCQP_STATUS_INFEASIBLE;
           goto done;
         }
         if (ti < t2) {
-#pragma unroll
-          for (int r = 0; r < BS; ++r) {
-            if (st[r] == 1 || st[r] == 2) yi[r] = fma(ti, dy[r], yi[r]);
-            if (W.bi * BS + r == k) {
-              yi[r] = T(0);
-              st[r] = 0;
-            }
+          if (st == 1 || st == 2) yi = fma(ti, dy, yi);
+          if (lane == k) {
+            yi = T(0);
+            st = 0;
           }
           if (!dep) sp = sp - wpp * ysgn * ti;
           W.sweep(k, T(-1), buf);
         } else {
           // column p is still in registers (W unchanged since it was read)
           W.sweep_col(p, T(1), wpp, c, cc);
-          const T d = wpp;
-          if (!(d > T(0))) {
+          if (!(wpp > T(0))) {
             code = MPCQP_STATUS_NOT_CONVEX;
             goto done;
           }
-#pragma unroll
-          for (int r = 0; r < BS; ++r)
-            if (W.bi * BS + r == p) st[r] = side;
+          if (lane == p) st = side;
           refresh();
           added = true;
         }
@@ -253,27 +201,21 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
   }
 done:
   const bool okc = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
-  if (!okc) {
-#pragma unroll
-    for (int r = 0; r < BS; ++r) yi[r] = __builtin_nan("");
-  }
-  if (a.y && W.bj == 0) {
-#pragma unroll
-    for (int r = 0; r < BS; ++r) {
-      const int i = W.bi * BS + r;
-      if (i < n) a.y[(int64_t)b * n + i] = yi[r];
-    }
-  }
-  // epilogue: z = Kt' x0 - Hinv f1 - Ut' y   (lanes over z, coalesced rows)
-  publish<T, BS>(yi, ss, W.bi, W.bj);
-  __syncthreads();
+  if (!okc) yi = __builtin_nan("");
+  if (a.y && row) a.y[(int64_t)b * n + lane] = yi;
+  // epilogue: z = Kt' x0 - Hinv f1 - Ut' y   (lanes over z, coalesced rows;
+  // only the rows with y != 0 -- the active ones -- contribute)
+  const uint64_t yact = __builtin_amdgcn_ballot_w64(row && yi != T(0));
   for (int j = lane; j < nz; j += kWave) {
     T acc = T(0);
     if (x0)
       for (int k = 0; k < nx; ++k) acc = fma(a.Kt[(int64_t)k * nz + j], xs[k], acc);
     if (f1)
       for (int i = 0; i < nz; ++i) acc = fma(-a.Hinv[(int64_t)i * nz + j], f1[i], acc);
-    for (int r = 0; r < n; ++r) acc = fma(-a.Ut[(int64_t)r * nz + j], ss[r], acc);
+    for (uint64_t mk = yact; mk; mk &= mk - 1) {
+      const int r = uniform(__builtin_ctzll(mk));
+      acc = fma(-a.Ut[(int64_t)r * nz + j], readlane(yi, r), acc);
+    }
     a.z[(int64_t)b * nz + j] = okc ? acc : __builtin_nan("");
   }
   if (lane == 0) a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
@@ -426,8 +368,12 @@ static PolyWs poly_ws(size_t es, int n, int mt, int nx) {
 template <typename T, int BS>
 static void launch_dual(const DualArgs<T>& a, hipStream_t st) {
   const size_t bytes =
-      (size_t)(Sym2D<T, BS>::BUF + 6 * 8 * BS + 16 + a.mt * (a.mt + 1) / 2) * sizeof(T);
-  hipLaunchKernelGGL((dual_range_kernel<T, BS>), dim3(a.batch), dim3(kWave), bytes, st, a);
+      (size_t)(Sym2D<T, BS>::BUF + 16 + 8 * Sym2D<T, BS>::NMAX + a.mt * (a.mt + 1) / 2) * sizeof(T);
+  const char* w3 = getenv("MPCQP_POLY_W3");
+  if (w3 && atoi(w3) == 1)
+    hipLaunchKernelGGL((dual_range_kernel<T, BS, 3>), dim3(a.batch), dim3(kWave), bytes, st, a);
+  else
+    hipLaunchKernelGGL((dual_range_kernel<T, BS, 1>), dim3(a.batch), dim3(kWave), bytes, st, a);
 }
 
 template <typename T>

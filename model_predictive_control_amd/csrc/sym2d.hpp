@@ -110,7 +110,8 @@ struct Sym2D {
   static constexpr int NV = NMAX;  // row-indexed vectors
   static constexpr int NC = BS;    // columns per lane
   static constexpr int RPL = BS;   // rows per lane
-  // LDS scratch a kernel must provide: BUF elements
+  // LDS scratch a kernel must provide: BUF elements (column buffer NMAX, the
+  // mat-vec's vector at NMAX * BS)
   static constexpr int BUF = NMAX * BS + NMAX;
   T m[BS][BS];
   int bi, bj;
@@ -139,47 +140,100 @@ struct Sym2D {
 
   // Column k (wave-uniform) of M: colr[r] = M[bi*BS+r][k] for this lane's rows,
   // colc[c] = M[bj*BS+c][k] (= row k, by symmetry) for its columns; returns
-  // M_kk.  The owning block column publishes its whole BS x BS tile rows so
-  // that the (runtime) column offset is applied to an LDS address, never to a
-  // register index.
-  __device__ __forceinline__ T column(int k, T* buf, T (&colr)[BS], T (&colc)[BS]) {
-    const int kb = k / BS, kc = k - kb * BS;
-    if (bj == kb) {
+  // M_kk.  The owning block column publishes only its column kc = k mod BS:
+  // a uniform switch over kc (scalar branches; the asm marker keeps the cases
+  // from being merged back into one runtime register index, which would live
+  // in scratch), BS stores per owner lane instead of its whole tile.
+  template <int C>
+  __device__ __forceinline__ void put_col(int kc, T* buf) {
+    if constexpr (C < BS) {
+      if (kc == C) {
 #pragma unroll
-      for (int r = 0; r < BS; ++r)
-#pragma unroll
-        for (int c = 0; c < BS; ++c) buf[(bi * BS + r) * BS + c] = m[r][c];
+        for (int r = 0; r < BS; ++r) buf[bi * BS + r] = m[r][C];
+        asm volatile("; s2col %0" ::"n"(C));
+      } else {
+        put_col<C + 1>(kc, buf);
+      }
     }
+  }
+  __device__ __forceinline__ T column(int k, T* buf, T (&colr)[BS], T (&colc)[BS]) {
+    T unused;
+    return column<false>(k, buf, colr, colc, unused);
+  }
+  // The same, and with LANE: cl = M[lane][k] for the row-per-lane layout
+  // (lanes past NMAX read row 0).
+  template <bool LANE>
+  __device__ __forceinline__ T column(int k, T* buf, T (&colr)[BS], T (&colc)[BS], T& cl) {
+    k = __builtin_amdgcn_readfirstlane(k);
+    const int kb = k / BS, kc = k - kb * BS;
+    if (bj == kb) put_col<0>(kc, buf);
     lds_exchange();
 #pragma unroll
-    for (int r = 0; r < BS; ++r) colr[r] = buf[(bi * BS + r) * BS + kc];
+    for (int r = 0; r < BS; ++r) colr[r] = buf[bi * BS + r];
 #pragma unroll
-    for (int c = 0; c < BS; ++c) colc[c] = buf[(bj * BS + c) * BS + kc];
-    const T d = buf[k * BS + kc];
+    for (int c = 0; c < BS; ++c) colc[c] = buf[bj * BS + c];
+    if constexpr (LANE) {
+      const int l = (int)lane_id();
+      cl = buf[l < NMAX ? l : 0];
+    }
+    const T d = buf[k];
     lds_exchange();
     return d;
   }
 
   // Goodnight sweep on pivot k with its column fetched (d = M_kk): sigma =
   // +1 moves k into the swept set, sigma = -1 (reverse sweep) moves it out.
-  // Row/column k are selected, not produced by cancellation.
+  // Every element takes the rank-1 update; row and column k are then set
+  // (selected, not produced by cancellation) by the lanes that hold them,
+  // through uniform switches over k's in-block offset.
+  // row k: sigma rd M[k][j] (-rd on the diagonal), on the lanes with bi == kb
+  template <int R>
+  __device__ __forceinline__ void patch_row(int kc, bool on, int k, T rd, T srd,
+                                            const T (&colc)[BS]) {
+    if constexpr (R < BS) {
+      if (kc == R) {
+#pragma unroll
+        for (int c = 0; c < BS; ++c) {
+          const T v = (bj * BS + c) == k ? -rd : srd * colc[c];
+          m[R][c] = on ? v : m[R][c];
+        }
+        asm volatile("; s2row %0" ::"n"(R));
+      } else {
+        patch_row<R + 1>(kc, on, k, rd, srd, colc);
+      }
+    }
+  }
+  // column k: sigma rd M[i][k], on the lanes with bj == kb
+  template <int C>
+  __device__ __forceinline__ void patch_col(int kc, bool on, int k, T rd, T sigma,
+                                            const T (&ar)[BS]) {
+    if constexpr (C < BS) {
+      if (kc == C) {
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+          const T v = (bi * BS + r) == k ? -rd : sigma * ar[r];
+          m[r][C] = on ? v : m[r][C];
+        }
+        asm volatile("; s2pc %0" ::"n"(C));
+      } else {
+        patch_col<C + 1>(kc, on, k, rd, sigma, ar);
+      }
+    }
+  }
   __device__ __forceinline__ void sweep_col(int k, T sigma, T d, const T (&colr)[BS],
                                             const T (&colc)[BS]) {
+    k = __builtin_amdgcn_readfirstlane(k);
+    const int kb = k / BS, kc = k - kb * BS;
     const T rd = fast_rcp(d);
     T ar[BS];
 #pragma unroll
     for (int r = 0; r < BS; ++r) ar[r] = colr[r] * rd;
 #pragma unroll
-    for (int r = 0; r < BS; ++r) {
-      const bool ik = (bi * BS + r) == k;
+    for (int r = 0; r < BS; ++r)
 #pragma unroll
-      for (int c = 0; c < BS; ++c) {
-        const bool jk = (bj * BS + c) == k;
-        const T gen = fma(-ar[r], colc[c], m[r][c]);
-        const T spec = ik ? (jk ? -rd : sigma * colc[c] * rd) : sigma * ar[r];
-        m[r][c] = (ik || jk) ? spec : gen;
-      }
-    }
+      for (int c = 0; c < BS; ++c) m[r][c] = fma(-ar[r], colc[c], m[r][c]);
+    patch_row<0>(kc, bi == kb, k, rd, sigma * rd, colc);
+    patch_col<0>(kc, bj == kb, k, rd, sigma, ar);
   }
 
   // Fetch column k and sweep on it.  Returns the pivot M_kk.
@@ -211,6 +265,67 @@ struct Sym2D {
     lds_exchange();
   }
 };
+
+// out_l = sum_j M[l][j] w_j with both vectors one row per lane (lane l = row
+// l; lanes past NMAX pass 0 and get row 0's value).  Uses the mat-vec's
+// vector slot of buf and its column slot for the result.
+template <typename T, int BS>
+__device__ __forceinline__ T matvec_lane(const Sym2D<T, BS>& W, T w, T* buf) {
+  constexpr int NMAX = Sym2D<T, BS>::NMAX;
+  T* wb = buf + NMAX * BS;
+  const int l = (int)lane_id();
+  if (l < NMAX) wb[l] = w;
+  lds_exchange();
+  T wc[BS];
+#pragma unroll
+  for (int c = 0; c < BS; ++c) wc[c] = wb[W.bj * BS + c];
+  T out[BS];
+#pragma unroll
+  for (int r = 0; r < BS; ++r) {
+    T s = T(0);
+#pragma unroll
+    for (int c = 0; c < BS; ++c) s = fma(W.m[r][c], wc[c], s);
+    out[r] = rowblock_sum(s);
+  }
+  if (W.bj == 0) {
+#pragma unroll
+    for (int r = 0; r < BS; ++r) buf[W.bi * BS + r] = out[r];
+  }
+  lds_exchange();
+  const T v = buf[l < NMAX ? l : 0];
+  lds_exchange();
+  return v;
+}
+
+// The same with the row sums reduced through LDS instead of DPP butterflies:
+// every lane stores its BS partial row sums (part: 8 * NMAX elements), and
+// lane l adds the 8 partials of row l -- BS stores, 8 loads and 7 adds per
+// lane instead of 3 DPP steps per row.
+template <typename T, int BS>
+__device__ __forceinline__ T matvec_lane_lds(const Sym2D<T, BS>& W, T w, T* buf, T* part) {
+  constexpr int NMAX = Sym2D<T, BS>::NMAX;
+  T* wb = buf + NMAX * BS;
+  const int l = (int)lane_id();
+  if (l < NMAX) wb[l] = w;
+  lds_exchange();
+  T wc[BS];
+#pragma unroll
+  for (int c = 0; c < BS; ++c) wc[c] = wb[W.bj * BS + c];
+#pragma unroll
+  for (int r = 0; r < BS; ++r) {
+    T s = T(0);
+#pragma unroll
+    for (int c = 0; c < BS; ++c) s = fma(W.m[r][c], wc[c], s);
+    part[(W.bi * BS + r) * 8 + W.bj] = s;
+  }
+  lds_exchange();
+  const T* pr = part + (l < NMAX ? l : 0) * 8;
+  T v = pr[0];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) v += pr[q];
+  lds_exchange();
+  return v;
+}
 
 // Publish a row-block vector to LDS (vb[0..8*BS)) so that a wave-uniform
 // element can be read back by address.
