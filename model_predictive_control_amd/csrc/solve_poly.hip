@@ -28,8 +28,6 @@
 // pivot W_pp (its Schur complement -- zero when p depends on the active rows,
 // in which case a pure dual step drops rows first), dropping row k is a
 // reverse sweep.  Same register-resident sweep machinery as solve_box.hip.
-#include <cstdlib>
-
 #include "sym2d.hpp"
 
 namespace mpcqp {
@@ -61,8 +59,10 @@ struct DualArgs {
 // row-indexed vector (s0, bounds, scales, y, s, st) one row per lane (lane i =
 // row i, mt <= 64), so the scan and the ratio test run once per row instead
 // of once per row-block replica, with full-wave DPP arg-max / arg-min.
-template <typename T, int BS, int WPS>
-__global__ __launch_bounds__(64, WPS) void dual_range_kernel(DualArgs<T> a) {
+// (218 VGPRs: 2 waves per SIMD.  Forcing 3 spills 212 B per lane and doubles
+// the time: measured 5.11 vs 2.73 ms at config 4.)
+template <typename T, int BS>
+__global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
   using S2 = Sym2D<T, BS>;
   constexpr int NMAX = S2::NMAX;
   static_assert(NMAX <= kWave, "one row per lane");
@@ -369,11 +369,7 @@ template <typename T, int BS>
 static void launch_dual(const DualArgs<T>& a, hipStream_t st) {
   const size_t bytes =
       (size_t)(Sym2D<T, BS>::BUF + 16 + 8 * Sym2D<T, BS>::NMAX + a.mt * (a.mt + 1) / 2) * sizeof(T);
-  const char* w3 = getenv("MPCQP_POLY_W3");
-  if (w3 && atoi(w3) == 1)
-    hipLaunchKernelGGL((dual_range_kernel<T, BS, 3>), dim3(a.batch), dim3(kWave), bytes, st, a);
-  else
-    hipLaunchKernelGGL((dual_range_kernel<T, BS, 1>), dim3(a.batch), dim3(kWave), bytes, st, a);
+  hipLaunchKernelGGL((dual_range_kernel<T, BS>), dim3(a.batch), dim3(kWave), bytes, st, a);
 }
 
 template <typename T>

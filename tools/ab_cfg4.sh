@@ -6,5 +6,3 @@ timeout -k 10 200 python bench.py --config 4 --steps 20 --warmup 3 --no-cpu > $O
 python -c "import json; d=json.load(open('$O/c4.json')); print(d['value'], d['max_abs_u_err_vs_oracle'], d['status_hist'], d.get('kernel_us'), d.get('iters_mean'))"
 timeout -k 10 200 python bench.py --steps 50 --warmup 5 --no-cpu > $O/c2.json 2>$O/c2.err
 python -c "import json; d=json.load(open('$O/c2.json')); print(d['value'], d['max_abs_u_err_vs_oracle'], d.get('kernel_us'))"
-MPCQP_POLY_W3=1 timeout -k 10 200 python bench.py --config 4 --steps 20 --warmup 3 --no-cpu > $O/c4w3.json 2>$O/c4w3.err
-python -c "import json; d=json.load(open('$O/c4w3.json')); print('w3', d['value'], d['max_abs_u_err_vs_oracle'], d['status_hist'], d.get('kernel_us'), d.get('iters_mean'))"
