@@ -275,6 +275,108 @@ class Config2:
                           f"oracle/c/mpcqp_oracle.c) in {dt:.1f} s on {cores} host threads"}
 
 
+class Config2Loop:
+    """Config 2's plant and MPC (FHC double integrator, N=20, |u|<=1, fp64) in
+    a receding-horizon loop on the device: one bench step = one episode of
+    --loop-steps closed-loop steps for the batch (mpcqp_condense once, then
+    mpcqp_mpc_box_loop: every step warm-started from the shifted previous
+    active set).  Unit: closed-loop MPC steps (instance x step) per second,
+    the per-step counterpart of the config-2 solves/s."""
+
+    dtype = torch.float64
+    dname = "f64"
+    default_batch = 4096
+    default_slots = 4
+    default_steps = (50, 5)
+    default_loop_steps = 50
+
+    def __init__(self, args, dev, rank):
+        self.base = Config2(args, dev, rank)
+        self.args, self.dev = args, dev
+        self.T = args.loop_steps
+        self.units_per_step = self.T
+        b, c = self.base, self.base
+        bsz, S, n = args.batch, args.slots, c.n
+        t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64, device=dev)  # noqa: E731
+        self.A_t, self.B_t = t(b.A), t(b.B)
+        self.cd = {"H": torch.empty((bsz, n * (n + 1) // 2), dtype=torch.float64, device=dev),
+                   "F": torch.empty((bsz, n, 2), dtype=torch.float64, device=dev)}
+        self.outs = [{"xs": torch.empty((self.T + 1, bsz, 2), dtype=torch.float64, device=dev),
+                      "us": torch.empty((self.T, bsz, 1), dtype=torch.float64, device=dev),
+                      "status": torch.empty((self.T, bsz), dtype=torch.int32, device=dev)}
+                     for _ in range(S)]
+        self.ST = torch.empty((S, bsz), dtype=torch.int32, device=dev)
+
+    def workload(self):
+        return {"workload": f"cfg2-loop: config-2 plant and MPC (FHC.py double integrator, ts=0.5, "
+                            f"N=20, |u|<=1, per-instance (A,B)) in a {self.T}-step receding-horizon "
+                            f"loop on the device, x0~U(-10,10)^2; per episode: mpcqp_condense once + "
+                            f"mpcqp_mpc_box_loop (warm-started active sets)",
+                "horizon": self.base.N, "nx": 2, "nu": 1, "samples": self.T}
+
+    def _episode(self, s):
+        b = self.base
+        batched.condense(b.A_b, b.B_b, b.Q_t, b.R_t, b.Qf_t, b.N, outputs=("H", "F"), out=self.cd)
+        batched.mpc_box_loop(b.A_b, b.B_b, b.Q_t, b.R_t, b.Qf_t, b.N, b.X0_t[s], b.lb, b.ub, self.T,
+                             condensed=self.cd, out=self.outs[s])
+
+    def step(self, s):
+        self._episode(s)
+        # an episode is optimal when every one of its steps is
+        st = self.outs[s]["status"]
+        self.ST[s].copy_((st & 0xFF).amax(0))
+
+    def status(self):
+        return self.ST
+
+    def kernels(self, traffic):
+        R = self.args.reps
+        b, bsz, n, T = self.base, self.args.batch, self.base.n, self.T
+        t_e = time_kernel(lambda: self._episode(0), max(2, R // 10), self.dev)
+        t_c = time_kernel(lambda: batched.condense(b.A_b, b.B_b, b.Q_t, b.R_t, b.Qf_t, b.N,
+                                                   outputs=("H", "F"), out=self.cd), R, self.dev)
+        t_l = t_e - t_c
+        torch.cuda.synchronize()
+        its = ((self.outs[0]["status"] >> 8) & 0xFFFF).double()
+        # per step and instance: each sweep / active-set iteration one rank-1
+        # update of the n x n matrix (2 n^2 flops) plus the mat-vec refresh
+        flops = float(its.sum()) * 2 * n * n + T * bsz * (2 * n * n + 2 * n * 2)
+        r = roof("box_loop_kernel<double,2,1,5>", "valu-fp64", flops, t_l, FP64_PEAK_TFS, "TFLOP/s",
+                 traffic.get("box_loop"),
+                 {"flops_per_launch": flops, "note": "T closed-loop steps in one launch; flops = "
+                  "(sweeps + active-set iterations + 1 refresh) x 2n^2 per step and instance"})
+        extra = {"kernel_us": {"episode": round(t_e * 1e3, 2), "condense_once": round(t_c * 1e3, 2),
+                               "box_loop": round(t_l * 1e3, 2)},
+                 "us_per_closed_loop_step": round(t_e * 1e3 / T, 3),
+                 "loop_kernel_us_per_step": round(t_l * 1e3 / T, 3),
+                 "sweeps_iters_first_step_mean": round(float(its[0].mean()), 2),
+                 "sweeps_iters_later_steps_mean": round(float(its[1:].mean()), 2) if T > 1 else None}
+        return r, {}, extra
+
+    def check(self):
+        """Max |x - x_ref| over the episode of 16 instances of slot 0 against
+        the host loop: the C/OpenMP oracle's config-2 MPC step (per-instance
+        condense + GI box QP) and x+ = A x + B u_0 on the host."""
+        from oracle import cbaseline as cbl
+
+        b = self.base
+        nchk = min(16, self.args.batch)
+        x = b.X0[0, :nchk].copy()
+        xs = self.outs[0]["xs"][:, :nchk].cpu().numpy()
+        err = 0.0
+        for k in range(self.T):
+            err = max(err, float(np.abs(xs[k] - x).max()))
+            zr, _ = cbl.mpc_box(b.A, b.B, b.Q, b.R, b.Qf, b.N, x, -1.0, 1.0, nthreads=1)
+            x = x @ b.A.T + zr[:, :1] @ b.B.T
+        return err
+
+    def cpu_baseline(self, seconds):
+        r = self.base.cpu_baseline(seconds)
+        r["unit"] = "closed-loop MPC steps/s"
+        r["sample"] += " (one closed-loop step on the host = one such solve + x+ = Ax + Bu)"
+        return r
+
+
 def _stable_plant(rng, nx, nu, rho=0.98):
     U, _ = np.linalg.qr(rng.normal(size=(nx, nx)))
     sig = rng.uniform(0.5, rho, size=nx)
@@ -853,8 +955,8 @@ class ConfigLoop:
         return None
 
 
-CONFIGS = {"2": Config2, "3": Config3, "4": Config4, "5": Config5, "nlp": ConfigNLP,
-           "loop": ConfigLoop}
+CONFIGS = {"2": Config2, "2loop": Config2Loop, "3": Config3, "4": Config4, "5": Config5,
+           "nlp": ConfigNLP, "loop": ConfigLoop}
 
 
 def main():
@@ -867,7 +969,8 @@ def main():
                          "MPCController.solve), loop (on-device receding-horizon loop)")
     ap.add_argument("--sqp-iters", type=int, default=0,
                     help="nlp: SQP iterations per solve (default 30); loop: per sample (8)")
-    ap.add_argument("--loop-steps", type=int, default=20, help="loop: samples per episode")
+    ap.add_argument("--loop-steps", type=int, default=0,
+                    help="loop / 2loop: closed-loop steps per episode (default 20 / 50)")
     ap.add_argument("--gather", action="store_true",
                     help="N>1: time the final all-gather of z (RCCL) after the timed loop")
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU per step (0 = config default)")
@@ -889,6 +992,7 @@ def main():
     args.batch = args.batch or C.default_batch
     args.slots = args.slots or C.default_slots
     args.sqp_iters = args.sqp_iters or getattr(C, "default_sqp_iters", 0)
+    args.loop_steps = args.loop_steps or getattr(C, "default_loop_steps", 20)
     dsteps, dwarm = getattr(C, "default_steps", (200, 20))
     args.steps = args.steps or dsteps
     args.warmup = dwarm if args.warmup < 0 else args.warmup

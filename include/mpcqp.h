@@ -425,6 +425,30 @@ int mpcqp_sqp_shift(int dtype, int batch, int N, void* U, void* y, void* pi, int
                     double* rho, double* mu, double* kkt, double mu0, void* stream);
 
 /*
+ * The receding-horizon loop of an input-box MPC on a linear plant, T steps in
+ * one launch (session_1 LinearSystem.simulate, LinearSystem.py:20-26, under
+ * the box-constrained MPC policy of session_4 MPCController.solve,
+ * main.py:115-116 / input box main.py:68-69; simulate(...) main.py:270-271):
+ *   for t = 0..steps-1:  z_t = argmin 1/2 z'Hz + (F x_t)'z,  lb <= z <= ub
+ *                        x_{t+1} = A x_t + B u_0(z_t)
+ * H (packed lower n(n+1)/2, n = N*nu) and F (n x nx) are the instance's
+ * condensed problem (mpcqp_condense of the same plant, once per episode);
+ * A (nx x nx), Bm (nx x nu) the plant (stride 0 = shared).  Each step is
+ * warm-started from the previous active set shifted one stage.  Outputs:
+ * xs ((steps+1) x batch x nx: x_0..x_T), us (steps x batch x nu: the applied
+ * u_0), zs (optional, steps x batch x n: the input plans, the
+ * input_prediction of ControllerLog), status (steps x batch; bits 8..23 =
+ * sweeps + active-set iterations of the step; us and status may be NULL
+ * when steps = 0).  Limits: nx <= 4, nu <= 2, N*nu <= 32.
+ */
+int mpcqp_mpc_box_loop(int dtype, int batch, int nx, int nu, int N, int steps,
+                       const void* H, int64_t strideH, const void* F, int64_t strideF,
+                       const void* A, int64_t strideA, const void* Bm, int64_t strideB,
+                       const void* x0, int64_t strideX0, const void* lb, int64_t strideLb,
+                       const void* ub, int64_t strideUb, void* xs, void* us, void* zs,
+                       int32_t* status, int max_iter, double tol, void* stream);
+
+/*
  * Batched finite-horizon Riccati recursion, FHC.py:51-61:
  *   K_k = -(R + B'P B)^{-1} B'P A,  P_k = Q + A'P A + A'P B K_k,  P_N = Pf
  * Outputs in the reference's order (lists reversed: K[0] is the first-stage

@@ -24,7 +24,7 @@ import torch
 from . import _native as nat
 
 __all__ = [
-    "condense", "solve_box", "mpc_box", "mpc_qp", "mpc_ipm", "solve_poly", "solve_qp", "sweep", "riccati", "gemv",
+    "condense", "solve_box", "mpc_box", "mpc_box_loop", "mpc_qp", "mpc_ipm", "solve_poly", "solve_qp", "sweep", "riccati", "gemv",
     "rollout", "bicycle_rti", "bicycle_linearise", "bicycle_hessian", "bicycle_sqp_step",
     "pack_lower", "unpack_lower", "status_code", "status_iters", "workspace_bytes",
 ]
@@ -360,6 +360,53 @@ def mpc_ipm(A, B, Q, R, Qf, N: int, x0, xlo=None, xhi=None, lb=None, ub=None, c=
                            int(skip_mask) if skip is not None else 0, int(max_iter),
                            float(tol), _ptr(ws), wsb, _stream())
     nat.check(rc, "mpcqp_mpc_ipm")
+    return o
+
+
+def mpc_box_loop(A, B, Q, R, Qf, N: int, x0, lb=None, ub=None, steps: int = 1, *,
+                 plans: bool = False, max_iter: int = 0, tol: float = 0.0,
+                 condensed: dict | None = None, out: dict | None = None) -> dict:
+    """The receding-horizon loop of the input-box MPC on a linear plant, on
+    the device (include/mpcqp.h ``mpcqp_mpc_box_loop``): for t < steps,
+    z_t = argmin 1/2 z'Hz + (F x_t)'z over lb <= z <= ub, x_{t+1} = A x_t + B
+    u_0(z_t) -- LinearSystem.simulate (LinearSystem.py:20-26) under the MPC
+    policy of MPCController.solve (main.py:115-116).  A (nx,nx) | (b,nx,nx), B
+    likewise; x0 (b, nx).  H and F come from ``condense`` of the same plant
+    (once; pass ``condensed`` to reuse them).  Returns xs (steps+1, b, nx), us
+    (steps, b, nu), status (steps, b), and with ``plans`` zs (steps, b, N*nu)."""
+    dt = A.dtype if isinstance(A, torch.Tensor) else torch.float64
+    dev = A.device if isinstance(A, torch.Tensor) else torch.device("cuda")
+    A, B = _dev(A, dt, dev), _dev(B, dt, dev)
+    x0 = _dev(x0, dt, dev)
+    nx, nu = int(B.shape[-2]), int(B.shape[-1])
+    if x0.ndim != 2 or x0.shape[1] != nx:
+        raise ValueError(f"x0 must be (batch, {nx}), got {tuple(x0.shape)}")
+    batch, n, T = int(x0.shape[0]), N * nu, int(steps)
+    cd = condensed or condense(A, B, Q, R, Qf, N, outputs=("H", "F"))
+    H, F = cd["H"], cd["F"]
+    sH, _ = _inst(H, 1, "H")
+    sF, _ = _inst(F, 2, "F")
+    if H.ndim == 2 and H.shape[0] == 1:   # a shared plant condenses to one instance
+        sH = 0
+    if F.ndim == 3 and F.shape[0] == 1:
+        sF = 0
+    sA, _ = _inst(A, 2, "A")
+    sB, _ = _inst(B, 2, "B")
+    lbt, slb = _bound(lb, n, dt, dev)
+    ubt, sub = _bound(ub, n, dt, dev)
+    o = dict(out or {})
+    shapes = dict(xs=((T + 1, batch, nx), dt), us=((T, batch, nu), dt),
+                  status=((T, batch), torch.int32))
+    if plans:
+        shapes["zs"] = ((T, batch, n), dt)
+    for k, (shp, kd) in shapes.items():
+        if k not in o:
+            o[k] = torch.empty(shp, dtype=kd, device=dev)
+    rc = _lib().mpcqp_mpc_box_loop(_code(dt), batch, nx, nu, N, T, _ptr(H), sH, _ptr(F), sF,
+                                   _ptr(A), sA, _ptr(B), sB, _ptr(x0), nx, _ptr(lbt), slb,
+                                   _ptr(ubt), sub, _ptr(o["xs"]), _ptr(o["us"]), _ptr(o.get("zs")),
+                                   _ptr(o["status"]), int(max_iter), float(tol), _stream())
+    nat.check(rc, "mpcqp_mpc_box_loop")
     return o
 
 

@@ -277,17 +277,21 @@ __device__ __forceinline__ void qscan(const Mat& M, const int (&st)[BS], const T
 }
 
 
-template <typename T, int BS, class Mat>
-__device__ __forceinline__ int gi_box(Mat& M, T* gb, const T* fs, const T* lbs,
-                                           const T* ubs, int n, int max_iter, T tol, bool live,
-                                           T (&zr)[BS], int& iters MPCQP_CLK_PARAM) {
+// WARM: st (this lane's rows: 0 free, 1 at lb, 2 at ub, 3 padding) is the
+// starting active set and M the matrix swept on its free rows (H swept on F
+// equals -H^-1 swept back on the active rows); the active rows whose
+// multipliers have the wrong sign are released first (one sweep each), then
+// the active set runs as from a cold start.  st is returned either way.
+template <typename T, int BS, bool WARM, class Mat>
+__device__ __forceinline__ int gi_box_st(Mat& M, T* gb, const T* fs, const T* lbs,
+                                         const T* ubs, int n, int max_iter, T tol, bool live,
+                                         T (&zr)[BS], int& iters, int (&st)[BS] MPCQP_CLK_PARAM) {
   QBounds<T, BS> B;
   B.load(M, lbs, ubs);
-  int st[BS];
   T mu[BS];
 #pragma unroll
   for (int r = 0; r < BS; ++r) {
-    st[r] = (M.bi * BS + r < n) ? 0 : 3;
+    if constexpr (!WARM) st[r] = (M.bi * BS + r < n) ? 0 : 3;
     mu[r] = T(0);
     zr[r] = T(0);
   }
@@ -313,6 +317,43 @@ __device__ __forceinline__ int gi_box(Mat& M, T* gb, const T* fs, const T* lbs,
   };
   refresh();
   bool active = live;
+  if constexpr (WARM) {
+    // release wrong-signed multipliers, the most negative first
+    bool drop = live;
+    while (true) {
+      T mv = Lim<T>::inf();
+      int k = 0;
+#pragma unroll
+      for (int r = 0; r < BS; ++r) {
+        const bool a = (st[r] == 1 || st[r] == 2) && mu[r] < -tol;
+        const bool take = a && mu[r] < mv;
+        mv = take ? mu[r] : mv;
+        k = take ? (M.bi * BS + r) : k;
+      }
+      rows_argmin(M, mv, k);
+      drop = drop && mv < Lim<T>::inf();
+      if (!__any(drop)) break;
+      if (drop && ++iters > max_iter) {
+        code = MPCQP_STATUS_MAXITER;
+        drop = false;
+        active = false;
+      }
+      T kr[BS], kc[Mat::NC];
+      const T d = M.column(k, gb, kr, kc);
+      if (drop && !(d > T(0))) {
+        code = MPCQP_STATUS_NOT_CONVEX;
+        drop = false;
+        active = false;
+      }
+      if (drop) {
+        M.sweep_col(k, T(1), d, kr, kc);
+#pragma unroll
+        for (int r = 0; r < BS; ++r)
+          if (M.bi * BS + r == k) st[r] = 0;
+      }
+      refresh();
+    }
+  }
   for (int pass = 0; pass < 3; ++pass) {
     bool need_p = true;
     int p = 0, side = 1;
@@ -427,6 +468,15 @@ __device__ __forceinline__ int gi_box(Mat& M, T* gb, const T* fs, const T* lbs,
     zr[r] = fmin(fmax(zr[r], B.lo[r]), B.hi[r]);
   }
   return code;
+}
+
+template <typename T, int BS, class Mat>
+__device__ __forceinline__ int gi_box(Mat& M, T* gb, const T* fs, const T* lbs,
+                                           const T* ubs, int n, int max_iter, T tol, bool live,
+                                           T (&zr)[BS], int& iters MPCQP_CLK_PARAM) {
+  int st[BS];
+  return gi_box_st<T, BS, false>(M, gb, fs, lbs, ubs, n, max_iter, tol, live, zr, iters,
+                                 st MPCQP_CLK_ARG);
 }
 
 }  // namespace mpcqp
