@@ -144,3 +144,21 @@ class ClosedLoop:
 
     def _reset(self, s):
         s["sqp"].reset()
+
+
+def lti_box_mpc_loop(A, B, Q, R, Qf, N: int, X0, lb, ub, steps: int) -> dict:
+    """The receding-horizon loop of the input-box MPC on a linear plant
+    (LinearSystem.simulate, session_1/LinearSystem.py:20-26, with the
+    box-constrained MPC step as the policy; simulate(...) main.py:270-271),
+    all ``steps`` in one launch (``batched.mpc_box_loop``; each step
+    warm-started from the shifted previous active set).  X0 (b, nx) ->
+    xs (T+1, b, nx), us (T, b, nu), success (T, b), iters (T, b), and the
+    ControllerLog input_prediction (T, b, N, nu)."""
+    dev = torch.device("cuda")
+    t = lambda a: torch.as_tensor(a, dtype=torch.float64, device=dev)  # noqa: E731
+    A, B, X0 = t(A), t(B), t(X0).reshape(-1, t(A).shape[-1])
+    r = batched.mpc_box_loop(A, B, t(Q), t(R), t(Qf), N, X0, lb, ub, steps, plans=True)
+    nu = B.shape[-1]
+    return {"xs": r["xs"], "us": r["us"], "success": batched.status_code(r["status"]) == 0,
+            "iters": batched.status_iters(r["status"]),
+            "input_prediction": r["zs"].reshape(steps, X0.shape[0], N, nu)}

@@ -138,3 +138,17 @@ def test_loop_edge_cases(dev):
     assert (code[:, 1] == 3).all() and (code[:, [0, 2]] == 0).all()
     with pytest.raises(Exception):
         batched.mpc_box_loop(t(A), t(B), t(Q), t(R), t(Qf), 40, t(X0), -1.0, 1.0, 2)  # N*nu > 32
+
+
+def test_lti_loop_helper(dev):
+    """closed_loop.lti_box_mpc_loop: the ControllerLog-shaped outputs of the
+    same episode (success per step, input_prediction (T, b, N, nu) whose first
+    input is the applied one)."""
+    from model_predictive_control_amd.closed_loop import lti_box_mpc_loop
+
+    A, B, Q, R, Qf = _fhc_plant()
+    X0 = np.array([[5.0, -3.0], [-8.0, 2.0]])
+    out = lti_box_mpc_loop(A, B, Q, R, Qf, 20, X0, -1.0, 1.0, 6)
+    assert out["success"].all()
+    assert tuple(out["input_prediction"].shape) == (6, 2, 20, 1)
+    assert torch.equal(out["input_prediction"][:, :, 0], out["us"])
