@@ -22,6 +22,7 @@
 
 #define MPCQP_HD __host__ __device__
 #include "ipm_lane.hpp"
+#include "ipm_quad.hpp"
 
 namespace mpcqp {
 
@@ -44,6 +45,17 @@ __global__ __launch_bounds__(64) void ipm_lds_kernel(ipm::Args<T> a) {
   const int b = blockIdx.x * G + lane;
   if (lane >= G || b >= a.batch) return;
   ipm::solve_lane<T, NX, NU, G>(a, b, ipm_lds + lane);
+}
+
+// Four lanes per instance (ipm_quad.hpp), G instances per workgroup, the
+// workspace in LDS.  The (4, 2) shapes whose horizon fits 160 KB of LDS.
+template <typename T, int G>
+__global__ __launch_bounds__(64, 1) void ipm_quad_kernel(ipm::Args<T> a) {
+  extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
+  const int g = threadIdx.x >> 2;
+  const int b = blockIdx.x * G + g;
+  if (g >= G || b >= a.batch) return;
+  ipmq::solve_quad<T, G>(a, b, ipm_lds + g);
 }
 
 static int64_t ipm_ldb(int batch) { return ((int64_t)batch + 63) / 64 * 64; }
@@ -81,8 +93,40 @@ bool ipm_supported(int nx, int nu) {
   return ipm_dims(nx, nu, NX, NU);
 }
 
+template <typename T>
+static int ipm_quad_launch(ipm::Args<T>& a, hipStream_t st) {
+  const int F = ipm::Layout<4, 2>::F;
+  const size_t per = (size_t)a.N * F * sizeof(double);
+  const int G = per * 4 <= 160 * 1024 ? 4 : (per * 2 <= 160 * 1024 ? 2 : 1);
+  const size_t bytes = (size_t)G * per;
+  auto launch = [&](auto kern) -> int {
+    if (bytes > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+      if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(ipm_quad)");
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)((a.batch + G - 1) / G)), dim3(64), bytes, st, a);
+    MPCQP_CHECK_LAUNCH("ipm_quad_kernel");
+    return MPCQP_OK;
+  };
+  if (G == 4) return launch(ipm_quad_kernel<T, 4>);
+  if (G == 2) return launch(ipm_quad_kernel<T, 2>);
+  return launch(ipm_quad_kernel<T, 1>);
+}
+
+// The quad kernel for the (4, 2) shapes whose horizon fits LDS;
+// MPCQP_IPM_QUAD=0 selects the lane-per-instance kernels instead.
+static bool ipm_use_quad(int N) {
+  const char* env = getenv("MPCQP_IPM_QUAD");
+  if (env && atoi(env) == 0) return false;
+  return (size_t)N * ipm::Layout<4, 2>::F * sizeof(double) <= 160 * 1024;
+}
+
 template <typename T, int NX, int NU>
 static int ipm_launch_t(ipm::Args<T>& a, hipStream_t st) {
+  if constexpr (NX == 4 && NU == 2) {
+    if (ipm_use_quad(a.N)) return ipm_quad_launch(a, st);
+  }
   const int F = ipm::Layout<NX, NU>::F;
   const int G = ipm_lds_group(a.batch, F, a.N);
   const dim3 blk(64);
