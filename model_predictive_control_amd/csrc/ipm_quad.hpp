@@ -68,6 +68,29 @@ MPCQP_QD double sel4RowB(const double (&M)[4][2], int i, int r) {
 constexpr int NX = 4, NU = 2;
 using L = Layout<NX, NU>;
 
+// Workspace accessor of one quad: field f of stage k, and the lane-relative
+// fields with the lane's row offset folded into a per-lane base pointer, so
+// every access is a base + compile-time immediate (a runtime row index in
+// the field offset costs address arithmetic on every access):
+//   r(k, f) = f + i,  ra(k, f) = f + i*NX,  rb(k, f) = f + i*NU,
+//   p(k, f, j) = f + pk(i, j)  (row i of a packed symmetric block).
+template <int LD>
+struct WsQ {
+  double* W;
+  double* Wi;
+  double* Wa;
+  double* Wb;
+  double* Wp[4];
+  MPCQP_QD WsQ(double* w, int i)
+      : W(w), Wi(w + i * LD), Wa(w + i * NX * LD), Wb(w + i * NU * LD),
+        Wp{w + pk(i, 0) * LD, w + pk(i, 1) * LD, w + pk(i, 2) * LD, w + pk(i, 3) * LD} {}
+  MPCQP_QD double& operator()(int k, int f) const { return W[(k * L::F + f) * LD]; }
+  MPCQP_QD double& r(int k, int f) const { return Wi[(k * L::F + f) * LD]; }
+  MPCQP_QD double& ra(int k, int f) const { return Wa[(k * L::F + f) * LD]; }
+  MPCQP_QD double& rb(int k, int f) const { return Wb[(k * L::F + f) * LD]; }
+  MPCQP_QD double& p(int k, int f, int j) const { return Wp[j][(k * L::F + f) * LD]; }
+};
+
 // The stage data every lane reads several times per stage, in registers.
 struct StageQ {
   double A[4][4], B[4][2], WXU[4][2], WUU[3];
@@ -114,7 +137,7 @@ MPCQP_QD bool riccati_q(const W& at, const StageQ& S, int k, int i, double (&Ph)
   // P_{k+1} row i = Q' + H2xx_{k+1} + Sigma_x + Ph,  p = g_x + ph
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    P[j] = at(k, L::WXX + pk(i, j)) + Ph[j] + (i == j ? sx + dreg : 0.0);
+    P[j] = at.p(k, L::WXX, j) + Ph[j] + (i == j ? sx + dreg : 0.0);
   p = gx + ph;
   double ea[4];
   bcast4(e, ea);
@@ -191,12 +214,12 @@ MPCQP_QD bool riccati_q(const W& at, const StageQ& S, int k, int i, double (&Ph)
   for (int j = 0; j < 4; ++j) {
     double s = 0.0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s = fma(at(k, L::DA + q * NX + i), PAa[q][j], s);
+    for (int q = 0; q < 4; ++q) s = fma(at.r(k, L::DA + q * NX), PAa[q][j], s);
     Ph[j] = fma(Hxi[1], K[1][j], fma(Hxi[0], K[0][j], s));
   }
   double s = 0.0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) s = fma(at(k, L::DA + q * NX + i), Pea[q], s);
+  for (int q = 0; q < 4; ++q) s = fma(at.r(k, L::DA + q * NX), Pea[q], s);
   ph = fma(Hxi[1], kk[1], fma(Hxi[0], kk[0], s));
   return ok;
 }
@@ -208,12 +231,12 @@ MPCQP_QD void store_factor_q(const W& at, int k, int i, const double (&P)[4], do
                              double e) {
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    if (j <= i) at(k, L::PP + pk(i, j)) = P[j];
+    if (j <= i) at.p(k, L::PP, j) = P[j];
 #pragma unroll
-  for (int r = 0; r < 2; ++r) at(k, L::KM + r * NX + i) = sel4(K[r], i);
-  at(k, L::E + i) = e;
-  at(k, L::PV + i) = p;
-  if (i < 2) at(k, L::KV + i) = sel2(kk, i);
+  for (int r = 0; r < 2; ++r) at.r(k, L::KM + r * NX) = sel4(K[r], i);
+  at.r(k, L::E) = e;
+  at.r(k, L::PV) = p;
+  if (i < 2) at.r(k, L::KV) = sel2(kk, i);
   if (i == 0) {
     at(k, L::GI + 0) = Gi[0];
     at(k, L::GI + 1) = Gi[1];
@@ -230,9 +253,9 @@ MPCQP_QD void grad_q(const W& at, const StageQ& S, int k, int i, const double (&
                      const double (&x1a)[4],
                      const double (&pia)[4], const double (&ua)[2], double pii, double gx1,
                      double& gx, double (&gu)[2]) {
-  double s = gx1 - pii + at(k, L::QX + i);
+  double s = gx1 - pii + at.r(k, L::QX);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) s = fma(at(k, L::WXX + pk(i, q)), x1a[q], s);
+  for (int q = 0; q < 4; ++q) s = fma(at.p(k, L::WXX, q), x1a[q], s);
   gx = s;
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -254,9 +277,9 @@ MPCQP_QD double next_gx1_q(const W& at, const StageQ& S, int k, int i, const dou
                            const double (&ua)[2]) {
   double s = 0.0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) s = fma(at(k, L::DA + q * NX + i), pia[q], s);
+  for (int q = 0; q < 4; ++q) s = fma(at.r(k, L::DA + q * NX), pia[q], s);
 #pragma unroll
-  for (int r = 0; r < 2; ++r) s = fma(at(k, L::WXU + i * NU + r), ua[r], s);
+  for (int r = 0; r < 2; ++r) s = fma(at.rb(k, L::WXU + r), ua[r], s);
   return s;
 }
 
@@ -265,11 +288,11 @@ template <class W>
 MPCQP_QD double resid_q(const W& at, const StageQ& S, int k, int i, const double (&xa)[4],
                         const double (&ua)[2],
                         double x1i) {
-  double s = at(k, L::DC + i) - x1i;
+  double s = at.r(k, L::DC) - x1i;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) s = fma(at(k, L::DA + i * NX + j), xa[j], s);
+  for (int j = 0; j < 4; ++j) s = fma(at.ra(k, L::DA + j), xa[j], s);
 #pragma unroll
-  for (int r = 0; r < 2; ++r) s = fma(at(k, L::DB + i * NU + r), ua[r], s);
+  for (int r = 0; r < 2; ++r) s = fma(at.rb(k, L::DB + r), ua[r], s);
   return s;
 }
 
@@ -288,11 +311,11 @@ MPCQP_QD void forward_q(const W& at, int N, int i, Body&& body) {
       for (int j = 0; j < 4; ++j) s = fma(at(k, L::KM + r * NX + j), dx[j], s);
       du[r] = s;
     }
-    double s = at(k, L::E + i);
+    double s = at.r(k, L::E);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s = fma(at(k, L::DA + i * NX + j), dx[j], s);
+    for (int j = 0; j < 4; ++j) s = fma(at.ra(k, L::DA + j), dx[j], s);
 #pragma unroll
-    for (int r = 0; r < 2; ++r) s = fma(at(k, L::DB + i * NU + r), du[r], s);
+    for (int r = 0; r < 2; ++r) s = fma(at.rb(k, L::DB + r), du[r], s);
     double dxa[4];
     bcast4(s, dxa);
     body(k, du, s, dxa);
@@ -314,7 +337,7 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i) {
     for (int part = 0; part < 2; ++part) {
       if (part == 1 && !ou) continue;
       const int j = part == 0 ? NU + i : i;
-      const double vj = part == 0 ? at(k, L::X + i) : at(k, L::U + i);
+      const double vj = part == 0 ? at.r(k, L::X) : at.r(k, L::U);
       const double lo = at(k, L::LO + j), hi = at(k, L::HI + j);
       const double l = at(k, L::LL + j), u = at(k, L::LU + j);
       const double rl = fin(lo) ? l / (vj - lo) : 0.0;
@@ -322,10 +345,10 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i) {
       const double act = (ru > 1.0 && ru >= rl) ? 1.0 : ((rl > 1.0) ? -1.0 : 0.0);
       at(k, L::GA + j) = act;
       const double y = act > 0.0 ? u : (act < 0.0 ? -l : 0.0);
-      if (part == 1) { at(k, L::DU + i) = vj; at(k, L::DUA + i) = y; }
-      else { at(k, L::DX + i) = vj; at(k, L::DXA + i) = y; }
+      if (part == 1) { at.r(k, L::DU) = vj; at.r(k, L::DUA) = y; }
+      else { at.r(k, L::DX) = vj; at.r(k, L::DXA) = y; }
     }
-    at(k, L::DPI + i) = at(k, L::PI + i);
+    at.r(k, L::DPI) = at.r(k, L::PI);
   }
   constexpr int kSteps = 4, kRounds = 4;
   for (int round = 0; round < kRounds; ++round) {
@@ -334,9 +357,9 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i) {
       const double rho = step == 0 ? 1e8 : (step == 1 ? 1e6 : 1e4);
       double Ph[4] = {0.0, 0.0, 0.0, 0.0}, ph = 0.0, gx1 = 0.0;
       for (int k = N - 1; k >= 0; --k) {
-        const double xi = at(k, L::DX + i), pii = at(k, L::DPI + i);
-        const double ui = ou ? at(k, L::DU + i) : 0.0;
-        const double xki = k == 0 ? x0i : at(k - 1, L::DX + i);
+        const double xi = at.r(k, L::DX), pii = at.r(k, L::DPI);
+        const double ui = ou ? at.r(k, L::DU) : 0.0;
+        const double xki = k == 0 ? x0i : at.r(k - 1, L::DX);
         double xa[4], x1a[4], pia[4], ua[2];
         bcast4(xki, xa);
         bcast4(xi, x1a);
@@ -356,16 +379,16 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i) {
           if (act != 0.0) {
             const double bnd = act > 0.0 ? at(k, L::HI + j) : at(k, L::LO + j);
             sx = rho;
-            gx += at(k, L::DXA + i) + rho * (xi - bnd);
+            gx += at.r(k, L::DXA) + rho * (xi - bnd);
           }
         }
         double gum = 0.0;
         if (ou) {
-          const double act = at(k, L::GA + i);
+          const double act = at.r(k, L::GA);
           if (act != 0.0) {
-            const double bnd = act > 0.0 ? at(k, L::HI + i) : at(k, L::LO + i);
+            const double bnd = act > 0.0 ? at.r(k, L::HI) : at.r(k, L::LO);
             sui = rho;
-            gum = at(k, L::DUA + i) + rho * (ui - bnd);
+            gum = at.r(k, L::DUA) + rho * (ui - bnd);
           }
         }
         double su2[2] = {qb<0>(sui), qb<1>(sui)};
@@ -378,21 +401,21 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i) {
       }
       const bool last = step == kSteps - 1;
       forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&dxa)[4]) {
-        double s = at(k, L::PV + i);
+        double s = at.r(k, L::PV);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) s = fma(at(k, L::PP + pk(i, j)), dxa[j], s);
-        at(k, L::DPI + i) += s;
+        for (int j = 0; j < 4; ++j) s = fma(at.p(k, L::PP, j), dxa[j], s);
+        at.r(k, L::DPI) += s;
 #pragma unroll
         for (int part = 0; part < 2; ++part) {
           if (part == 1 && !ou) continue;
           const int j = part == 0 ? NU + i : i;
-          double& vr = part == 0 ? at(k, L::DX + i) : at(k, L::DU + i);
+          double& vr = part == 0 ? at.r(k, L::DX) : at.r(k, L::DU);
           const double vj = vr + (part == 0 ? dxn : sel2(du, i));
           vr = vj;
           const double lo = at(k, L::LO + j), hi = at(k, L::HI + j);
           const double act = at(k, L::GA + j);
           if (act != 0.0) {
-            double& yr = part == 0 ? at(k, L::DXA + i) : at(k, L::DUA + i);
+            double& yr = part == 0 ? at.r(k, L::DXA) : at.r(k, L::DUA);
             const double bnd = act > 0.0 ? hi : lo;
             const double y = yr + rho * (vj - bnd);
             yr = y;
@@ -430,20 +453,20 @@ MPCQP_QD void emit_q(const Args<T>& a, int b, const W& at, int i, bool polished,
   const int N = a.N, nx = a.nx, nu = a.nu;
   for (int k = 0; k < N; ++k) {
     if (i < nu) {
-      a.z[(int64_t)b * N * nu + (int64_t)k * nu + i] = (T)at(k, (polished ? L::DU : L::U) + i);
+      a.z[(int64_t)b * N * nu + (int64_t)k * nu + i] = (T)at.r(k, polished ? L::DU : L::U);
       if (a.lam_u)
         a.lam_u[(int64_t)b * N * nu + (int64_t)k * nu + i] =
-            (T)(polished ? at(k, L::DUA + i) : at(k, L::LU + i) - at(k, L::LL + i));
+            (T)(polished ? at.r(k, L::DUA) : at.r(k, L::LU) - at.r(k, L::LL));
     }
     if (i < nx) {
       if (a.X)
-        a.X[(int64_t)b * N * nx + (int64_t)k * nx + i] = (T)at(k, (polished ? L::DX : L::X) + i);
+        a.X[(int64_t)b * N * nx + (int64_t)k * nx + i] = (T)at.r(k, polished ? L::DX : L::X);
       if (a.pi)
         a.pi[(int64_t)b * N * nx + (int64_t)k * nx + i] =
-            (T)at(k, (polished ? L::DPI : L::PI) + i);
+            (T)at.r(k, polished ? L::DPI : L::PI);
       if (a.y)
         a.y[(int64_t)b * N * nx + (int64_t)k * nx + i] =
-            (T)(polished ? at(k, L::DXA + i) : at(k, L::LU + NU + i) - at(k, L::LL + NU + i));
+            (T)(polished ? at.r(k, L::DXA) : at.r(k, L::LU + NU) - at.r(k, L::LL + NU));
     }
   }
   if (i == 0) a.status[b] = code | ((it & 0xFFFF) << 8) | (polished ? (1 << 24) : 0);
@@ -453,8 +476,8 @@ MPCQP_QD void emit_q(const Args<T>& a, int b, const W& at, int i, bool polished,
 // (LD instances interleaved).  Requires nx <= 4, nu <= 2.
 template <typename T, int LD>
 MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
-  const Ws<L::F, LD> at{W};
   const int i = (int)(threadIdx.x & 3);
+  const WsQ<LD> at(W, i);
   const bool ou = i < NU;
   const int N = a.N, nx = a.nx, nu = a.nu;
   if (a.skip && (a.skip[b] & a.skip_mask)) return;
@@ -471,34 +494,34 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
       // bounds of the lane's components (ipm::load_bounds order: u then x)
       double lo[L::NB], hi[L::NB];
       ipm::load_bounds<T, NX, NU>(a, b, k, lo, hi);
-      at(k, L::LO + NU + i) = sel4({lo[2], lo[3], lo[4], lo[5]}, i);
-      at(k, L::HI + NU + i) = sel4({hi[2], hi[3], hi[4], hi[5]}, i);
+      at.r(k, L::LO + NU) = sel4({lo[2], lo[3], lo[4], lo[5]}, i);
+      at.r(k, L::HI + NU) = sel4({hi[2], hi[3], hi[4], hi[5]}, i);
       if (ou) {
-        at(k, L::LO + i) = sel2({lo[0], lo[1]}, i);
-        at(k, L::HI + i) = sel2({hi[0], hi[1]}, i);
+        at.r(k, L::LO) = sel2({lo[0], lo[1]}, i);
+        at.r(k, L::HI) = sel2({hi[0], hi[1]}, i);
       }
       // stage data, row i (A, B, c, the x_{k+1} cost, the coupling H2xu)
       const bool term = (k == N - 1);
       const double ci = (ck && i < nx) ? (double)ck[i] : 0.0;
-      at(k, L::DC + i) = ci;
+      at.r(k, L::DC) = ci;
 #pragma unroll
       for (int j = 0; j < NX; ++j)
-        at(k, L::DA + i * NX + j) = (i < nx && j < nx) ? (double)Ak[i * nx + j] : 0.0;
+        at.ra(k, L::DA + j) = (i < nx && j < nx) ? (double)Ak[i * nx + j] : 0.0;
 #pragma unroll
       for (int r = 0; r < NU; ++r) {
-        at(k, L::DB + i * NU + r) = (i < nx && r < nu) ? (double)Bk[i * nu + r] : 0.0;
-        at(k, L::WXU + i * NU + r) = ipm::h2xu(a, b, k, i, r);
+        at.rb(k, L::DB + r) = (i < nx && r < nu) ? (double)Bk[i * nu + r] : 0.0;
+        at.rb(k, L::WXU + r) = ipm::h2xu(a, b, k, i, r);
       }
 #pragma unroll
       for (int j = 0; j < NX; ++j)
         if (j <= i)
-          at(k, L::WXX + pk(i, j)) = ipm::wq(a, b, term, i, j) + ipm::h2xx(a, b, k + 1, i, j);
-      at(k, L::QX + i) = ipm::q2x(a, b, k + 1, i);
+          at.p(k, L::WXX, j) = ipm::wq(a, b, term, i, j) + ipm::h2xx(a, b, k + 1, i, j);
+      at.r(k, L::QX) = ipm::q2x(a, b, k + 1, i);
       if (ou) {
 #pragma unroll
         for (int q = 0; q < NU; ++q)
           if (q <= i) at(k, L::WUU + pk(i, q)) = ipm::wr(a, b, i, q) + ipm::h2uu(a, b, k, i, q);
-        at(k, L::QU + i) = ipm::q2u(a, b, k, i);
+        at.r(k, L::QU) = ipm::q2u(a, b, k, i);
       }
       // start point: inputs inside their box, states rolled out and pushed
       // inside theirs, pi = 0, duals = 1
@@ -506,8 +529,8 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
       if (ou) {
         const double u0 =
             (a.U0 && i < nu) ? (double)a.U0[(int64_t)b * a.sU0 + (int64_t)k * nu + i] : 0.0;
-        ui = interior(u0, at(k, L::LO + i), at(k, L::HI + i));
-        at(k, L::U + i) = ui;
+        ui = interior(u0, at.r(k, L::LO), at.r(k, L::HI));
+        at.r(k, L::U) = ui;
       }
       double xa[4], ua[2];
       bcast4(xi, xa);
@@ -515,20 +538,20 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
       ua[1] = qb<1>(ui);
       double s = ci;
 #pragma unroll
-      for (int j = 0; j < NX; ++j) s = fma(at(k, L::DA + i * NX + j), xa[j], s);
+      for (int j = 0; j < NX; ++j) s = fma(at.ra(k, L::DA + j), xa[j], s);
 #pragma unroll
-      for (int r = 0; r < NU; ++r) s = fma(at(k, L::DB + i * NU + r), ua[r], s);
-      const double lox = at(k, L::LO + NU + i), hix = at(k, L::HI + NU + i);
+      for (int r = 0; r < NU; ++r) s = fma(at.rb(k, L::DB + r), ua[r], s);
+      const double lox = at.r(k, L::LO + NU), hix = at.r(k, L::HI + NU);
       xi = interior(s, lox, hix);
-      at(k, L::X + i) = xi;
-      at(k, L::PI + i) = 0.0;
-      at(k, L::LL + NU + i) = fin(lox) ? 1.0 : 0.0;
-      at(k, L::LU + NU + i) = fin(hix) ? 1.0 : 0.0;
+      at.r(k, L::X) = xi;
+      at.r(k, L::PI) = 0.0;
+      at.r(k, L::LL + NU) = fin(lox) ? 1.0 : 0.0;
+      at.r(k, L::LU + NU) = fin(hix) ? 1.0 : 0.0;
       mc += (fin(lox) ? 1.0 : 0.0) + (fin(hix) ? 1.0 : 0.0);
       if (ou) {
-        const double lou = at(k, L::LO + i), hiu = at(k, L::HI + i);
-        at(k, L::LL + i) = fin(lou) ? 1.0 : 0.0;
-        at(k, L::LU + i) = fin(hiu) ? 1.0 : 0.0;
+        const double lou = at.r(k, L::LO), hiu = at.r(k, L::HI);
+        at.r(k, L::LL) = fin(lou) ? 1.0 : 0.0;
+        at.r(k, L::LU) = fin(hiu) ? 1.0 : 0.0;
         mc += (fin(lou) ? 1.0 : 0.0) + (fin(hiu) ? 1.0 : 0.0);
       }
     }
@@ -546,14 +569,14 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
     double rstat = 0.0, rdyn = 0.0, musum = 0.0;
     bool pd = true;
     for (int k = N - 1; k >= 0; --k) {
-      double xi = at(k, L::X + i), pii = at(k, L::PI + i);
-      double llx = at(k, L::LL + NU + i), lux = at(k, L::LU + NU + i);
+      double xi = at.r(k, L::X), pii = at.r(k, L::PI);
+      double llx = at.r(k, L::LL + NU), lux = at.r(k, L::LU + NU);
       double ui = 0.0, llu = 0.0, luu = 0.0;
-      if (ou) { ui = at(k, L::U + i); llu = at(k, L::LL + i); luu = at(k, L::LU + i); }
-      const double lox = at(k, L::LO + NU + i), hix = at(k, L::HI + NU + i);
-      const double lou = ou ? at(k, L::LO + i) : -kInf, hiu = ou ? at(k, L::HI + i) : kInf;
-      double xki = k == 0 ? x0i : at(k - 1, L::X + i);
-      if (alpha > 0.0 && k > 0) xki += alpha * at(k - 1, L::DX + i);
+      if (ou) { ui = at.r(k, L::U); llu = at.r(k, L::LL); luu = at.r(k, L::LU); }
+      const double lox = at.r(k, L::LO + NU), hix = at.r(k, L::HI + NU);
+      const double lou = ou ? at.r(k, L::LO) : -kInf, hiu = ou ? at.r(k, L::HI) : kInf;
+      double xki = k == 0 ? x0i : at.r(k - 1, L::X);
+      if (alpha > 0.0 && k > 0) xki += alpha * at.r(k - 1, L::DX);
       if (alpha > 0.0) {  // apply the corrector step of the previous iteration
         auto apply = [&](double& v, double& ll, double& lu, double lo, double hi, double dv,
                          double dva) {
@@ -571,14 +594,14 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
           }
           v += alpha * dv;
         };
-        apply(xi, llx, lux, lox, hix, at(k, L::DX + i), at(k, L::DXA + i));
-        if (ou) apply(ui, llu, luu, lou, hiu, at(k, L::DU + i), at(k, L::DUA + i));
-        pii += alpha * at(k, L::DPI + i);
-        at(k, L::X + i) = xi;
-        at(k, L::PI + i) = pii;
-        at(k, L::LL + NU + i) = llx;
-        at(k, L::LU + NU + i) = lux;
-        if (ou) { at(k, L::U + i) = ui; at(k, L::LL + i) = llu; at(k, L::LU + i) = luu; }
+        apply(xi, llx, lux, lox, hix, at.r(k, L::DX), at.r(k, L::DXA));
+        if (ou) apply(ui, llu, luu, lou, hiu, at.r(k, L::DU), at.r(k, L::DUA));
+        pii += alpha * at.r(k, L::DPI);
+        at.r(k, L::X) = xi;
+        at.r(k, L::PI) = pii;
+        at.r(k, L::LL + NU) = llx;
+        at.r(k, L::LU + NU) = lux;
+        if (ou) { at.r(k, L::U) = ui; at.r(k, L::LL) = llu; at.r(k, L::LU) = luu; }
       }
       double xa[4], x1a[4], pia[4], ua[2];
       bcast4(xki, xa);
@@ -599,7 +622,7 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
         if (fin(lox)) { const double sl = xi - lox; sx += llx / sl; musum += sl * llx; r -= llx; }
         if (fin(hix)) { const double su = hix - xi; sx += lux / su; musum += su * lux; r += lux; }
         rstat = fmax(rstat, fabs(r));
-        at(k, L::GA + NU + i) = gx;
+        at.r(k, L::GA + NU) = gx;
       }
       if (ou) {
         const double gui = sel2(gu, i);
@@ -607,7 +630,7 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
         if (fin(lou)) { const double sl = ui - lou; sui += llu / sl; musum += sl * llu; r -= llu; }
         if (fin(hiu)) { const double su = hiu - ui; sui += luu / su; musum += su * luu; r += luu; }
         rstat = fmax(rstat, fabs(r));
-        at(k, L::GA + i) = gui;
+        at.r(k, L::GA) = gui;
       }
       const double su2[2] = {qb<0>(sui), qb<1>(sui)};
       double P[4], p, K[2][4], kk[2], Gi[3];
@@ -659,8 +682,8 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
     // ========================================== pass 2: forward predictor
     double amax = 1.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
     forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&)[4]) {
-      at(k, L::DXA + i) = dxn;
-      if (ou) at(k, L::DUA + i) = sel2(du, i);
+      at.r(k, L::DXA) = dxn;
+      if (ou) at.r(k, L::DUA) = sel2(du, i);
       auto comp = [&](double vj, double dv, double lo, double hi, double l, double lu) {
         if (fin(lo)) {
           const double sl = vj - lo;
@@ -681,11 +704,11 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
           c2 -= dv * dl;
         }
       };
-      comp(at(k, L::X + i), dxn, at(k, L::LO + NU + i), at(k, L::HI + NU + i),
-           at(k, L::LL + NU + i), at(k, L::LU + NU + i));
+      comp(at.r(k, L::X), dxn, at.r(k, L::LO + NU), at.r(k, L::HI + NU),
+           at.r(k, L::LL + NU), at.r(k, L::LU + NU));
       if (ou)
-        comp(at(k, L::U + i), sel2(du, i), at(k, L::LO + i), at(k, L::HI + i), at(k, L::LL + i),
-             at(k, L::LU + i));
+        comp(at.r(k, L::U), sel2(du, i), at.r(k, L::LO), at.r(k, L::HI), at.r(k, L::LL),
+             at.r(k, L::LU));
     });
     amax = qmin(amax);
     if (mcount > 0.0) {
@@ -713,18 +736,18 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
           }
           return s;
         };
-        const double gx = rhs(at(k, L::X + i), at(k, L::DXA + i), at(k, L::LO + NU + i),
-                              at(k, L::HI + NU + i), at(k, L::LL + NU + i),
-                              at(k, L::LU + NU + i), at(k, L::GA + NU + i));
-        const double gum = ou ? rhs(at(k, L::U + i), at(k, L::DUA + i), at(k, L::LO + i),
-                                    at(k, L::HI + i), at(k, L::LL + i), at(k, L::LU + i),
-                                    at(k, L::GA + i))
+        const double gx = rhs(at.r(k, L::X), at.r(k, L::DXA), at.r(k, L::LO + NU),
+                              at.r(k, L::HI + NU), at.r(k, L::LL + NU),
+                              at.r(k, L::LU + NU), at.r(k, L::GA + NU));
+        const double gum = ou ? rhs(at.r(k, L::U), at.r(k, L::DUA), at.r(k, L::LO),
+                                    at.r(k, L::HI), at.r(k, L::LL), at.r(k, L::LU),
+                                    at.r(k, L::GA))
                               : 0.0;
         const double gu[2] = {qb<0>(gum), qb<1>(gum)};
         const double p = gx + phc;
         double Pe = p;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Pe = fma(at(k, L::PP + pk(i, j)), at(k, L::E + j), Pe);
+        for (int j = 0; j < 4; ++j) Pe = fma(at.p(k, L::PP, j), at(k, L::E + j), Pe);
         double Pea[4];
         bcast4(Pe, Pea);
         double h[2];
@@ -739,27 +762,27 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
         double kk[2];
 #pragma unroll
         for (int r = 0; r < 2; ++r) kk[r] = -(Gi[pk(r, 0)] * h[0] + Gi[pk(r, 1)] * h[1]);
-        if (ou) at(k, L::KV + i) = sel2(kk, i);
+        if (ou) at.r(k, L::KV) = sel2(kk, i);
         // ph = A'Pe + K'h
         double s = 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s = fma(at(k, L::DA + q * NX + i), Pea[q], s);
+        for (int q = 0; q < 4; ++q) s = fma(at.r(k, L::DA + q * NX), Pea[q], s);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) s = fma(at(k, L::KM + r * NX + i), h[r], s);
+        for (int r = 0; r < 2; ++r) s = fma(at.r(k, L::KM + r * NX), h[r], s);
         phc = s;
-        at(k, L::PV + i) = p;
+        at.r(k, L::PV) = p;
       }
     }
 
     // ========================================== pass 4: forward corrector
     amax = 1.0;
     forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&dxa)[4]) {
-      double s = at(k, L::PV + i);
+      double s = at.r(k, L::PV);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) s = fma(at(k, L::PP + pk(i, j)), dxa[j], s);
-      at(k, L::DPI + i) = s;
-      at(k, L::DX + i) = dxn;
-      if (ou) at(k, L::DU + i) = sel2(du, i);
+      for (int j = 0; j < 4; ++j) s = fma(at.p(k, L::PP, j), dxa[j], s);
+      at.r(k, L::DPI) = s;
+      at.r(k, L::DX) = dxn;
+      if (ou) at.r(k, L::DU) = sel2(du, i);
       auto comp = [&](double vj, double dv, double dva, double lo, double hi, double l,
                       double lu) {
         if (fin(lo)) {
@@ -777,11 +800,11 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
           if (dl < 0.0) amax = fmin(amax, -lu / dl);
         }
       };
-      comp(at(k, L::X + i), dxn, at(k, L::DXA + i), at(k, L::LO + NU + i), at(k, L::HI + NU + i),
-           at(k, L::LL + NU + i), at(k, L::LU + NU + i));
+      comp(at.r(k, L::X), dxn, at.r(k, L::DXA), at.r(k, L::LO + NU), at.r(k, L::HI + NU),
+           at.r(k, L::LL + NU), at.r(k, L::LU + NU));
       if (ou)
-        comp(at(k, L::U + i), sel2(du, i), at(k, L::DUA + i), at(k, L::LO + i), at(k, L::HI + i),
-             at(k, L::LL + i), at(k, L::LU + i));
+        comp(at.r(k, L::U), sel2(du, i), at.r(k, L::DUA), at.r(k, L::LO), at.r(k, L::HI),
+             at.r(k, L::LL), at.r(k, L::LU));
     });
     alpha = fmin(1.0, 0.995 * qmin(amax));
   }
