@@ -87,6 +87,11 @@ extern "C" {
 
 /* status bit 24: the solution was polished to the exact active-set vertex */
 #define MPCQP_STATUS_POLISHED (1 << 24)
+/* status bit 25 (mpcqp_mpc_qp, fp32): more than 64 active constraints sent the
+   instance to the workgroup kernel, which solves the fp32 condensed QP without
+   the refinement against the dynamics -- z is at the fp32 condensing floor
+   (~1e-5 relative) instead of the fp64 solution of the step */
+#define MPCQP_STATUS_UNREFINED (1 << 25)
 
 int mpcqp_abi_version(void);
 const char* mpcqp_last_error(void);

@@ -21,6 +21,7 @@ TV = 1
 IPM = 2
 STRICT = 4
 STATUS_POLISHED = 1 << 24
+STATUS_UNREFINED = 1 << 25
 SQP_DONE = 1
 SQP_EXACT = 2
 MODEL_FE = 0

@@ -318,6 +318,18 @@ static int pf_refine() {
 // fp32, n + m > 64: sweep (MFMA) -> product-form active set, one instance per
 // wavefront -> qp_wg_kernel for the instances with more than 64 active
 // constraints (none at configs 3 and 5).
+//
+// With the dynamics refinement (mpcqp_mpc_qp), an instance handed off this
+// way is solved on the fp32 condensed data without it: its status carries
+// MPCQP_STATUS_UNREFINED so that the caller sees the fp32 condensing floor.
+__global__ void flag_unrefined_kernel(const int* cnt, const int* list, int32_t* status) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < *cnt) {
+    int32_t* s = status + list[j];
+    *s = *s | MPCQP_STATUS_UNREFINED;
+  }
+}
+
 int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const void* f,
                      int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
                      int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
@@ -339,8 +351,13 @@ int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const v
                  sUb, M0, s0, (float*)z, (float*)y, status, cnt, list, mi,
                  refine >= 0 ? refine : pf_refine(), tl, st, dyn);
   if (rc != MPCQP_OK) return rc;
-  return solve_qp_t<float>(batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, z, y,
-                           status, max_iter, tol, st, M0, cnt, list);
+  rc = solve_qp_t<float>(batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, z, y,
+                         status, max_iter, tol, st, M0, cnt, list);
+  if (rc != MPCQP_OK || !dyn) return rc;
+  hipLaunchKernelGGL(flag_unrefined_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0,
+                     st, cnt, list, status);
+  MPCQP_CHECK_LAUNCH("flag_unrefined_kernel");
+  return MPCQP_OK;
 }
 
 int max_qp_size_dtype(int dtype) {

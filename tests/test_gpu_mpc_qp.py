@@ -261,3 +261,34 @@ def test_mpc_qp_f32_near_active_bound_stays_optimal(dev):
         zr = oq.poly_qp(d["H"], d["f"], G, h, r(pb["lb"]), r(pb["ub"]))[0]
         err = max(err, float(np.abs(z[i].double().cpu().numpy() - zr).max()))
     assert err < TOL_F32, err
+
+
+def test_mpc_qp_handoff_flags_unrefined(dev):
+    """more than 64 active constraints send an fp32 instance of the
+    refined path to the workgroup kernel, which solves the fp32 condensed QP
+    without the refinement against the dynamics -- its status carries
+    STATUS_UNREFINED (code still OPTIMAL); an instance with few active bounds
+    in the same batch keeps the refined path and no flag.  Plant: nx = 1,
+    nu = 2, N = 60 (n = 120 inputs, m = 60 state rows), |u| <= 1e-3."""
+    from model_predictive_control_amd import _native as nat
+
+    N = 60
+    t = lambda a: torch.as_tensor(np.asarray(a, float), dtype=torch.float32, device=dev)  # noqa: E731
+    A, B = t([[0.9]]), t([[1.0, 1.0]])
+    Q, R = t([[1.0]]), t(np.eye(2))
+    X0 = t([[5.0], [0.0]])
+    z, y, st = batched.mpc_qp(A, B, Q, R, Q, N, X0, xlo=t([-100.0]), xhi=t([100.0]),
+                              lb=-1e-3, ub=1e-3)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert (st & 0xFF == 0).all(), st
+    assert st[0] & nat.STATUS_UNREFINED and not st[1] & nat.STATUS_UNREFINED, st
+    zn = z.cpu().numpy()
+    # accuracy of the flagged instance: the fp32 condensed QP's, against the
+    # fp64 oracle (the state box is not active)
+    d = oc.condense(np.array([[0.9]]), np.array([[1.0, 1.0]]), np.eye(1), np.eye(2), np.eye(1),
+                    N, x0=np.array([5.0]))
+    zr = oq.box_qp(d["H"], d["f"], -1e-3, 1e-3)[0]
+    assert (np.abs(zr) > 1e-3 - 1e-12).sum() > 64       # the hand-off case: > 64 active
+    assert np.abs(zn[0] - zr).max() < 1e-4
+    assert np.abs(zn[1]).max() < 1e-9                   # x0 = 0: z = 0
