@@ -490,8 +490,7 @@ class Config3:
         """fp64 oracle (explicit condensing + Goldfarb-Idnani) on a few
         instances of slot 0, from the same fp32-valued (A_k, B_k, c_k, x0,
         weights, bounds) the device saw."""
-        from oracle import condense as oc
-        from oracle import qp as oq
+        from oracle import parallel
 
         N = self.N
         r = lambda t: t.double().cpu().numpy()  # noqa: E731
@@ -501,13 +500,11 @@ class Config3:
         xlo, xhi, lb, ub = r(self.xmin_t), r(self.xmax_t), r(self.lbz), r(self.ubz)
         Z = self.Z[0].double().cpu().numpy()
         code = batched.status_code(self.ST[0]).cpu().numpy()
-        for i in range(min(self.args.check, self.args.batch)):
-            d = oc.condense(A[i], B[i], Q, Rm, QN, N, x0=X0[i], c=c[i])
-            G = np.vstack([d["Gam"], -d["Gam"]])
-            h = np.concatenate([xhi - d["xbar"], -(xlo - d["xbar"])])
-            try:
-                zr = oq.poly_qp(d["H"], d["f"], G, h, lb, ub)[0]
-            except ValueError:
+        nchk = min(self.args.check, self.args.batch)
+        sols = parallel.solve_map(parallel.cfg3_solve, lambda lo, hi: (
+            A[lo:hi], B[lo:hi], c[lo:hi], X0[lo:hi], Q, Rm, QN, N, xlo, xhi, lb, ub), nchk)
+        for i, zr in enumerate(sols):
+            if zr is None:
                 assert code[i] == 3
                 continue
             errs.append(np.abs(Z[i] - zr).max())
@@ -588,22 +585,27 @@ class Config4:
         bsz, n, m, nx = self.args.batch, self.n, self.m, self.nx
         t_s = time_kernel(lambda: self._solve(0), R, self.dev)
         sb = (nx + n + m) * 8 * bsz + 4 * bsz      # x0 in; z, y, status out
-        r_s = roof("dual_range_kernel<double,5> (fused s0 / z epilogue)", "hbm", sb, t_s,
-                   HBM_PEAK_GBS, "GB/s", traffic.get("poly_solve"), {"bytes_per_launch": sb})
+        # SURVEY.md 8(d), config 4 per instance: f = F x0 4.8 kflop, h(x0) ~1
+        # kflop, the dual active set on the shared 40 x 40 M and the primal
+        # recovery ~21 kflop.  96 B in / 1.6 KB out per instance is far below
+        # the HBM roof: the kernel is fp64 VALU issue/latency bound
+        fl = 26_800 * bsz
+        r_s = roof("dual_range_kernel<double,5> (fused s0 / z epilogue)", "valu-fp64", fl, t_s,
+                   FP64_PEAK_TFS, "TFLOP/s", traffic.get("poly_solve"),
+                   {"flops_per_launch": fl, "hbm_bytes_per_launch": sb})
         extra = {"kernel_us": {"poly_solve": round(t_s * 1e3, 2)}}
         return r_s, {}, extra
 
     def check(self):
         from oracle import condense as oc
-        from oracle import qp as oq
+        from oracle import parallel
 
         d = oc.condense(self.A, self.B, self.Qn, self.Rn, self.Qn, self.N)
         Z = self.Z[0].cpu().numpy()
-        errs = []
-        for i in range(min(4, self.args.batch)):
-            zr = oq.poly_qp(d["H"], d["F"] @ self.X0[0, i], self.G, self.h)[0]
-            errs.append(np.abs(Z[i] - zr).max())
-        return float(max(errs))
+        nchk = min(self.args.check, self.args.batch)
+        sols = parallel.solve_map(parallel.cfg4_solve, lambda lo, hi: (
+            d["H"], d["F"], self.G, self.h, self.X0[0, lo:hi]), nchk)
+        return float(max(np.abs(Z[i] - zr).max() for i, zr in enumerate(sols)))
 
     def cpu_baseline(self, seconds):
         from oracle import condense as oc
@@ -711,20 +713,17 @@ class Config5:
         return rs[0][1], {"roofline_other": [r for _, r in rs[1:]]}, extra
 
     def check(self):
-        from oracle import condense as oc
-        from oracle import qp as oq
+        from oracle import parallel
 
         N = self.N
         A, B = self.A[0].double().cpu().numpy(), self.B[0].double().cpu().numpy()
         X0 = self.X0_t[0].double().cpu().numpy()
         Q, Rm = self.Q_t.double().cpu().numpy(), self.R_t.double().cpu().numpy()
         Z = self.Z[0].double().cpu().numpy()
-        errs = []
-        for i in range(min(self.args.check, self.args.batch)):
-            d = oc.condense(A[i], B[i], Q, Rm, Q, N, x0=X0[i])
-            zr = oq.box_qp(d["H"], d["f"], np.full(self.n, self.lb), np.full(self.n, self.ub))[0]
-            errs.append(np.abs(Z[i] - zr).max())
-        return float(max(errs))
+        nchk = min(self.args.check, self.args.batch)
+        sols = parallel.solve_map(parallel.cfg5_solve, lambda lo, hi: (
+            A[lo:hi], B[lo:hi], X0[lo:hi], Q, Rm, N, self.lb, self.ub), nchk)
+        return float(max(np.abs(Z[i] - zr).max() for i, zr in enumerate(sols)))
 
     def cpu_baseline(self, seconds):
         from oracle import parallel
@@ -982,7 +981,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--reps", type=int, default=20, help="launches per kernel-timing graph")
-    ap.add_argument("--check", type=int, default=16, help="instances checked against the oracle")
+    ap.add_argument("--check", type=int, default=64, help="instances checked against the oracle")
     ap.add_argument("--mode", choices=("fused", "split"), default="fused", help="config 2 only")
     ap.add_argument("--traffic", default=None,
                     help="JSON with PMC-measured HBM bytes per launch {kernel: bytes} "

@@ -15,6 +15,10 @@
 #pragma once
 #include "sym2d.hpp"
 
+#ifndef MPCQP_SCAN_AHEAD
+#define MPCQP_SCAN_AHEAD 1
+#endif
+
 namespace mpcqp {
 
 // Max over the 4 row blocks of a group (lanes differing in bits 2..3),
@@ -358,11 +362,26 @@ __device__ __forceinline__ int gi_box_st(Mat& M, T* gb, const T* fs, const T* lb
     bool need_p = true;
     int p = 0, side = 1;
     T tgt = T(0), zp = T(0), gp = T(0);
+#if MPCQP_SCAN_AHEAD
+    T a_viol = T(0), a_zv = T(0);
+    int a_pi = 0;
+    bool have_scan = false;
+#endif
     while (true) {
       if (__any(active && need_p)) {
         T viol, zv;
         int pi;
+#if MPCQP_SCAN_AHEAD
+        if (have_scan) {
+          viol = a_viol;
+          pi = a_pi;
+          zv = a_zv;
+        } else {
+          qscan<T, BS>(M, st, zr, B, viol, pi, zv);
+        }
+#else
         qscan<T, BS>(M, st, zr, B, viol, pi, zv);
+#endif
         if (active && need_p) {
           if (!(viol > tol)) {
             active = false;  // settled (pending the exact re-check)
@@ -432,6 +451,35 @@ __device__ __forceinline__ int gi_box_st(Mat& M, T* gb, const T* fs, const T* lb
         for (int r = 0; r < NC; ++r) kcol[r] = cc[r];
       }
       const bool bad = stepping && (partial ? !(d > T(0)) : !(d < T(0)));
+#if MPCQP_SCAN_AHEAD
+      // the state changes first, then the next pivot's scan: it reads only z
+      // and the states, so its arg-max chain runs ahead of (and can overlap)
+      // the sweep; used when the step was full (need_p)
+      if (stepping && !bad) {
+#pragma unroll
+        for (int r = 0; r < BS; ++r) {
+          const int i = M.bi * BS + r;
+          if (partial && i == k) {
+            st[r] = 0;
+            mu[r] = T(0);
+          }
+          if (!partial && i == p) {
+            st[r] = side;
+            zr[r] = tgt;
+            mu[r] = (side == 1) ? gp : -gp;
+          }
+        }
+        need_p = !partial;
+      }
+      if (bad) {
+        code = MPCQP_STATUS_NOT_CONVEX;
+        active = false;
+      }
+      qscan<T, BS>(M, st, zr, B, a_viol, a_pi, a_zv);
+      have_scan = true;
+      if (stepping && !bad) M.sweep_col(idx, sigma, d, kr, kcol);
+      MPCQP_PHASE(7);
+#else
       if (stepping && !bad) {
         M.sweep_col(idx, sigma, d, kr, kcol);
 #pragma unroll
@@ -454,6 +502,7 @@ __device__ __forceinline__ int gi_box_st(Mat& M, T* gb, const T* fs, const T* lb
         code = MPCQP_STATUS_NOT_CONVEX;
         active = false;
       }
+#endif
     }
     // exact refresh for every group, then re-check the bounds
     refresh();

@@ -90,6 +90,68 @@ def nlp_chunk(a):
     return done
 
 
+# -------------------------------------------- spot-check solves (bench check)
+def cfg3_solve(a):
+    """Oracle solutions of config-3 instances (None where infeasible)."""
+    from oracle import condense as oc
+    from oracle import qp as oq
+
+    A, B, c, X0, Q, R, QN, N, xlo, xhi, lb, ub = a
+    out = []
+    for i in range(A.shape[0]):
+        d = oc.condense(A[i], B[i], Q, R, QN, N, x0=X0[i], c=c[i])
+        G = np.vstack([d["Gam"], -d["Gam"]])
+        h = np.concatenate([xhi - d["xbar"], -(xlo - d["xbar"])])
+        try:
+            out.append(oq.poly_qp(d["H"], d["f"], G, h, lb, ub)[0])
+        except ValueError:
+            out.append(None)
+    return out
+
+
+def cfg4_solve(a):
+    from oracle import qp as oq
+
+    H, F, G, h, X0 = a
+    return [oq.poly_qp(H, F @ X0[i], G, h)[0] for i in range(X0.shape[0])]
+
+
+def cfg5_solve(a):
+    from oracle import condense as oc
+    from oracle import qp as oq
+
+    A, B, X0, Q, R, N, lo, hi = a
+    n = N * B.shape[-1]
+    out = []
+    for i in range(A.shape[0]):
+        d = oc.condense(A[i], B[i], Q, R, Q, N, x0=X0[i])
+        out.append(oq.box_qp(d["H"], d["f"], np.full(n, lo), np.full(n, hi))[0])
+    return out
+
+
+def solve_map(worker, make_args, total: int, cores: int | None = None) -> list:
+    """``worker`` over chunks [lo, hi) of ``total`` instances on ``cores``
+    spawned processes (one BLAS thread each); the per-instance results in
+    order."""
+    cores = min(cores or host_cores(), max(1, total))
+    ctx = mp.get_context("spawn")
+    saved = {k: os.environ.get(k) for k in _BLAS_ENV}
+    os.environ.update({k: "1" for k in _BLAS_ENV})
+    try:
+        pool = ctx.Pool(cores)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    per = -(-total // cores)
+    with pool:
+        parts = pool.map(worker, [make_args(k * per, min(total, (k + 1) * per))
+                                  for k in range(cores) if k * per < total])
+    return [x for part in parts for x in part]
+
+
 def rate(worker, make_args, total: int, seconds: float, cores: int | None = None) -> dict:
     """Run ``worker`` over ``cores`` spawned processes; ``make_args(lo, hi,
     deadline)`` builds the argument of the chunk [lo, hi) of ``total``
