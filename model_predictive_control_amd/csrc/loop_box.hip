@@ -128,6 +128,9 @@ __global__ __launch_bounds__(64, (LoopOcc<T, BS>::w)) void box_loop_kernel(LoopA
                         : (((__ballot(badbox) & gmask) != 0) ? MPCQP_STATUS_INFEASIBLE
                                                               : MPCQP_STATUS_OPTIMAL);
 
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
   QSym<T, BS> M;
   M.init(lane);
   int st[BS];
@@ -175,7 +178,8 @@ __global__ __launch_bounds__(64, (LoopOcc<T, BS>::w)) void box_loop_kernel(LoopA
     T zr[BS];
     int iters = 0;
     const int c2 = gi_box_st<T, BS, true>(M, gb, fs, lbs, ubs, n, a.max_iter, a.tol,
-                                          live && code == MPCQP_STATUS_OPTIMAL, zr, iters, st);
+                                          live && code == MPCQP_STATUS_OPTIMAL, zr, iters, st
+                                          MPCQP_CLK_ARG);
     if (code == MPCQP_STATUS_OPTIMAL) code = c2;
     const bool okc = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
     if (!okc) {

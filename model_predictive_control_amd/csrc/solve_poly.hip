@@ -59,8 +59,9 @@ struct DualArgs {
 // row-indexed vector (s0, bounds, scales, y, s, st) one row per lane (lane i =
 // row i, mt <= 64), so the scan and the ratio test run once per row instead
 // of once per row-block replica, with full-wave DPP arg-max / arg-min.
-// (218 VGPRs: 2 waves per SIMD.  Forcing 3 spills 212 B per lane and doubles
-// the time: measured 5.11 vs 2.73 ms at config 4.)
+// (152 VGPRs, 3 waves per SIMD, since the drop and the add share one sweep
+// call: with two sweep sites W lived in two register sets, 220 VGPRs and 2
+// waves per SIMD; config 4 poly_solve 2.72 -> 1.99 ms.)
 template <typename T, int BS>
 __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
   using S2 = Sym2D<T, BS>;
@@ -177,17 +178,26 @@ __global__ __launch_bounds__(64) void dual_range_kernel(DualArgs<T> a) {
           code = MPCQP_STATUS_INFEASIBLE;
           goto done;
         }
-        if (ti < t2) {
+        // one sweep call for both steps (its pivot column fetched for a
+        // drop, still in registers for an add): W stays in one register set
+        // across the loop (two sweep sites had the compiler copy all of W
+        // between two sets at the back edge)
+        const bool part = ti < t2;  // wave-uniform
+        int idx = p;
+        T sig = T(1), d = wpp;
+        if (part) {
           if (st == 1 || st == 2) yi = fma(ti, dy, yi);
           if (lane == k) {
             yi = T(0);
             st = 0;
           }
           if (!dep) sp = sp - wpp * ysgn * ti;
-          W.sweep(k, T(-1), buf);
-        } else {
-          // column p is still in registers (W unchanged since it was read)
-          W.sweep_col(p, T(1), wpp, c, cc);
+          idx = k;
+          sig = T(-1);
+          d = W.column(k, buf, c, cc);
+        }
+        W.sweep_col(idx, sig, d, c, cc);
+        if (!part) {
           if (!(wpp > T(0))) {
             code = MPCQP_STATUS_NOT_CONVEX;
             goto done;

@@ -10,7 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CS = os.environ.get("PT_CS", os.path.join(ROOT, "model_predictive_control_amd", "csrc"))
 LIB = os.path.join(ROOT, "model_predictive_control_amd", "lib", "libmpcqp_timing.so")
 SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.hip", "quad_box.hip",
-        "solve_qp.hip", "sweep.hip", "solve_pf.hip", "mpc_qp.hip", "bicycle.hip", "misc.hip"]
+        "solve_qp.hip", "sweep.hip", "solve_pf.hip", "mpc_qp.hip", "bicycle.hip", "misc.hip",
+        "ipm.hip", "sqp.hip", "loop_box.hip"]
 PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/recheck", "GI: scan+argmax", "GI: pivot col+ratio", "GI: sweep"]
 
 DYN = "--dyn" in sys.argv or (len(sys.argv) > 1 and sys.argv[1].startswith("dyn"))
@@ -67,7 +68,7 @@ elif cfg == 55:
     reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
     PHASES = ["backward W/What", "fw: loads+What", "fw: MFMA tiles", "fw: Gam/H epilogue", "fw: E tile", "", "", ""]
     a = A(); a.batch = 32768; a.slots = 1; a.horizon = 0; a.reps = 1
-    w = bench.CONFIGS[5](a, torch.device("cuda"), 0)
+    w = bench.CONFIGS["5"](a, torch.device("cuda"), 0)
     run = lambda: batched.condense(w.A[0], w.B[0], w.Q_t, w.R_t, w.Q_t, w.N, x0=w.X0_t[0],  # noqa: E731
                                    tv=True, outputs=("H", "f"))
     waves = a.batch * R
@@ -105,7 +106,7 @@ elif pf:
                   "DYN: residual tail", "correction (M0)", "re-scan", "output"]
     a = A(); a.batch = int(os.environ.get("PT_BATCH", 4096)); a.slots = 1; a.horizon = 0; a.reps = 1
     a.check = 0
-    w = bench.CONFIGS[cfg](a, torch.device("cuda"), 0)
+    w = bench.CONFIGS[str(cfg)](a, torch.device("cuda"), 0)
     run = lambda: w.step(0)  # noqa: E731
     waves = a.batch * R
 else:
@@ -113,7 +114,7 @@ else:
     PHASES = ["load K", "sweep-in z", "active set", "refinement", "", "", "", ""]
     a = A(); a.batch = 4096; a.slots = 1; a.horizon = 0; a.reps = 1
     a.check = 0
-    w = bench.CONFIGS[cfg](a, torch.device("cuda"), 0)
+    w = bench.CONFIGS[str(cfg)](a, torch.device("cuda"), 0)
     if cfg == 3:
         d = batched.condense(w.A[0], w.B[0], w.Q_t, w.R_t, w.QN_t, w.N, x0=w.X0_t[0], c=w.c[0],
                              tv=True, outputs=("H", "f", "Gam", "xbar"))
