@@ -818,9 +818,10 @@ class ConfigNLP:
         box = ctl._box()
         qp = {}
 
-        def ipm():
-            batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, lb=ctl.lbz, ub=ctl.ubz, c=c, tv=True,
-                            H2=H2, q2=q2, strict=True, max_iter=SqpSolver.QP_MAX_ITER, out=qp, **box)
+        def ipm():  # the outputs allocated once, then written in place
+            qp.update(batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, lb=ctl.lbz, ub=ctl.ubz,
+                                      c=c, tv=True, H2=H2, q2=q2, strict=True,
+                                      max_iter=SqpSolver.QP_MAX_ITER, out=qp or None, **box))
         t_i = time_kernel(ipm, R, self.dev)
         torch.cuda.synchronize()
         its = ((qp["status"] >> 8) & 0xFFFF).double()

@@ -97,7 +97,16 @@ template <typename T>
 static int ipm_quad_launch(ipm::Args<T>& a, hipStream_t st) {
   const int F = ipm::Layout<4, 2>::F;
   const size_t per = (size_t)a.N * F * sizeof(double);
-  const int G = per * 4 <= 160 * 1024 ? 4 : (per * 2 <= 160 * 1024 ? 2 : 1);
+  // One instance per single-wave workgroup: the CU's four SIMDs then each run
+  // a wave (four instances in one wave left three SIMDs idle, LDS allowing one
+  // such workgroup per CU).  Measured at the nlp line (N = 30, B = 4096, the
+  // SQP's strict QPs): 12.2 ms per interior-point launch against 15.0 ms
+  // (four per workgroup) and 13.4 ms (two).
+  int G = 1;
+  if (const char* env = getenv("MPCQP_IPM_G")) {  // A/B: instances per workgroup
+    const int g = atoi(env);
+    if ((g == 1 || g == 2 || g == 4) && (size_t)g * per <= 160 * 1024) G = g;
+  }
   const size_t bytes = (size_t)G * per;
   auto launch = [&](auto kern) -> int {
     if (bytes > 64 * 1024) {
