@@ -829,12 +829,13 @@ class ConfigNLP:
         # (nx = 4, nu = 2): Riccati factorisation ~270 FMA, residuals and
         # gradients ~90, predictor / corrector sweeps ~180 -> ~540 FMA
         flops = 2 * 540 * N * float(its.sum())
-        r_i = roof("ipm_kernel<double,4,2> / ipm_lds_kernel", "valu-fp64", flops, t_i,
+        r_i = roof("ipm_quad_kernel<double,1>", "valu-fp64", flops, t_i,
                    FP64_PEAK_TFS, "TFLOP/s", traffic.get("ipm"),
                    {"flops_per_launch": flops, "ipm_iters_mean": round(float(its.mean()), 2),
                     "ipm_iters_max": int(its.max()),
-                    "note": "lane per instance, serial over the stages: latency/issue-bound "
-                            "(one wave per SIMD); flops = 1080 per stage per IPM iteration "
+                    "note": "four lanes per instance, serial over the stages, the horizon in "
+                            "LDS (four per CU, one single-wave workgroup each): latency/LDS-"
+                            "bound; flops = 1080 per stage per IPM iteration "
                             "summed over the instances' own iteration counts, polish not counted"})
         extra = {"kernel_us": {"bicycle_rti": round(t_r * 1e3, 2),
                                "bicycle_hessian": round(t_h * 1e3, 2),
