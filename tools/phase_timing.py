@@ -80,7 +80,7 @@ elif cfg in (35, 36):
               "out: rows + M_GG", ""]
     a = A(); a.batch = int(os.environ.get("PT_BATCH", 65536)); a.slots = 1; a.horizon = 0; a.reps = 1
     a.check = 0
-    w = bench.CONFIGS[3](a, torch.device("cuda"), 0)
+    w = bench.CONFIGS["3"](a, torch.device("cuda"), 0)
     run = lambda: w.step(0)  # noqa: E731
     waves = a.batch * R
 elif cfg == 33:
