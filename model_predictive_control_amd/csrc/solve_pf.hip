@@ -485,9 +485,12 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
       constexpr int kCB = 4;
       while (mm) {
         float c[kCB], v[kCB][NR];
+        // an empty entry of the last batch re-reads the previous entry's row
+        // with coefficient 0: the pool outside the cached slots holds the
+        // refinement's doubles, whose bits can be NaN (and 0 * NaN = NaN)
+        int j = 0;
 #pragma unroll
         for (int t = 0; t < kCB; ++t) {
-          int j = 0;
           c[t] = 0.f;
           if (mm) {
             j = __builtin_ctzll(mm);
@@ -1066,6 +1069,15 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
       break;
     }
     }
+  }
+  // a non-finite value in the final state (never expected; the scan skips
+  // NaN violations, so it would otherwise pass as optimal): hand the
+  // instance to the workgroup kernel, which solves it from scratch
+  if (code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER) {
+    bool nf = false;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) nf |= (l + kWave * r < nt) && !(finite(val[r]) && finite(mu[r]));
+    if (__builtin_amdgcn_ballot_w64(nf)) code = kStatusRetry;
   }
 out:
   MPCQP_PHASE_K(7);

@@ -1,0 +1,134 @@
+"""GPU parity at the BASELINE configs' full single-GPU batch sizes, through
+size-independent properties (the oracle cannot solve 10^5 instances in a test):
+
+- config 3 (B = 65,536, fp32, state + input box, N = 30) and config 5
+  (B = 32,768, fp32, input box, nx = 12, N = 40): the product path
+  (mpcqp_mpc_qp: condense + MFMA sweep + product-form active set refined from
+  the dynamics in fp64) against the fp64 path of the same entry point (the
+  one-QP-per-workgroup kernel, a different algorithm and code path) on the SAME
+  fp32-valued inputs: every instance optimal, max|u_f32 - u_f64| < 1e-5 (the
+  north-star bar) over the whole batch;
+- config 4 (B = 131,072 per GPU, fp64, 40 polytope rows, N = 50): a KKT
+  certificate of every instance, evaluated in fp64 with torch from the shared
+  H, F, G: stationarity H z + F x0 + G'y = 0, primal feasibility G z <= h,
+  dual feasibility y >= 0 and complementarity y (G z - h) = 0.
+
+Data as bench.py builds it for these configs (seeded synthetic x0; the bicycle
+linearised by mpcqp_bicycle_rti about the zero-input rollout)."""
+import numpy as np
+import pytest
+import torch
+
+from model_predictive_control_amd import batched
+from model_predictive_control_amd.parameters import VehicleParameters
+from oracle import condense as oc
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5  # north star: max|u - u_ref| < 1e-5
+
+
+def _codes(st):
+    return batched.status_code(st).cpu().numpy()
+
+
+def _stable_plant(rng, nx, nu, rho=0.98):
+    U, _ = np.linalg.qr(rng.normal(size=(nx, nx)))
+    A = (U * rng.uniform(0.5, rho, size=nx)) @ U.T
+    B = rng.normal(size=(nx, nu)) / np.sqrt(nx)
+    return A, B
+
+
+def test_cfg3_full_batch_f32_vs_f64(dev):
+    """Config 3 at B = 65,536: fp32 product path = fp64 workgroup path."""
+    b, N, ts = 65536, 30, 0.08
+    p = VehicleParameters()
+    rng = np.random.default_rng(20261015 + 3)
+    X0 = np.stack([rng.uniform(-1, 1, b), rng.uniform(-.5, .5, b),
+                   rng.uniform(-np.pi / 4, np.pi / 4, b), rng.uniform(-.3, .3, b)], -1)
+    x = torch.as_tensor(X0, dtype=torch.float64, device=dev)
+    A, B, c = batched.bicycle_rti(x, torch.zeros((b, N, 2), dtype=torch.float64, device=dev),
+                                  p, ts)
+    Q = np.diag([1., 6., .2, .05])
+    xlo = np.tile([p.min_pos_x, p.min_pos_y, p.min_heading, p.min_vel], N)
+    xhi = np.tile([p.max_pos_x, p.max_pos_y, p.max_heading, p.max_vel], N)
+    lb, ub = np.tile([p.min_drive, -p.max_steer], N), np.tile([p.max_drive, p.max_steer], N)
+    # the fp32-valued data, and the same values in fp64
+    f32 = [t.to(torch.float32).contiguous() for t in (A, B, c, x)]
+    f64 = [t.double().contiguous() for t in f32]
+
+    def run(dt, A_, B_, c_, x_):
+        t = lambda a: torch.as_tensor(np.asarray(a, float), dtype=torch.float32,  # noqa: E731
+                                      device=dev).to(dt)
+        return batched.mpc_qp(A_, B_, t(Q), t(np.diag([1., .01])), t(100 * Q), N, x_,
+                              xlo=t(xlo), xhi=t(xhi), lb=t(lb), ub=t(ub), c=c_, tv=True)
+
+    z32, _, st32 = run(torch.float32, *f32)
+    z64, _, st64 = run(torch.float64, *f64)
+    torch.cuda.synchronize()
+    c32, c64 = _codes(st32), _codes(st64)
+    assert (c32 == 0).all(), np.unique(c32, return_counts=True)
+    assert (c64 == 0).all(), np.unique(c64, return_counts=True)
+    err = float((z32.double() - z64).abs().max())
+    assert err < TOL, err
+
+
+def test_cfg5_full_batch_f32_vs_f64(dev):
+    """Config 5 at B = 32,768 (nx = 12, nu = 4, N = 40, |u| <= 0.5, per-stage
+    perturbed plant): fp32 product path = fp64 workgroup path."""
+    b, nx, nu, N = 32768, 12, 4, 40
+    rng = np.random.default_rng(20261015 + 4)
+    A0, B0 = _stable_plant(rng, nx, nu)
+    g = torch.Generator(device=dev)
+    g.manual_seed(20261015 + 5)
+    t32 = lambda a: torch.as_tensor(a, dtype=torch.float32, device=dev)  # noqa: E731
+    A = (t32(A0) + 0.01 * torch.randn((b, N, nx, nx), generator=g, device=dev)).contiguous()
+    B = (t32(B0) + 0.01 * torch.randn((b, N, nx, nu), generator=g, device=dev)).contiguous()
+    x0 = (3.0 * torch.randn((b, nx), generator=g, device=dev)).contiguous()
+    Q, R = np.eye(nx), 0.1 * np.eye(nu)
+    n = N * nu
+
+    def run(dt):
+        t = lambda a: t32(a).to(dt)  # noqa: E731
+        return batched.mpc_qp(A.to(dt).contiguous(), B.to(dt).contiguous(), t(Q), t(R), t(Q), N,
+                              x0.to(dt).contiguous(), lb=t(np.full(n, -0.5)),
+                              ub=t(np.full(n, 0.5)), tv=True)
+
+    z32, _, st32 = run(torch.float32)
+    z64, _, st64 = run(torch.float64)
+    torch.cuda.synchronize()
+    c32, c64 = _codes(st32), _codes(st64)
+    assert (c32 == 0).all(), np.unique(c32, return_counts=True)
+    assert (c64 == 0).all(), np.unique(c64, return_counts=True)
+    err = float((z32.double() - z64).abs().max())
+    assert err < TOL, err
+
+
+def test_cfg4_full_batch_kkt(dev):
+    """Config 4 at B = 131,072: KKT certificate of every instance."""
+    b, nx, nu, N, m = 131072, 12, 4, 50, 40
+    n = N * nu
+    rng = np.random.default_rng(20261015 + 4)
+    A, B = _stable_plant(rng, nx, nu)
+    Q, R = np.eye(nx), 0.1 * np.eye(nu)
+    G = rng.normal(size=(m, n))
+    h = rng.uniform(0.5, 1.5, size=m)
+    d = oc.condense(A, B, Q, R, Q, N)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float64,  # noqa: E731
+                                  device=dev)
+    qp = batched.PolyQP(t(oc.pack_lower(d["H"])), t(G), t(d["F"]))
+    X0 = t(np.random.default_rng(20261015 + 4 + 1000).normal(size=(b, nx)) * 3.0)
+    z, y, st = qp.solve(X0, hu=t(h))
+    torch.cuda.synchronize()
+    code = _codes(st)
+    assert (code == 0).all(), np.unique(code, return_counts=True)
+    H, F, Gt, ht = t(d["H"]), t(d["F"]), t(G), t(h)
+    f = X0 @ F.T
+    grad = z @ H + f + y @ Gt              # H symmetric
+    scale = 1.0 + f.abs().amax(1, keepdim=True)
+    s = z @ Gt.T - ht                      # row slacks, <= 0 when feasible
+    assert float((grad.abs() / scale).max()) < 1e-9
+    assert float(s.max()) < 1e-9
+    assert float(y.min()) > -1e-12         # y > 0 only at the upper bound h
+    assert float((y * s).abs().max()) < 1e-9
+    assert int((y > 0).sum(1).max()) <= m
