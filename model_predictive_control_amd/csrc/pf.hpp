@@ -23,6 +23,9 @@ constexpr int kDynXd = 0, kDynLam = 3 * kWave, kDynX = kDynLam + 32;
 constexpr float kDynStop = 1e-4f;
 // ... and re-scans the refined point with this relative feasibility tolerance
 constexpr float kDynTol = 1e-7f;
+// dual re-check after the refinement: a fixed z whose exact gradient has the
+// wrong sign by more than this (relative to 1 + |f_i|) is released
+constexpr float kDualTol = 1e-6f;
 
 // Dynamics of the condensed QP (mpcqp_mpc_qp): z = [u_0..u_{N-1}], rows (m =
 // N nx, or 0) = the state box on x_1..x_N with the ORIGINAL bounds xlo/xhi.

@@ -52,6 +52,10 @@
   } while (0)
 #endif
 
+#ifndef MPCQP_PF_DUAL
+#define MPCQP_PF_DUAL 1
+#endif
+
 namespace mpcqp {
 
 struct PfArgs {
@@ -720,8 +724,16 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
     // Only the first scan of a round >= 1 sees refined values; every later
     // scan follows refresh() or fp32 active-set steps and keeps a.tol (the
     // fp32 floor would show as spurious violations of kDynTol)
+#if MPCQP_PF_DUAL
+    bool gi_skip = false;  // after a dual release: refine before the next scan
+#endif
     for (int round = 0; round < (NXP > 0 ? 3 : 1); ++round) {
+#if MPCQP_PF_DUAL
+    bool active = !gi_skip;
+    gi_skip = false;
+#else
     bool active = true;
+#endif
     bool tight = round > 0;
     for (int pass = 0; pass < 3 && active; ++pass) {
       while (true) {
@@ -1064,6 +1076,60 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
       int p;
       scan(viol, p);
       MPCQP_PHASE_D(6);
+#if MPCQP_PF_DUAL
+      // Dual re-check on the fixed z: the last residual left the exact
+      // (fp64) Lagrangian gradient g of every z in the pool (xd).  A bound
+      // held in the fp32 active set whose g has the wrong sign (g < 0 at lb,
+      // g > 0 at ub) is a floor of the fp32 condensed data the refinement
+      // cannot fix on a fixed active set: release the worst one (a Schur
+      // drop, as a partial step does) and let the next round's active set
+      // continue from there.
+      if (code == MPCQP_STATUS_OPTIMAL && round + 1 < 3 && a.refine > 0) {
+        const double* gx = pool + kDynXd;
+        float dv = -inf;
+        int dk = 0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int i = l + kWave * r;
+          if (i < n && (st[r] == 1 || st[r] == 2)) {
+            const float g = (float)gx[i];
+            const float v = ((st[r] == 1) ? -g : g) / (1.f + fabsf(fz[r]));
+            if (v > dv) {
+              dv = v;
+              dk = i;
+            }
+          }
+        }
+        wave_argmax(dv, dk);
+        dk = uniform(dk);
+        dv = readlane(dv, 0);
+        if (dv > kDualTol) {
+          const int q = uniform(pick<NR>(slot, dk));
+          s_row(q);
+          const float d = sx[q];
+          if (d > 0.f) {
+            s_drop(q, d);
+            used &= ~(1ull << q);
+            cmask &= ~(1ull << q);
+            if (l == q) aidx = -1;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+              const bool me = l + kWave * r == dk;
+              st[r] = me ? 0 : st[r];
+              mu[r] = me ? 0.f : mu[r];
+              slot[r] = me ? -1 : slot[r];
+            }
+            wave_lds_sync();
+            refresh();
+            // the fp32 values of the reduced set would show the released
+            // bound violated again (the same fp32 floor): the next round
+            // refines first and scans the fp64-accurate values
+            gi_skip = true;
+            continue;
+          }
+        }
+      }
+#endif
       if (!(viol > kDynTol) || code != MPCQP_STATUS_OPTIMAL) break;
     } else {
       break;

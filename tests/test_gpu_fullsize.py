@@ -71,16 +71,15 @@ def test_cfg3_full_batch_f32_vs_f64(dev):
     assert (c32 == 0).all(), np.unique(c32, return_counts=True)
     assert (c64 == 0).all(), np.unique(c64, return_counts=True)
     err = (z32.double() - z64).abs().amax(1)
-    # Open issue: 17 instances in 65,536 end up to 2.8e-3 from
-    # the fp64 solution (checked against the oracle: the fp32 answer is the
-    # off one).  Their fp32 active set holds one bound whose exact multiplier
-    # has the wrong sign -- every fp32 solver here (product form, two-kernel,
-    # workgroup) picks it, a floor of the fp32 condensed data -- and the fp64
-    # refinement corrects values on a fixed active set, re-checking primal
-    # feasibility only.  The bar holds for every other instance.
+    # Open issue: 7 instances in 65,536 end 1.4e-5 .. 2.7e-4
+    # from the fp64 solution (checked against the oracle: the fp32 answer is
+    # the off one).  The dual re-check after the fp64 refinement releases a
+    # fixed input bound whose exact multiplier has the wrong sign (it brought
+    # 17 instances, max 2.8e-3, down to these); the rest are not yet
+    # explained.  The bar holds for every other instance.
     above = int((err >= TOL).sum())
-    assert above <= 32, (above, float(err.max()))
-    assert float(err.max()) < 1e-2, float(err.max())
+    assert above <= 16, (above, float(err.max()))
+    assert float(err.max()) < 1e-3, float(err.max())
 
 
 def test_cfg5_full_batch_f32_vs_f64(dev):
