@@ -58,3 +58,16 @@ Hi = np.linalg.inv(Hd)
 Mref = np.block([[-Hi, Hi @ Gd.T], [Gd @ Hi, -Gd @ Hi @ Gd.T]])
 fin = np.isfinite(Mn)
 print("   max |M0 - ref| (finite)", float(np.abs(np.where(fin, Mn - Mref, 0)).max()), " cond(H)", np.linalg.cond(Hd))
+# active sets: oracle vs the mpc_qp result
+zf = z[0].double().cpu().numpy()
+so = dd["xbar"] + dd["Gam"] @ zr
+sf = dd["xbar"] + dd["Gam"] @ zf
+def act(zv, sv, tz, ts_):
+    az = set(np.where((zv <= r(lb) + tz) | (zv >= r(ub) - tz))[0].tolist())
+    ar = set((np.where((sv <= r(xlo) + ts_) | (sv >= r(xhi) - ts_))[0] + 60).tolist())
+    return az | ar
+Ao, Af = act(zr, so, 1e-9, 1e-9), act(zf, sf, 1e-6, 1e-5)
+print("   active oracle", sorted(Ao))
+print("   active f32   ", sorted(Af), " only-oracle", sorted(Ao - Af), " only-f32", sorted(Af - Ao))
+yy = y[0].double().cpu().numpy()
+print("   f32 row multipliers (nonzero):", {int(j) + 60: round(float(yy[j]), 6) for j in np.nonzero(yy)[0]})
