@@ -76,9 +76,9 @@ def test_cfg3_full_batch_f32_vs_f64(dev):
     # the off one).  The dual re-check after the fp64 refinement releases a
     # fixed input bound whose exact multiplier has the wrong sign (it brought
     # 17 instances, max 2.8e-3, down to these); on the rest the active set is
-    # right and the dynamics refinement does not contract within its step cap
-    # (the K-pass refinement meets the bar there).  The bar holds for every
-    # other instance.
+    # right and the dynamics refinement settles at a point that is not the
+    # QP's solution (the K-pass refinement meets the bar there): open defect.
+    # The bar holds for every other instance.
     above = int((err >= TOL).sum())
     assert above <= 16, (above, float(err.max()))
     assert float(err.max()) < 1e-3, float(err.max())
