@@ -999,6 +999,10 @@ def main():
     args.warmup = dwarm if args.warmup < 0 else args.warmup
 
     rank, world, local = mdist.env_rank_world()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} rank processes")
+    # N > 1: the final all-gather of z (the path's only collective) is timed by default
+    args.gather = args.gather or world > 1
     # rehearsal knobs (one-GPU box): MPCQP_BENCH_DEVICE pins every rank to one
     # device, MPCQP_DIST_BACKEND=gloo replaces RCCL (which needs one GPU per rank)
     local = int(os.environ.get("MPCQP_BENCH_DEVICE", local))
@@ -1090,8 +1094,8 @@ def main():
     units = getattr(wl, "units_per_step", 1)
     value = world * args.batch * units * args.steps / elapsed
     gather = None
-    if args.gather and world > 1:
-        gather = time_gather(wl, args, world, dev)
+    if args.gather and world > 1 and hasattr(wl, "Z"):
+        gather = time_gather(wl, args, world, dev, backend)
 
     # ---- correctness of what was timed: statuses + oracle spot check (rank 0)
     st = wl.status()
@@ -1157,24 +1161,34 @@ def main():
     return out
 
 
-def time_gather(wl, args, world, dev):
+def time_gather(wl, args, world, dev, backend="nccl"):
     """The only collective of the multi-GPU path: all-gather
     of every rank's solutions z (slot 0) into the whole batch on every rank,
-    timed with HIP events around the collective, outside the timed loop."""
+    timed with HIP events around the collective, outside the timed loop.
+    (gloo, the one-GPU rehearsal backend: host copies, host clock.)"""
     z = wl.Z[0]
     total = world * z.shape[0]
     torch.distributed.barrier()
-    mdist.gather_shards(z, total)          # warm-up (communicator setup)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    full = mdist.gather_shards(z, total)
-    e1.record()
-    e1.synchronize()
-    ms = mdist.max_over_ranks(e0.elapsed_time(e1), dev)
+    if backend != "nccl":
+        zc = z.cpu()
+        mdist.gather_shards(zc, total)
+        t0 = time.perf_counter()
+        full = mdist.gather_shards(zc, total)
+        ms = mdist.max_over_ranks((time.perf_counter() - t0) * 1e3, torch.device("cpu"))
+        note = "all-gather of z over ranks (gloo over host copies: one-GPU rehearsal)"
+    else:
+        mdist.gather_shards(z, total)          # warm-up (communicator setup)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        full = mdist.gather_shards(z, total)
+        e1.record()
+        e1.synchronize()
+        ms = mdist.max_over_ranks(e0.elapsed_time(e1), dev)
+        note = "all-gather of z over ranks (RCCL), after the timed loop"
     nbytes = full.numel() * full.element_size()
     return {"ms": round(ms, 4), "bytes": int(nbytes), "GBps": round(nbytes / (ms * 1e-3) / 1e9, 2),
-            "note": "all-gather of z over ranks (RCCL), after the timed loop"}
+            "note": note}
 
 
 def host_roundtrip(wl, graphs, args, reps=50):
@@ -1212,5 +1226,56 @@ def host_roundtrip(wl, graphs, args, reps=50):
             "note": "pinned host x0 -> device, one step, z -> pinned host, synchronize; per step"}
 
 
+def spawn_ranks(n):
+    """``--gpus N`` (N > 1) started without a launcher's environment: start N
+    rank processes, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, a free
+    127.0.0.1 rendezvous port), and wait for them.  This process never touches
+    the GPU; it only starts children.  If a rank fails the others are stopped
+    (they would wait at the first barrier), and the worst exit code is
+    returned.  Under torchrun (WORLD_SIZE set) main() runs directly."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        time.sleep(0.2)
+    bad = [rc for rc in rcs if rc != 0]
+    return (abs(bad[0]) or 1) if bad else 0
+
+
+def _gpus_arg(argv):
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
 if __name__ == "__main__":
+    ngpu = _gpus_arg(sys.argv[1:])
+    if ngpu > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(ngpu))
     main()

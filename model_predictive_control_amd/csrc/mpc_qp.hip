@@ -77,6 +77,17 @@ __global__ void states_kernel(int batch, int nx, int nu, int N, int tv, const T*
   }
 }
 
+// skip[b] = 1 for every instance except the hand-offs of the product-form
+// kernel (list[0..cnt)), which the fp64 fallback then solves
+__global__ void skip_all_kernel(int batch, int32_t* skip) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < batch) skip[b] = 1;
+}
+__global__ void unskip_list_kernel(const int* cnt, const int* list, int32_t* skip) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < *cnt) skip[list[j]] = 0;
+}
+
 static size_t al256(size_t v) { return (v + 255) / 256 * 256; }
 
 struct MpcWs {
@@ -110,6 +121,13 @@ static int mpc_refine() {
 static bool mpc_dyn() {
   const char* v = getenv("MPCQP_MPC_DYN");
   return v ? atoi(v) != 0 : true;
+}
+
+// MPCQP_MPC_FALLBACK=wg sends uncertified instances to the fp32 workgroup
+// kernel (flagged MPCQP_STATUS_UNREFINED) instead of the fp64 interior point
+static bool mpc_fallback_f64() {
+  const char* v = getenv("MPCQP_MPC_FALLBACK");
+  return !(v && v[0] == 'w');
 }
 
 template <typename T>
@@ -227,11 +245,37 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
       d.Qf = (const float*)Qf; d.sQf = strideQf;
       d.xlo = (const float*)xlo; d.xhi = (const float*)xhi; d.sXb = strideXb;
     }
+    // An instance the product-form kernel hands back -- more than 64 active
+    // constraints, a non-finite state, or (DYN) a refined point it could not
+    // certify as the QP's KKT point -- is solved again by the stage-wise fp64
+    // interior point with its exact polish (status bit
+    // MPCQP_STATUS_POLISHED), on the same inputs; it never returns OPTIMAL
+    // from the fp32 path uncertified.  The fallback runs over the whole batch
+    // with every other instance skipped, its workspace in the (then free)
+    // dense M0 region.
+    const QpWsParts P = qp_ws_parts(w + L.qp, batch, n, m);
+    const bool f64_fb = dyn_ok && mpc_fallback_f64() && ipm_supported(nx, nu) &&
+                        P.m0_bytes >= ipm_ws_bytes(batch, nx, nu, N) &&
+                        P.s0_bytes >= (size_t)batch * sizeof(int32_t);
     // a missing side of the state box has no finite bound: no row can be
     // active on it, so the residual never reads it
     rc = solve_two_kernel(batch, n, m, Hw, sH, fw, n, Gw, sG, hl, hu, m, lb, strideLb, ub,
                           strideUb, z, y, status, max_iter, tol, w + L.qp, st,
-                          dyn_ok ? &d : nullptr, dyn_ok ? mpc_refine() : -1);
+                          dyn_ok ? &d : nullptr, dyn_ok ? mpc_refine() : -1, f64_fb ? 0 : 1);
+    if (rc == MPCQP_OK && f64_fb) {
+      int32_t* skip = (int32_t*)P.s0;
+      const dim3 blk(256);
+      hipLaunchKernelGGL(skip_all_kernel, dim3((unsigned)((batch + 255) / 256)), blk, 0, st, batch,
+                         skip);
+      MPCQP_CHECK_LAUNCH("skip_all_kernel");
+      hipLaunchKernelGGL(unskip_list_kernel, dim3((unsigned)((batch + 255) / 256)), blk, 0, st,
+                         P.cnt, P.list, skip);
+      MPCQP_CHECK_LAUNCH("unskip_list_kernel");
+      rc = mpc_ipm_impl(MPCQP_F32, batch, nx, nu, N, flags & MPCQP_TV, A, strideA, Bm, strideB, Q,
+                        strideQ, R, strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi,
+                        strideXb, lb, strideLb, ub, strideUb, nullptr, 0, nullptr, 0, nullptr, 0, z,
+                        y, nullptr, nullptr, nullptr, status, skip, 1, 0, 0.0, P.m0, P.m0_bytes, st);
+    }
   } else if (m == 0) {  // input box only: the wavefront box kernels
     rc = mpcqp_solve_box(dtype, batch, n, Hw, sH, fw, n, lb, strideLb, ub, strideUb, z, status,
                          max_iter, tol, stream);

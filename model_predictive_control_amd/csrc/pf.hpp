@@ -19,13 +19,21 @@ constexpr int kPoolCacheExtra = 400;
 // rows; g overwrites u) | lam (2 x 16) | X ((N+1) nx) | Q, Qf, R (floats) |
 // stage chunk (floats): [A_s | B_s | c_s] for a run of stages
 constexpr int kDynXd = 0, kDynLam = 3 * kWave, kDynX = kDynLam + 32;
-// DYN refinement stops once a correction is below this (relative to 1+|z|)
-constexpr float kDynStop = 1e-4f;
-// ... and re-scans the refined point with this relative feasibility tolerance
+// DYN refinement: converged once a correction is below this (relative to
+// 1 + |value|); the residual after it is the certificate's
+constexpr float kDynStop = 1e-7f;
+// certificate, primal: relative violation of an inactive row or free z (the
+// scan's scales), from the exact values
 constexpr float kDynTol = 1e-7f;
-// dual re-check after the refinement: a fixed z whose exact gradient has the
-// wrong sign by more than this (relative to 1 + |f_i|) is released
-constexpr float kDualTol = 1e-6f;
+// certificate, dual: a fixed z whose exact Lagrangian gradient has the wrong
+// sign by more than kDualTol (1 + |f_i|), or an active row whose multiplier is
+// below -kDualTol, is released.  A wrong-signed weakly active bound moves z by
+// about its multiplier over the reduced curvature (>= 1e-2 at config 3), so
+// this keeps such a bound's effect below the 1e-5 bar.
+constexpr float kDualTol = 2e-8f;
+// DYN: active-set + refinement + certificate rounds before an uncertified
+// instance goes to the fp64 fallback
+constexpr int kDynRounds = 4;
 
 // Dynamics of the condensed QP (mpcqp_mpc_qp): z = [u_0..u_{N-1}], rows (m =
 // N nx, or 0) = the state box on x_1..x_N with the ORIGINAL bounds xlo/xhi.

@@ -75,11 +75,21 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
                  size_t ws_bytes, hipStream_t st);
 size_t qp_ws_bytes(int dtype, int batch, int n, int m);
 struct PfDyn;
-// dyn != NULL: refine from the dynamics (pf.hpp); refine < 0: default steps
+// dyn != NULL: refine from the dynamics (pf.hpp); refine < 0: default steps;
+// wg_fallback = 0: the hand-off list is left to the caller (see qp_ws_parts)
 int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const void* f,
                      int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
                      int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
                      void* z, void* y, int32_t* status, int max_iter, double tol, void* ws,
-                     hipStream_t st, const PfDyn* dyn = nullptr, int refine = -1);
+                     hipStream_t st, const PfDyn* dyn = nullptr, int refine = -1,
+                     int wg_fallback = 1);
+// the two-kernel workspace's parts: the dense M0 region and the s0 region
+// (both free once the product-form kernel has run), the hand-off count and list
+struct QpWsParts {
+  void* m0; size_t m0_bytes;
+  void* s0; size_t s0_bytes;
+  int* cnt; int* list;
+};
+QpWsParts qp_ws_parts(void* ws, int batch, int n, int m);
 
 }  // namespace mpcqp

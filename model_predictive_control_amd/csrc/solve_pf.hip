@@ -35,6 +35,8 @@
 //     exactly (no fp32 rounding of the condensed H, Gam, xbar), so refinement
 //     converges past the fp32 condensing floor, and it costs O(N nx (nx+nu))
 //     instead of O((n+m)^2) reads.
+#include <cstdlib>
+
 #include "mfma.hpp"
 #include "pf.hpp"
 
@@ -50,10 +52,6 @@
 #define MPCQP_PHASE_D(i) \
   do {               \
   } while (0)
-#endif
-
-#ifndef MPCQP_PF_DUAL
-#define MPCQP_PF_DUAL 1
 #endif
 
 namespace mpcqp {
@@ -73,6 +71,7 @@ struct PfArgs {
   int max_iter, refine;
   float tol;
   PfDyn d;                     // DYN kernels only
+  float dyn_stop;              // DYN: refinement stop (kDynStop; MPCQP_DYN_STOP)
 };
 
 // cnt floats from up to three contiguous global segments into LDS, every
@@ -139,8 +138,8 @@ __device__ __forceinline__ double group_sum(double v, int P) {
 }
 
 // KKT residual of the condensed QP from the dynamics, in fp64 (DYN pf
-// kernels).  x: z (i < n) and the signed row multipliers (rows i >= n, the
-// state box on x_1..x_N in stage-major order).  Out: w_i = (H z + f + G'mu)_i
+// kernels).  x + xl (a float pair): z (i < n) and the signed row multipliers
+// (rows i >= n, the state box on x_1..x_N in stage-major order).  Out: w_i = (H z + f + G'mu)_i
 // on free z, (G z - h)_i = x_k(z)_c - xlo/xhi on active rows, 0 elsewhere.
 //   forward   x_{s+1} = A_s x_s + B_s u_s + c_s
 //   backward  lam_N = Qf x_N + mu_N,  g_s = R u_s + B_s' lam_{s+1},
@@ -155,7 +154,8 @@ __device__ __forceinline__ double group_sum(double v, int P) {
 // spills and short runs than the round trips it hid.
 template <int NR, int NXP>
 __device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m, int l,
-                                             const float (&x)[NR], const int (&st)[NR],
+                                             const float (&x)[NR], const float* xl,
+                                             const int (&st)[NR],
                                              double* pool, int& loaded,
                                              float (&w)[NR] MPCQP_CLK_PARAM) {
   static_assert(NXP % 4 == 0 && NXP <= 16, "4 lanes per row, at most 16 rows");
@@ -197,7 +197,7 @@ __device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m
   // x0, u and the row multipliers into LDS
   if (l < nx) X[l] = (double)d.x0[(int64_t)b * d.sX0 + l];
 #pragma unroll
-  for (int r = 0; r < NR; ++r) xd[l + kWave * r] = (double)x[r];
+  for (int r = 0; r < NR; ++r) xd[l + kWave * r] = (double)x[r] + (double)xl[l + kWave * r];
 
   auto fwd_run = [&](int r) __attribute__((always_inline)) {
     const int s0 = r * cap, S = run_len(r);
@@ -346,7 +346,11 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
   // M0 row cache (below), extended past the refinement's needs where the row
   // cache is on: 34 KB of LDS per wave, 4 waves per CU
   constexpr bool kCache = NXP <= 4;
-  constexpr int kPoolX = kCache ? kPool + kPoolCacheExtra : kPool;
+  // past kPool: the row cache's extra rows (active set) or, in the DYN
+  // refinement, the low parts of the refined values (NR * 64 floats)
+  constexpr int kExtD = NR * kWave / 2;
+  static_assert(kExtD <= kPoolCacheExtra, "the refinement's low parts fit the cache extension");
+  constexpr int kPoolX = kCache ? kPool + kPoolCacheExtra : (NXP > 0 ? kPool + kExtD : kPool);
   __shared__ double pool[kPoolX];
   double* red = pool;
   double* rsum = pool + 8 * kWave;
@@ -724,16 +728,10 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
     // Only the first scan of a round >= 1 sees refined values; every later
     // scan follows refresh() or fp32 active-set steps and keeps a.tol (the
     // fp32 floor would show as spurious violations of kDynTol)
-#if MPCQP_PF_DUAL
     bool gi_skip = false;  // after a dual release: refine before the next scan
-#endif
-    for (int round = 0; round < (NXP > 0 ? 3 : 1); ++round) {
-#if MPCQP_PF_DUAL
+    for (int round = 0; round < (NXP > 0 ? kDynRounds : 1); ++round) {
     bool active = !gi_skip;
     gi_skip = false;
-#else
-    bool active = true;
-#endif
     bool tight = round > 0;
     for (int pass = 0; pass < 3 && active; ++pass) {
       while (true) {
@@ -928,9 +926,33 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
     // when it fits one chunk
     int dyn_loaded = -1;
     cmask = 0;  // the residual below reuses the pool
-    for (int it = 0; it < a.refine; ++it) {
-      MPCQP_PHASE_D(0);
-      float x[NR];
+    // correction sv = M w for a residual w on free z and active rows, in
+    // product form: y2 = M0[:, free z] w, q = S^-1 (y2_P - w_P),
+    // sv_i = y2_i + M0[i, P] q (i not in P), -q_i (i in P)
+    auto correction = [&](const float (&w)[NR], float (&sv)[NR]) __attribute__((always_inline)) {
+      float y2[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) y2[r] = 0.f;
+      // (measured: skipping the fixed z rows pays in the DYN kernels, the
+      // plain sweep over every z row is faster in the others)
+      if constexpr (NXP > 0)
+        zcols_free(w, y2);
+      else
+        zcols([&](int j) __attribute__((always_inline)) { return pick<NR>(w, j); }, y2);
+      const float ys = gather(y2);
+      const float wsl = gather(w);
+      const float q = smul(aidx >= 0 ? ys - wsl : 0.f);
+      pcols(q, y2, 1.f, false, used);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const bool act = st[r] == 1 || st[r] == 2;
+        const float qi = bperm(q, slot[r] < 0 ? 0 : slot[r]);
+        sv[r] = act ? -qi : y2[r];
+      }
+    };
+    // the refinement variable: z on free z, the signed multiplier on active
+    // rows (0 elsewhere; fixed z sit on their bound)
+    auto refvar = [&](float (&x)[NR]) __attribute__((always_inline)) {
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         const int i = l + kWave * r;
@@ -939,12 +961,13 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
         const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
         x[r] = (st[r] == 3) ? 0.f : (isz ? val[r] : (act ? sside * mu[r] : 0.f));
       }
-      float w[NR];
-      float dmax = 0.f;
-      if constexpr (NXP > 0) {
-        dyn_residual<NR, NXP>(a.d, b, n, m, l, x, st, pool, dyn_loaded, w MPCQP_CLK_ARG);
-        MPCQP_PHASE_K(0);  // phase timing: the residual is charged with the setup
-      } else {
+    };
+    if constexpr (NXP == 0) {
+      // K-pass: the residual from the fp32 condensed data (H, G), fp64
+      // accumulation; converges to the fp32 data floor
+      for (int it = 0; it < a.refine; ++it) {
+        float x[NR], w[NR];
+        refvar(x);
       // yk = K x in fp64, K = [[H, G'], [G, 0]]: row sweeps over packed H
       // and over G; the row-direction sums reduce 8 rows at a time in LDS
       double yk[NR];
@@ -1034,105 +1057,177 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
         const double e = isz ? yi + (double)fz[r] : yi - bnd;
         w[r] = (inS && i < nt) ? (float)e : 0.f;
       }
-      }
-      wave_lds_sync();
-      // sv = M w (w on free z and active rows): y2 = M0[:, free z] w
-      float y2[NR];
-#pragma unroll
-      for (int r = 0; r < NR; ++r) y2[r] = 0.f;
-      // (measured: skipping the fixed z rows pays in the DYN kernels, the
-      // plain sweep over every z row is faster in the others)
-      if constexpr (NXP > 0)
-        zcols_free(w, y2);
-      else
-        zcols([&](int j) __attribute__((always_inline)) { return pick<NR>(w, j); }, y2);
-      const float ys = gather(y2);
-      const float wsl = gather(w);
-      const float q = smul(aidx >= 0 ? ys - wsl : 0.f);
-      pcols(q, y2, 1.f, false, used);
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const int i = l + kWave * r;
-        const bool isz = i < n;
-        const bool act = st[r] == 1 || st[r] == 2;
-        const float qi = bperm(q, slot[r] < 0 ? 0 : slot[r]);
-        const float sv = act ? -qi : y2[r];
-        const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
-        val[r] = (isz && st[r] == 0) ? val[r] + sv : val[r];
-        val[r] = (!isz && st[r] == 0) ? val[r] - sv : val[r];  // row values G z
-        mu[r] = (!isz && act) ? mu[r] + sside * sv : mu[r];
-        dmax = (isz && st[r] == 0) ? fmaxf(dmax, fabsf(sv) / (1.f + fabsf(val[r]))) : dmax;
-      }
-      // DYN: the residual is exact, so a small correction means converged
-      // (the next step would shrink it by the contraction of the fp32 M0,
-      // ~1e-2); a large one (ill-conditioned instance) takes another step
-      MPCQP_PHASE_D(5);
-      if constexpr (NXP > 0) {
-        if (!(wave_max(dmax) > kDynStop)) break;
-      }
-    }
-    if constexpr (NXP > 0) {
-      float viol;
-      int p;
-      scan(viol, p);
-      MPCQP_PHASE_D(6);
-#if MPCQP_PF_DUAL
-      // Dual re-check on the fixed z: the last residual left the exact
-      // (fp64) Lagrangian gradient g of every z in the pool (xd).  A bound
-      // held in the fp32 active set whose g has the wrong sign (g < 0 at lb,
-      // g > 0 at ub) is a floor of the fp32 condensed data the refinement
-      // cannot fix on a fixed active set: release the worst one (a Schur
-      // drop, as a partial step does) and let the next round's active set
-      // continue from there.
-      if (code == MPCQP_STATUS_OPTIMAL && round + 1 < 3 && a.refine > 0) {
-        const double* gx = pool + kDynXd;
-        float dv = -inf;
-        int dk = 0;
+        wave_lds_sync();
+        float sv[NR];
+        correction(w, sv);
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
           const int i = l + kWave * r;
-          if (i < n && (st[r] == 1 || st[r] == 2)) {
-            const float g = (float)gx[i];
-            const float v = ((st[r] == 1) ? -g : g) / (1.f + fabsf(fz[r]));
-            if (v > dv) {
-              dv = v;
-              dk = i;
+          const bool isz = i < n;
+          const bool act = st[r] == 1 || st[r] == 2;
+          const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
+          val[r] = (isz && st[r] == 0) ? val[r] + sv[r] : val[r];
+          val[r] = (!isz && st[r] == 0) ? val[r] - sv[r] : val[r];  // row values G z
+          mu[r] = (!isz && act) ? mu[r] + sside * sv[r] : mu[r];
+        }
+      }
+      break;
+    } else {
+      if (a.refine <= 0) break;  // (A/B knob: no refinement, no certificate)
+      // DYN: refine from the exact (fp64) residual of the dynamics.  The
+      // refinement variable is carried as a float pair (val or mu, and its
+      // low part ext), so the fixed point is the fp64 solution on this
+      // active set, not its fp32 rounding: the certificate below then decides
+      // near-degenerate bounds and rows from values accurate to ~1e-10.
+      // The loop stops once a correction is below dyn_stop (relative); the
+      // residual evaluated after that correction is the certificate's.
+      float* ext = reinterpret_cast<float*>(pool + kPool);  // low parts, in LDS
+#pragma unroll
+      for (int r = 0; r < NR; ++r) ext[l + kWave * r] = 0.f;
+      bool conv = false;
+      float prev = inf;
+      for (int it = 0;; ++it) {
+        MPCQP_PHASE_D(0);
+        float x[NR], w[NR];
+        refvar(x);
+        dyn_residual<NR, NXP>(a.d, b, n, m, l, x, ext, st, pool, dyn_loaded, w MPCQP_CLK_ARG);
+        MPCQP_PHASE_K(0);  // phase timing: the residual is charged with the setup
+        if (it > 0 && !(prev > a.dyn_stop)) {
+          conv = true;
+          break;
+        }
+        if (it >= a.refine) break;
+        float sv[NR];
+        correction(w, sv);
+        float dmax = 0.f;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int i = l + kWave * r;
+          const bool isz = i < n;
+          const bool act = st[r] == 1 || st[r] == 2;
+          const bool ref = isz ? st[r] == 0 : act;
+          const float sside = ((st[r] == 1) ? 1.f : -1.f) * (isz ? 1.f : -1.f);
+          // x + ext + sv in fp64, split back into the float pair
+          const double xf = (double)x[r] + (double)ext[i] + (double)sv[r];
+          const float xh = (float)xf;
+          ext[i] = ref ? (float)(xf - (double)xh) : 0.f;
+          val[r] = (isz && st[r] == 0) ? xh : val[r];
+          val[r] = (!isz && st[r] == 0) ? val[r] - sv[r] : val[r];  // row values G z (re-set below)
+          mu[r] = (!isz && act) ? sside * xh : mu[r];
+          dmax = ref ? fmaxf(dmax, fabsf(sv[r]) / (1.f + fabsf(xh))) : dmax;
+        }
+        prev = wave_max(dmax);
+#ifdef MPCQP_PF_DEBUG
+        {
+          float rz = 0.f, rr = 0.f;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            const bool act = st[r] == 1 || st[r] == 2;
+            if (i < n && st[r] == 0) rz = fmaxf(rz, fabsf(w[r]));
+            if (i >= n && i < nt && act) rr = fmaxf(rr, fabsf(w[r]));
+          }
+          rz = wave_max(rz);
+          rr = wave_max(rr);
+          if (l == 0)
+            printf("pf b=%d round=%d it=%d |g_free|=%.3e |row_res|=%.3e dmax=%.3e nP=%d\n", b, round,
+                   it, rz, rr, prev, __builtin_popcountll(used));
+        }
+#endif
+        MPCQP_PHASE_D(5);
+      }
+      // ---- certificate of the refined point (the last residual is at it):
+      //   primal: every inactive state row from the fp64 rollout X, every
+      //           free z, within kDynTol (relative, the scan's scales);
+      //   dual:   the exact Lagrangian gradient g of every fixed z has the
+      //           bound's sign, every active row multiplier is >= 0, both
+      //           within kDualTol.
+      // The rows' values are re-set from X, so a violation is seen by the
+      // next round's tight scan with its exact size.
+      float pv = -inf, dv = -inf;
+      int dk = 0;
+      {
+        const double* gx = pool + kDynXd;
+        const double* Xr = pool + kDynX + a.d.nx;  // x_1..x_N, stage-major = row order
+        const float* xlo = a.d.xlo ? a.d.xlo + (int64_t)b * a.d.sXb : nullptr;
+        const float* xhi = a.d.xhi ? a.d.xhi + (int64_t)b * a.d.sXb : nullptr;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int i = l + kWave * r;
+          float p = -inf, dd = -inf;
+          if (i < n) {
+            if (st[r] == 0) {
+              p = fmaxf((s_lo[i] - val[r]) * s_sl[i], (val[r] - s_hi[i]) * s_su[i]);
+            } else {
+              const float g = (float)gx[i];
+              dd = ((st[r] == 1) ? -g : g) - kDualTol * (1.f + fabsf(fz[r]));
+            }
+          } else if (i < nt) {
+            const int j = i - n;
+            if (st[r] == 0) {
+              const double xv = Xr[j];
+              const bool hl = xlo && finite(s_lo[i]);
+              const bool hh = xhi && finite(s_hi[i]);
+              const float el = hl ? (float)((double)xlo[j] - xv) : -inf;  // > 0: below xlo
+              const float eh = hh ? (float)(xv - (double)xhi[j]) : -inf;  // > 0: above xhi
+              p = fmaxf(el * (hl ? s_sl[i] : 0.f), eh * (hh ? s_su[i] : 0.f));
+              // the exact row value on the condensed rows' scale
+              val[r] = hl ? s_lo[i] - el : (hh ? s_hi[i] + eh : val[r]);
+            } else if (st[r] == 1 || st[r] == 2) {
+              dd = -mu[r] - kDualTol;
             }
           }
+          pv = fmaxf(pv, p == p ? p : -inf);
+          const bool take = dd > dv;
+          dv = take ? dd : dv;
+          dk = take ? i : dk;
         }
+        pv = wave_max(pv);
         wave_argmax(dv, dk);
         dk = uniform(dk);
         dv = readlane(dv, 0);
-        if (dv > kDualTol) {
-          const int q = uniform(pick<NR>(slot, dk));
-          s_row(q);
-          const float d = sx[q];
-          if (d > 0.f) {
-            s_drop(q, d);
-            used &= ~(1ull << q);
-            cmask &= ~(1ull << q);
-            if (l == q) aidx = -1;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-              const bool me = l + kWave * r == dk;
-              st[r] = me ? 0 : st[r];
-              mu[r] = me ? 0.f : mu[r];
-              slot[r] = me ? -1 : slot[r];
-            }
-            wave_lds_sync();
-            refresh();
-            // the fp32 values of the reduced set would show the released
-            // bound violated again (the same fp32 floor): the next round
-            // refines first and scans the fp64-accurate values
-            gi_skip = true;
-            continue;
-          }
-        }
       }
+      MPCQP_PHASE_D(6);
+#ifdef MPCQP_PF_DEBUG
+      if (l == 0)
+        printf("pf b=%d round=%d cert conv=%d pv=%.3e dv=%.3e (at %d) code=%d\n", b, round, (int)conv,
+               pv, dv, dk, code);
 #endif
-      if (!(viol > kDynTol) || code != MPCQP_STATUS_OPTIMAL) break;
-    } else {
-      break;
+      if (code != MPCQP_STATUS_OPTIMAL) break;
+      if (conv && !(pv > kDynTol) && !(dv > 0.f)) break;  // certified optimal
+      // not certified: a refinement that does not contract, or no round
+      // left, hands the instance to the fp64 fallback (never OPTIMAL)
+      if (!conv || round + 1 >= kDynRounds) {
+        code = kStatusRetry;
+        break;
+      }
+      if (dv > 0.f) {
+        // release the worst wrong-signed constraint (a Schur drop, as a
+        // partial step does); the next round refines first and certifies
+        // again (re-scanning fp32 values would re-add it: the fp32 floor)
+        const int q = uniform(pick<NR>(slot, dk));
+        s_row(q);
+        const float d = sx[q];
+        if (!(d > 0.f)) {
+          code = kStatusRetry;
+          break;
+        }
+        s_drop(q, d);
+        used &= ~(1ull << q);
+        if (l == q) aidx = -1;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const bool me = l + kWave * r == dk;
+          st[r] = me ? 0 : st[r];
+          mu[r] = me ? 0.f : mu[r];
+          slot[r] = me ? -1 : slot[r];
+        }
+        wave_lds_sync();
+        refresh();
+        gi_skip = true;
+      }
+      // else: a primal violation; the next round's active set adds it from
+      // the exact values (first scan with the tight tolerance)
     }
     }
   }
@@ -1177,8 +1272,9 @@ int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* 
               int* retry_list, int max_iter, int refine, float tol, hipStream_t st,
               const PfDyn* dyn) {
   PfArgs a{batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, M0, s0, z, y, status,
-           retry_count, retry_list, max_iter, refine, tol, PfDyn{}};
+           retry_count, retry_list, max_iter, refine, tol, PfDyn{}, kDynStop};
   if (dyn) a.d = *dyn;
+  if (const char* e = getenv("MPCQP_DYN_STOP")) a.dyn_stop = (float)atof(e);
   const bool two = n + m <= 2 * kWave;
   const int nxp = dyn ? dyn_nxp(dyn->nx, dyn->nu) : 0;
 #define MPCQP_PF(NRV, NXPV) \

@@ -330,16 +330,28 @@ __global__ void flag_unrefined_kernel(const int* cnt, const int* list, int32_t* 
   }
 }
 
+QpWsParts qp_ws_parts(void* ws, int batch, int n, int m) {
+  char* w = (char*)ws;
+  QpWsParts p;
+  p.m0 = w;
+  p.m0_bytes = ws_m0_bytes(batch, n, m);
+  p.s0 = w + p.m0_bytes;
+  p.s0_bytes = ws_s0_bytes(batch, n, m);
+  p.cnt = (int*)(w + p.m0_bytes + p.s0_bytes);
+  p.list = p.cnt + 64;
+  return p;
+}
+
 int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const void* f,
                      int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
                      int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,
                      void* z, void* y, int32_t* status, int max_iter, double tol, void* ws,
-                     hipStream_t st, const PfDyn* dyn, int refine) {
-  char* w = (char*)ws;
-  float* M0 = (float*)w;
-  float* s0 = (float*)(w + ws_m0_bytes(batch, n, m));
-  int* cnt = (int*)(w + ws_m0_bytes(batch, n, m) + ws_s0_bytes(batch, n, m));
-  int* list = cnt + 64;
+                     hipStream_t st, const PfDyn* dyn, int refine, int wg_fallback) {
+  const QpWsParts P = qp_ws_parts(ws, batch, n, m);
+  float* M0 = (float*)P.m0;
+  float* s0 = (float*)P.s0;
+  int* cnt = P.cnt;
+  int* list = P.list;
   hipError_t e = hipMemsetAsync(cnt, 0, sizeof(int), st);
   if (e != hipSuccess) return hip_fail(e, "mpcqp_solve_qp_ws: hipMemsetAsync");
   int rc = sweep_launch(batch, n, m, H, sH, G, sG, M0, 1, status, st, f, sf, s0);
@@ -350,7 +362,7 @@ int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const v
                  (const float*)hl, (const float*)hu, sh, (const float*)lb, sLb, (const float*)ub,
                  sUb, M0, s0, (float*)z, (float*)y, status, cnt, list, mi,
                  refine >= 0 ? refine : pf_refine(), tl, st, dyn);
-  if (rc != MPCQP_OK) return rc;
+  if (rc != MPCQP_OK || !wg_fallback) return rc;
   rc = solve_qp_t<float>(batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, z, y,
                          status, max_iter, tol, st, M0, cnt, list);
   if (rc != MPCQP_OK || !dyn) return rc;

@@ -166,6 +166,8 @@ class MPCController:
             U = z.view(b, N, nu)
         # predicted states x_1..x_N of the last linearisation (IPOPT's "g" rows)
         self.last_prediction = X
+        self.last_lam_u = None  # (the condensed step reports no input multipliers)
+        self.last_cost = self._cost(X0, X, U)
         self._warm = torch.cat([U[:, 1:], U[:, -1:]], 1).contiguous()
         self.last_status = status
         return z, status
@@ -183,6 +185,8 @@ class MPCController:
         status = sqp.status()
         self.last_prediction = sqp.X[:, 1:]
         self.last_lam_g = sqp.y
+        self.last_lam_u = sqp.qp["lam_u"] if sqp.qp is not None else None
+        self.last_cost = self._cost(X0, sqp.X[:, 1:], sqp.U)
         self.last_costates = sqp.pi
         self.last_kkt = sqp.kkt
         self.last_iters = sqp.iters()
@@ -191,25 +195,50 @@ class MPCController:
         self.last_status = status
         return U.reshape(b, N * nu), status
 
+    def _cost(self, X0, X, U):
+        """The reference's objective, NOT halved (main.py:86,106): sum over
+        k < N of x_k'Q x_k + u_k'R u_k, plus x_N'Q_N x_N; X = x_1..x_N."""
+        b = X0.shape[0]
+        Xs = torch.cat([X0.reshape(b, 1, self.nx), X.reshape(b, self.N, self.nx)], 1).to(self.Q.dtype)
+        Us = U.reshape(b, self.N, self.nu).to(self.Q.dtype)
+        J = torch.einsum("bki,ij,bkj->b", Xs[:, :-1], self.Q, Xs[:, :-1])
+        J = J + torch.einsum("bki,ij,bkj->b", Us, self.R, Us)
+        return J + torch.einsum("bi,ij,bj->b", Xs[:, -1], self.QN, Xs[:, -1])
+
     def solve(self, x) -> dict:
-        """main.py:115-116: returns {"x": (N*nu, 1)} (or (batch, N*nu)) with
-        "g" (the predicted states x_1..x_N, IPOPT's constraint rows),
-        "lam_g" (state-box multipliers), "status", "success" and, in SQP
-        mode, "kkt" (the NLP optimality residual) and "iterations"."""
+        """main.py:115-116 (IPOPT through CasADi's nlpsol): returns
+          "x"      (N*nu, 1) stage-major inputs (or (batch, N*nu)),
+          "f"      the objective at x -- the reference's cost, not halved
+                   (main.py:86,106),
+          "g"      the constraint rows: the predicted states x_1..x_N,
+          "lam_g"  their multipliers in IPOPT's convention for that cost
+                   (> 0 at the upper bound xhi),
+          "lam_x"  the input-bound multipliers (> 0 at ubx; SQP mode -- the
+                   condensed RTI step does not form them),
+        plus "status", "success" and, in SQP mode, "kkt" (the NLP optimality
+        residual) and "iterations".  The device solvers work with the halved
+        cost J/2, so their multipliers are doubled here."""
         xa = np.asarray(x, dtype=float)
         single = xa.ndim == 1
         X0 = torch.as_tensor(xa.reshape(-1, self.nx), dtype=self.dtype, device=self.device)
         z, status = self.solve_batch(X0)
         zn = z.cpu().numpy()
         st = batched.status_code(status).cpu().numpy()
-        g = self.last_prediction.reshape(X0.shape[0], -1).cpu().numpy()
-        lam = self.last_lam_g.reshape(X0.shape[0], -1).cpu().numpy() \
+        b = X0.shape[0]
+        g = self.last_prediction.reshape(b, -1).cpu().numpy()
+        lam = (2.0 * self.last_lam_g.reshape(b, -1).double()).cpu().numpy() \
             if self.last_lam_g is not None else None
+        lam_u = (2.0 * self.last_lam_u.reshape(b, -1).double()).cpu().numpy() \
+            if self.last_lam_u is not None else None
+        f = self.last_cost.double().cpu().numpy()
         one = (lambda a: a[0].reshape(-1, 1)) if single else (lambda a: a)  # noqa: E731
-        out = {"x": one(zn), "g": one(g), "status": st[0] if single else st,
+        out = {"x": one(zn), "f": float(f[0]) if single else f, "g": one(g),
+               "status": st[0] if single else st,
                "success": bool(st[0] == 0) if single else st == 0}
         if lam is not None:
             out["lam_g"] = one(lam)
+        if lam_u is not None:
+            out["lam_x"] = one(lam_u)
         if self.mode == "sqp":
             kkt = self.last_kkt.cpu().numpy()
             it = self.last_iters.cpu().numpy()

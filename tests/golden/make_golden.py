@@ -285,6 +285,44 @@ def make_polyqp_s2(pr):
     np.savez_compressed(os.path.join(HERE, "polyqp_s2.npz"), **out)
 
 
+def make_cfg3_tail(dump=os.path.join(REPO, "tools", "cfg3_tail_inputs.npz")):
+    """The config-3 parity tail: the instances of the full B = 65,536 config-3
+    batch (seed 20261015 + 3, bicycle linearised about the zero-input rollout;
+    bench.py Config3) on which round 3's fp32 path ended >= 1e-6 from the fp64
+    solution, with their fp32-valued inputs as the GPU produced them
+    (tools/tail_dump.py dump -> tools/cfg3_tail_inputs.npz).  Each gets the
+    fp64 oracle solution of the QP those inputs define (oracle/condense.py +
+    oracle/qp.py poly_qp, Goldfarb-Idnani), KKT-certified here (< 1e-9): the
+    reference's IPOPT would return the same unique minimiser."""
+    from oracle import condense as oc
+    from oracle import qp as oq
+    from model_predictive_control_amd.parameters import VehicleParameters
+
+    d = np.load(dump)
+    N, p = 30, VehicleParameters()
+    r = lambda a: np.asarray(a, np.float32).astype(np.float64)  # noqa: E731
+    Q, R = r(np.diag([1., 6., .2, .05])), r(np.diag([1., .01]))
+    xlo = r(np.tile([p.min_pos_x, p.min_pos_y, p.min_heading, p.min_vel], N))
+    xhi = r(np.tile([p.max_pos_x, p.max_pos_y, p.max_heading, p.max_vel], N))
+    lb = r(np.tile([p.min_drive, -p.max_steer], N))
+    ub = r(np.tile([p.max_drive, p.max_steer], N))
+    Z, K = [], []
+    for j in range(len(d["index"])):
+        A, B, c, x0 = (d[k][j].astype(np.float64) for k in ("A", "B", "c", "x0"))
+        dd = oc.condense(A, B, Q, R, 100 * Q, N, x0=x0, c=c)
+        G = np.vstack([dd["Gam"], -dd["Gam"]])
+        h = np.concatenate([xhi - dd["xbar"], -(xlo - dd["xbar"])])
+        z, lam, _ = oq.poly_qp(dd["H"], dd["f"], G, h, lb, ub)
+        C = np.vstack([G, np.eye(60), -np.eye(60)])
+        rhs = np.concatenate([h, ub, -lb])
+        k = oq.kkt_poly(dd["H"], dd["f"], C, rhs, z, lam)
+        assert k < 1e-9, (j, k)
+        Z.append(z); K.append(k)
+    np.savez_compressed(os.path.join(HERE, "cfg3_tail.npz"), index=d["index"], A=d["A"], B=d["B"],
+                        c=d["c"], x0=d["x0"], z=np.array(Z), kkt=np.array(K),
+                        err_round3=d["err"])
+
+
 if __name__ == "__main__":
     only = sys.argv[1:]
     if not only or "session1" in only:
@@ -298,4 +336,6 @@ if __name__ == "__main__":
         make_polyqp_s2(pr)
     if not only or "nlp" in only:
         make_nlp()
+    if not only or "cfg3_tail" in only:
+        make_cfg3_tail()
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

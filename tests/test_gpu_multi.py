@@ -33,3 +33,23 @@ def test_two_ranks_shard_solve_gather_bitexact(tmp_path, total):
         res = json.load(fh)
     assert res["shape"] == [total, 20]
     assert res["bitexact"] and res["status_equal"] and res["optimal"], res
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    """`python bench.py --gpus 2` without a launcher starts its two rank
+    processes itself (the driver's N-GPU invocation).  On the
+    one-GPU test box both ranks are pinned to device 0 and gather over gloo."""
+    env = dict(os.environ, MPCQP_BENCH_DEVICE="0", MPCQP_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "8",
+                        "--warmup", "2", "--no-cpu", "--check", "16"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2
+    assert res["config"]["parallelism"] == "dp2"
+    assert res["optimal_frac"] == 1.0
+    assert res["max_abs_u_err_vs_oracle"] < 1e-9
+    assert res["gather"]["bytes"] == 2 * res["config"]["batch_per_gpu"] * 20 * 8

@@ -52,12 +52,39 @@ def test_solve_matches_nlp_fixtures(golden, tag):
         err = np.abs(U - Ustar[i]).max()
         assert err < TOL_U, (i, err)
         # the oracle's own evaluation of first-order optimality at (U, lam_g)
-        assert ocp.kkt(x0, U, np.asarray(sol["lam_g"]).reshape(-1)) < 10 * TOL_KKT
+        # (IPOPT's multipliers for the unhalved cost: the oracle's halved y x 2)
+        assert ocp.kkt(x0, U, np.asarray(sol["lam_g"]).reshape(-1) / 2) < 10 * TOL_KKT
         # g: the predicted states x_1..x_N along the solution
         assert np.abs(np.asarray(sol["g"]).reshape(-1, 4) - g[f"{tag}_X"][i][1:]).max() < 1e-6
         # __call__ (main.py:121-129) returns u_0 of a fresh solve
         u0 = _controller(g, tag)(x0)
         assert np.abs(u0 - Ustar[i][:2]).max() < TOL_U
+
+
+@pytest.mark.parametrize("tag", ["main", "sol"])
+def test_solve_returns_ipopt_result_mapping(golden, tag):
+    """main.py:115-116 returns CasADi's nlpsol dict: "f" is the reference's
+    objective (not halved, main.py:86,106), "lam_g" the state-row and "lam_x"
+    the input-bound multipliers in IPOPT's convention for that objective
+    (> 0 at the upper bound).  Against the oracle at the fixture optimum: f =
+    cost(U*), lam_g = 2 y*, lam_x = -2 grad(J/2 + y*'g)(U*) (zero on free
+    inputs, the bound's multiplier on active ones)."""
+    g = golden("nlp_s4.npz")
+    ocp = _ocp(g, tag)
+    X0, Ustar, Ystar = g[f"{tag}_x0"], g[f"{tag}_U"], g[f"{tag}_y"]
+    sol = _controller(g, tag).solve(X0)
+    assert np.asarray(sol["success"]).all()
+    for i, x0 in enumerate(X0):
+        J = ocp.cost(x0, Ustar[i])
+        assert abs(J - g[f"{tag}_J"][i]) < 1e-9 * (1 + abs(J))
+        assert abs(sol["f"][i] - J) < 1e-8 * (1 + abs(J)), (i, sol["f"][i], J)
+        lam_g = 2 * Ystar[i]
+        assert np.abs(sol["lam_g"][i] - lam_g).max() < 1e-6 * (1 + np.abs(lam_g).max())
+        grad, _ = ocp.grad(x0, Ustar[i], Ystar[i])
+        lam_x = -2 * grad
+        assert np.abs(sol["lam_x"][i] - lam_x).max() < 1e-6 * (1 + np.abs(lam_x).max()), i
+    one = _controller(g, tag).solve(X0[0])
+    assert isinstance(one["f"], float) and one["lam_x"].shape == (Ustar.shape[1], 1)
 
 
 @pytest.mark.parametrize("tag", ["main", "sol"])
