@@ -359,7 +359,9 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
  *   X ((N+1) x 4), U (N x 2), pi (N x 4) per instance.
  * mpcqp_bicycle_sqp_step: per instance not yet MPCQP_SQP_DONE: step d = Z - U
  *   (Z the QP solution; an instance whose qp_status is not OPTIMAL takes no
- *   step and leaves exact-Hessian mode), L1 merit 1/2 J + rho |state-box violation|_1 with
+ *   step: in exact-Hessian mode its damping mu grows x4, in Gauss-Newton mode
+ *   three failures in a row stop it with flags DONE | MPCQP_SQP_FAIL and the
+ *   QP's status code in bits 28..30), L1 merit 1/2 J + rho |state-box violation|_1 with
  *   rho >= 2 max|yq|, Armijo backtracking by quadratic interpolation; then
  *   U += alpha d, y += alpha (yq - y), pi += alpha (piq - pi), the rollout X
  *   ((N+1) x 4) at the new U and the first-order optimality residual of the
@@ -377,6 +379,7 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
  */
 #define MPCQP_SQP_DONE 1
 #define MPCQP_SQP_EXACT 2
+#define MPCQP_SQP_FAIL 4  /* with DONE: stopped by failing QPs; QP status in bits 28..30 */
 /* prediction models (integrator argument) */
 #define MPCQP_MODEL_FE 0  /* fwd_euler, main.py:132-135 */
 #define MPCQP_MODEL_RK4 1 /* runge_kutta4, main.py:138-147 (template.py:141) */
@@ -394,6 +397,19 @@ int mpcqp_bicycle_linearise(int dtype, int batch, int N, double ts, const double
 int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
                           const void* X, const void* U, const void* pi, const int32_t* flags,
                           const double* mu, void* H2, void* q2, void* stream);
+/*
+ * mpcqp_bicycle_hessian_convex: mpcqp_bicycle_hessian with a per-stage
+ * convexification: where the stage's QP Hessian W_k = blkdiag(Q, R) + H2_k
+ * (Q 4 x 4, R 2 x 2 shared, the stage weights) is not positive definite, its
+ * eigenvalues are lifted to eps and H2_k = W_k' - blkdiag(Q, R) (eigenvalue
+ * projection; stages with W_k > 0 keep the exact curvature), then + mu I.
+ * The SQP's QPs are convex by construction (no inertia correction, no
+ * rejected QP), and the exact Hessian is kept wherever it is convex.
+ */
+int mpcqp_bicycle_hessian_convex(int dtype, int batch, int N, double ts, const double* params,
+                                 const void* X, const void* U, const void* pi,
+                                 const int32_t* flags, const double* mu, const void* Q,
+                                 const void* R, double eps, void* H2, void* q2, void* stream);
 int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts, const double* params,
                            int integrator, const void* x0, int64_t strideX0, const void* Q, const void* R,
                            const void* Qf, const void* xlo, const void* xhi, int64_t strideXb,

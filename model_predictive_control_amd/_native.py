@@ -24,6 +24,7 @@ STATUS_POLISHED = 1 << 24
 STATUS_UNREFINED = 1 << 25
 SQP_DONE = 1
 SQP_EXACT = 2
+SQP_FAIL = 4
 MODEL_FE = 0
 MODEL_RK4 = 1
 PLANT_FE = 0
@@ -86,6 +87,8 @@ SIGNATURES = {
     "mpcqp_mpc_box_loop": (_i, [_i] * 6 + [_vp, _i64] * 7 + [_vp] * 3 + [_vp, _i, _d, _vp]),
     "mpcqp_bicycle_hessian": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _vp]),
+    "mpcqp_bicycle_hessian_convex": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _vp,
+                                          _vp, _vp, _vp, _vp, _vp, _d, _vp, _vp, _vp]),
     "mpcqp_bicycle_linearise": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp,
                                      _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "mpcqp_bicycle_sqp_step": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp, _i64,

@@ -717,17 +717,28 @@ def _bike_params(params):
 
 
 def bicycle_hessian(X, U, pi, params, ts: float, flags=None, mu=None,
-                    out: tuple | None = None):
+                    out: tuple | None = None, Q=None, R=None, eps: float = 1e-6):
     """Per stage, the curvature of the dynamics weighted by the costates plus
     a proximal mu I (include/mpcqp.h ``mpcqp_bicycle_hessian``): X (b, N+1,
     4), U (b, N, 2), pi (b, N, 4) fp64, mu (b,) or None -> H2 (b, N, 6, 6),
-    q2 (b, N, 6); zeros where flags (b,) lacks SQP_EXACT."""
+    q2 (b, N, 6); zeros where flags (b,) lacks SQP_EXACT.  With the stage
+    weights Q (4, 4) and R (2, 2): ``mpcqp_bicycle_hessian_convex``, the
+    curvature projected so that blkdiag(Q, R) + H2 >= eps I per stage."""
     b, N = int(U.shape[0]), int(U.shape[1])
     if out is None:
         H2 = torch.empty((b, N, 6, 6), dtype=torch.float64, device=U.device)
         q2 = torch.empty((b, N, 6), dtype=torch.float64, device=U.device)
     else:
         H2, q2 = out
+    if Q is not None:
+        Qc = Q.to(torch.float64).contiguous()
+        Rc = R.to(torch.float64).contiguous()
+        rc = _lib().mpcqp_bicycle_hessian_convex(nat.F64, b, N, float(ts), _bike_params(params),
+                                                 _ptr(X), _ptr(U), _ptr(pi), _ptr(flags), _ptr(mu),
+                                                 _ptr(Qc), _ptr(Rc), float(eps), _ptr(H2),
+                                                 _ptr(q2), _stream())
+        nat.check(rc, "mpcqp_bicycle_hessian_convex")
+        return H2, q2
     rc = _lib().mpcqp_bicycle_hessian(nat.F64, b, N, float(ts), _bike_params(params), _ptr(X),
                                       _ptr(U), _ptr(pi), _ptr(flags), _ptr(mu), _ptr(H2),
                                       _ptr(q2), _stream())

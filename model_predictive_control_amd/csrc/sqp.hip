@@ -20,7 +20,10 @@
 
 namespace mpcqp {
 
-constexpr int kSqpDone = 1, kSqpExact = 2;
+constexpr int kSqpDone = 1, kSqpExact = 2, kSqpFail = 4;
+// a Gauss-Newton QP (convex by construction) that fails this many times in a
+// row stops the instance: DONE | FAIL, the QP's status code in bits 28..30
+constexpr int kSqpMaxFails = 3;
 // KKT residual below which the exact Hessian is used (Gauss-Newton before:
 // far from a solution the costates that weight the curvature are poor)
 constexpr double kSqpSwitch = 1.0;
@@ -28,9 +31,121 @@ constexpr double kSqpSwitch = 1.0;
 // or a shortened step (at least kMuFloor), x1/4 after a full step
 constexpr double kMuFloor = 1e-4, kMuDec = 0.25;
 
-__global__ void bike_hess_kernel(int batch, int N, Bike p, const double* X, const double* U,
+// Symmetric eigen-decomposition of a 6 x 6 matrix by cyclic Jacobi sweeps,
+// fully unrolled (every index a compile-time constant: the matrix and the
+// rotation accumulate in registers).  On exit W is diagonal (the
+// eigenvalues) and V holds the eigenvectors as columns.
+__device__ __forceinline__ void jacobi6(double (&W)[6][6], double (&V)[6][6]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) V[i][j] = i == j ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 8; ++sweep) {
+    double off = 0.0, dia = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      dia = fma(W[i][i], W[i][i], dia);
+#pragma unroll
+      for (int j = i + 1; j < 6; ++j) off = fma(W[i][j], W[i][j], off);
+    }
+    if (!(off > 1e-30 * dia)) break;
+#pragma unroll
+    for (int pp = 0; pp < 5; ++pp) {
+#pragma unroll
+      for (int q = pp + 1; q < 6; ++q) {
+        const double apq = W[pp][q];
+        if (apq == 0.0) continue;
+        const double th = (W[q][q] - W[pp][pp]) / (2.0 * apq);
+        const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(fma(th, th, 1.0)));
+        const double c = 1.0 / sqrt(fma(t, t, 1.0)), sn = t * c;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {  // columns pp, q
+          const double wkp = W[k][pp], wkq = W[k][q];
+          W[k][pp] = c * wkp - sn * wkq;
+          W[k][q] = sn * wkp + c * wkq;
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {  // rows pp, q
+          const double wpk = W[pp][k], wqk = W[q][k];
+          W[pp][k] = c * wpk - sn * wqk;
+          W[q][k] = sn * wpk + c * wqk;
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const double vkp = V[k][pp], vkq = V[k][q];
+          V[k][pp] = c * vkp - sn * vkq;
+          V[k][q] = sn * vkp + c * vkq;
+        }
+      }
+    }
+  }
+}
+
+// Per-stage convexification (eigenvalue projection of the stage Hessian):
+// the stage's full QP Hessian is W = blkdiag(Q, R) + Hl (Hl the Lagrangian
+// curvature of the dynamics, whose (psi, v) block is always indefinite:
+// d2(v cos psi) couples them bilinearly).  Where W is not positive definite
+// (a Cholesky pivot below eps), its eigenvalues are lifted to eps and Hl is
+// replaced by W' - blkdiag(Q, R), so the QP is convex by construction; where
+// W is positive definite, Hl is left exact (Newton's rate near a solution).
+__device__ __forceinline__ void project_stage(double* Hl, const double* Qw, const double* Rw,
+                                              double eps) {
+  double W[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const double bd = (i < 4 && j < 4) ? Qw[i * 4 + j] : ((i >= 4 && j >= 4) ? Rw[(i - 4) * 2 + (j - 4)] : 0.0);
+      W[i][j] = Hl[i * 6 + j] + bd;
+    }
+  // Cholesky test
+  bool pd = true;
+  {
+    double L[6][6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      double d = W[j][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) d = fma(-L[j][k], L[j][k], d);
+      pd = pd && d > eps;
+      const double ljj = sqrt(fmax(d, eps));
+      L[j][j] = ljj;
+#pragma unroll
+      for (int i = j + 1; i < 6; ++i) {
+        double s = W[i][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s = fma(-L[i][k], L[j][k], s);
+        L[i][j] = s / ljj;
+      }
+    }
+  }
+  if (pd) return;
+  double V[6][6];
+  const double W0[6][6] = {{W[0][0], W[0][1], W[0][2], W[0][3], W[0][4], W[0][5]},
+                           {W[1][0], W[1][1], W[1][2], W[1][3], W[1][4], W[1][5]},
+                           {W[2][0], W[2][1], W[2][2], W[2][3], W[2][4], W[2][5]},
+                           {W[3][0], W[3][1], W[3][2], W[3][3], W[3][4], W[3][5]},
+                           {W[4][0], W[4][1], W[4][2], W[4][3], W[4][4], W[4][5]},
+                           {W[5][0], W[5][1], W[5][2], W[5][3], W[5][4], W[5][5]}};
+  jacobi6(W, V);
+  double lam[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) lam[i] = fmax(W[i][i], eps);
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) s = fma(V[i][k] * lam[k], V[j][k], s);
+      Hl[i * 6 + j] += s - W0[i][j];
+    }
+}
+
+__global__ __launch_bounds__(256) void bike_hess_kernel(int batch, int N, Bike p, const double* X, const double* U,
                                  const double* pi, const int32_t* flags, const double* mu,
-                                 double* H2, double* q2) {
+                                 const double* Qw, const double* Rw, double eps, double* H2,
+                                 double* q2) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)batch * N) return;
   const int64_t b = e / N;
@@ -49,6 +164,7 @@ __global__ void bike_hess_kernel(int batch, int N, Bike p, const double* X, cons
   const BikePt pt = bike_pt(p, x, u);
   double Hl[36];
   bike_lag_hess(p, pt, x, lam, Hl);
+  if (Qw && Rw) project_stage(Hl, Qw, Rw, eps);
   if (mu)
     for (int i = 0; i < 6; ++i) Hl[i * 6 + i] += mu[b];
   const double w[6] = {x[0], x[1], x[2], x[3], u[0], u[1]};
@@ -130,12 +246,23 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
   if (fl & kSqpDone) return;
   const int N = a.N;
   if (a.qp_status && (a.qp_status[b] & 0xFF) != MPCQP_STATUS_OPTIMAL) {
-    // the QP failed (non-convex beyond the inertia correction, or not
-    // converged): no step; an exact-Hessian iteration falls back to
-    // Gauss-Newton (positive definite) until the residual drops 10x
+    // the QP failed (not converged within its budget, or non-convex beyond
+    // the inertia correction with the unprojected Hessian): no step.  An
+    // exact-Hessian iteration raises the damping mu (x4, at least kMuFloor),
+    // which changes the next QP; a Gauss-Newton QP would be rebuilt
+    // unchanged, so kSqpMaxFails failures in a row stop the instance with
+    // the QP's status (never OPTIMAL)
     const int iters = ((fl >> 8) & 0xFFFF) + 1;
-    if (fl & kSqpExact) a.mu[b] = fmax(4.0 * a.mu[b], kMuFloor);
-    a.flags[b] = (iters << 8) | (fl & kSqpExact);
+    const int fails = ((fl >> 24) & 0xF) + 1;
+    const int code = a.qp_status[b] & 0x7;
+    if (fl & kSqpExact) {
+      a.mu[b] = fmax(4.0 * a.mu[b], kMuFloor);
+      a.flags[b] = (iters << 8) | kSqpExact;
+    } else if (fails >= kSqpMaxFails) {
+      a.flags[b] = (iters << 8) | kSqpDone | kSqpFail | (code << 28);
+    } else {
+      a.flags[b] = (iters << 8) | (fails << 24);
+    }
     return;
   }
   double* U = a.U + b * N * 2;
@@ -427,23 +554,42 @@ static Bike bike_of(double ts, const double* prm) {
   return p;
 }
 
-extern "C" int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
-                                     const void* X, const void* U, const void* pi,
-                                     const int32_t* flags, const double* mu, void* H2, void* q2,
-                                     void* stream) {
+static int bicycle_hessian_impl(const char* fn, int dtype, int batch, int N, double ts,
+                                const double* params, const void* X, const void* U,
+                                const void* pi, const int32_t* flags, const double* mu,
+                                const void* Q, const void* R, double eps, void* H2, void* q2,
+                                void* stream) {
   using namespace mpcqp;
-  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_bicycle_hessian: MPCQP_F64 only");
-  MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "mpcqp_bicycle_hessian: bad sizes");
-  MPCQP_CHECK_ARG(params && X && U && pi && H2 && q2, "mpcqp_bicycle_hessian: null pointer");
-  MPCQP_CHECK_ARG(params[1] > 0 && params[0] + params[1] > 0,
-                  "mpcqp_bicycle_hessian: bad axle lengths");
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "%s: MPCQP_F64 only", fn);
+  MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "%s: bad sizes", fn);
+  MPCQP_CHECK_ARG(params && X && U && pi && H2 && q2, "%s: null pointer", fn);
+  MPCQP_CHECK_ARG(params[1] > 0 && params[0] + params[1] > 0, "%s: bad axle lengths", fn);
   if (batch == 0) return MPCQP_OK;
   const int64_t total = (int64_t)batch * N;
   hipLaunchKernelGGL(bike_hess_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, batch, N, bike_of(ts, params), (const double*)X,
-                     (const double*)U, (const double*)pi, flags, mu, (double*)H2, (double*)q2);
+                     (const double*)U, (const double*)pi, flags, mu, (const double*)Q,
+                     (const double*)R, eps, (double*)H2, (double*)q2);
   MPCQP_CHECK_LAUNCH("bike_hess_kernel");
   return MPCQP_OK;
+}
+
+extern "C" int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
+                                     const void* X, const void* U, const void* pi,
+                                     const int32_t* flags, const double* mu, void* H2, void* q2,
+                                     void* stream) {
+  return bicycle_hessian_impl("mpcqp_bicycle_hessian", dtype, batch, N, ts, params, X, U, pi,
+                              flags, mu, nullptr, nullptr, 0.0, H2, q2, stream);
+}
+
+extern "C" int mpcqp_bicycle_hessian_convex(int dtype, int batch, int N, double ts,
+                                            const double* params, const void* X, const void* U,
+                                            const void* pi, const int32_t* flags,
+                                            const double* mu, const void* Q, const void* R,
+                                            double eps, void* H2, void* q2, void* stream) {
+  MPCQP_CHECK_ARG(Q && R && eps > 0.0, "mpcqp_bicycle_hessian_convex: Q, R and eps > 0 required");
+  return bicycle_hessian_impl("mpcqp_bicycle_hessian_convex", dtype, batch, N, ts, params, X, U,
+                              pi, flags, mu, Q, R, eps, H2, q2, stream);
 }
 
 extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,

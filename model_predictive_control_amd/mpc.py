@@ -39,7 +39,7 @@ import torch
 
 from . import _native as nat
 from . import batched
-from ._native import SQP_DONE, STATUS_MAXITER, STATUS_OPTIMAL
+from ._native import SQP_DONE, SQP_FAIL, STATUS_MAXITER, STATUS_OPTIMAL
 from .bicycle import KinematicBicycle
 from .parameters import VehicleParameters
 
@@ -76,8 +76,8 @@ class MPCController:
                           stacklevel=2)
         if mode not in ("sqp", "rti"):
             raise ValueError(f"mode must be 'sqp' or 'rti', got {mode!r}")
-        if hessian not in ("exact", "gauss-newton"):
-            raise ValueError(f"hessian must be 'exact' or 'gauss-newton', got {hessian!r}")
+        if hessian not in ("exact", "exact-raw", "gauss-newton"):
+            raise ValueError(f"hessian must be 'exact', 'exact-raw' or 'gauss-newton', got {hessian!r}")
         if integrator not in ("fe", "rk4"):
             raise ValueError(f"integrator must be 'fe' or 'rk4', got {integrator!r}")
         # the prediction model: fwd_euler (main.py:132-135, the model of
@@ -331,9 +331,14 @@ class SqpSolver:
         else:
             A, B, c, Xr = batched.bicycle_rti(X0, self.U, ctl.params, ctl.ts, states=True)
         H2 = q2 = None
-        if ctl.hessian == "exact":
+        if ctl.hessian != "gauss-newton":
+            # "exact": the Lagrangian curvature, projected per stage where the
+            # stage Hessian is not positive definite (convex QPs); "exact-raw":
+            # unprojected, the interior point's inertia correction and the
+            # damping mu handle indefiniteness
+            cw = dict(Q=ctl.Q, R=ctl.R) if ctl.hessian == "exact" else {}
             H2, q2 = batched.bicycle_hessian(Xr, self.U, self.pi, ctl.params, ctl.ts,
-                                             flags=self.flags, mu=self.mu)
+                                             flags=self.flags, mu=self.mu, **cw)
         self.qp = batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, X0, lb=ctl.lbz, ub=ctl.ubz,
                                   c=c, tv=True, H2=H2, q2=q2, strict=True, skip=self.flags,
                                   skip_mask=SQP_DONE, max_iter=self.QP_MAX_ITER, out=self.qp,
@@ -345,15 +350,19 @@ class SqpSolver:
                                  integrator=nat.MODEL_RK4 if ctl.integrator == "rk4" else nat.MODEL_FE)
 
     def done(self):
-        return (self.flags & SQP_DONE) != 0
+        """Converged instances (KKT <= tol)."""
+        return ((self.flags & SQP_DONE) != 0) & ((self.flags & SQP_FAIL) == 0)
 
     def iters(self):
         return (self.flags >> 8) & 0xFFFF
 
     def status(self):
-        """MPCQP status words: OPTIMAL (KKT <= tol) or MAXITER, iterations in
-        bits 8..23."""
+        """MPCQP status words: OPTIMAL (KKT <= tol), MAXITER, or the status
+        of the QP that stopped the instance (a Gauss-Newton QP failing
+        repeatedly); iterations in bits 8..23."""
+        failed = (self.flags & SQP_FAIL) != 0
         code = torch.where(self.done(), STATUS_OPTIMAL, STATUS_MAXITER).to(torch.int32)
+        code = torch.where(failed, (self.flags >> 28) & 0x7, code).to(torch.int32)
         return code | (self.iters() << 8)
 
 
