@@ -47,7 +47,9 @@ def _state_box(self) -> tuple[np.ndarray, np.ndarray]:
 
 VehicleParameters = make_dataclass(
     "VehicleParameters",
-    [(name, type(value), field(default=value)) for group in _GROUPS for name, value in group],
+    # every field is annotated float, as in the reference dataclass (parameters.py:4-54,
+    # whose friction/acceleration defaults are written as the literals 1 and 2)
+    [(name, float, field(default=value)) for group in _GROUPS for name, value in group],
     namespace={"input_box": _input_box, "state_box": _state_box,
                "__doc__": "Kinematic-bicycle parameters and bounds (session_4/parameters.py)."},
 )

@@ -285,6 +285,42 @@ def make_polyqp_s2(pr):
     np.savez_compressed(os.path.join(HERE, "polyqp_s2.npz"), **out)
 
 
+def make_nlp_tail(count=10, min_active=24):
+    """The saturated tail of the nlp bench's x0 distribution: initial states
+    of the main.py controller (N = 30, ts = 0.08, weights main.py:72-74,
+    input + state box) whose NLP optimum has at least ``min_active`` of its 60
+    inputs at a bound -- the instances the device SQP needed most iterations
+    on.  Kept whenever the oracle (oracle/nlp.py SQP + Newton polish) reaches
+    KKT < 1e-11, whether or not SciPy SLSQP finds the same point (on these it
+    often stops early); the oracle's point is a certified first-order
+    optimum, the one IPOPT would return from the same start."""
+    from oracle import nlp
+
+    xlo = np.array([-3.0, -2.0, -2 * np.pi, -0.5])
+    lbu = np.array([-1.0, -0.384])
+    Q = np.diag([1., 6., .2, .05])
+    ocp = nlp.OCP(30, 0.08, Q, 100 * Q, np.diag([1., .01]), xlo, -xlo, lbu, -lbu)
+    lb, ub = np.tile(lbu, 30), -np.tile(lbu, 30)
+    rng = np.random.default_rng(20261015 + 41)
+    X0, Us, Ys, K, J, NA = [], [], [], [], [], []
+    for _ in range(400):
+        x0 = np.array([rng.uniform(-.8, .8), rng.uniform(-.4, .4), rng.uniform(-.5, .5),
+                       rng.uniform(-.2, .2)])
+        U, y, k = ocp.solve(x0)
+        na = int(((np.abs(U - lb) < 1e-9) | (np.abs(U - ub) < 1e-9)).sum())
+        if k > 1e-11 or na < min_active:
+            continue
+        X0.append(x0); Us.append(U); Ys.append(y); K.append(k); J.append(ocp.cost(x0, U))
+        NA.append(na)
+        if len(X0) == count:
+            break
+    assert len(X0) == count, len(X0)
+    np.savez_compressed(os.path.join(HERE, "nlp_tail.npz"), x0=np.array(X0), U=np.array(Us),
+                        y=np.array(Ys), kkt=np.array(K), J=np.array(J), n_active=np.array(NA),
+                        N=np.array(30), ts=np.array(0.08), Q=Q, QN=100 * Q, R=np.diag([1., .01]),
+                        xlo=xlo, lbu=lbu)
+
+
 def make_cfg3_tail(dump=os.path.join(REPO, "tools", "cfg3_tail_inputs.npz")):
     """The config-3 parity tail: the instances of the full B = 65,536 config-3
     batch (seed 20261015 + 3, bicycle linearised about the zero-input rollout;
@@ -338,4 +374,6 @@ if __name__ == "__main__":
         make_nlp()
     if not only or "cfg3_tail" in only:
         make_cfg3_tail()
+    if not only or "nlp_tail" in only:
+        make_nlp_tail()
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from model_predictive_control_amd import batched
-from model_predictive_control_amd.bicycle import fe_linearize_batched, fe_step_batched
+from _torch_bicycle import fe_linearize_batched, fe_step_batched
 from model_predictive_control_amd.parameters import VehicleParameters
 from oracle import bicycle as ob
 

@@ -109,6 +109,57 @@ def test_n50_state_box_controller_runs(golden):
     assert np.abs(ctl.reshape_input(sol) - g["sol_U"][0].reshape(-1, 2)).max() < TOL_U
 
 
+def test_saturated_tail_fixtures(golden):
+    """The saturated tail of the nlp bench's x0 distribution
+    (tests/golden/nlp_tail.npz: 24-27 of the 60 inputs at a bound at the
+    optimum, oracle KKT < 1e-11): every instance converges within the
+    controller's default iteration budget, in one batched solve, to the
+    oracle's optimum (u to 1e-7, KKT < 1e-8)."""
+    g = golden("nlp_tail.npz")
+    ctl = MPCController(int(g["N"]), float(g["ts"]), VehicleParameters())
+    sol = ctl.solve(g["x0"])
+    its = np.asarray(sol["iterations"])
+    assert np.asarray(sol["success"]).all(), (sol["status"], sol["kkt"], its)
+    assert (np.asarray(sol["kkt"]) < TOL_KKT).all(), sol["kkt"]
+    err = np.abs(np.asarray(sol["x"]) - g["U"]).max(1)
+    assert err.max() < TOL_U, (err, its)
+    assert its.max() <= 60, its
+
+
+def test_hessian_convex_projection(dev):
+    """mpcqp_bicycle_hessian_convex: per stage, blkdiag(Q, R) + H2 is
+    positive definite (eigenvalues >= eps up to rounding); stages where the
+    exact one already is keep the exact curvature; q2 = -H2 w."""
+    p = VehicleParameters()
+    rng = np.random.default_rng(23)
+    b, N, ts = 4, 6, 0.08
+    X = rng.normal(size=(b, N + 1, 4)) * [1, 1, 1, 0.3]
+    U = rng.uniform(-0.35, 0.35, (b, N, 2))
+    pi = rng.normal(size=(b, N, 4)) * np.array([30, 30, 3, 3])  # large costates: indefinite
+    Q, R = np.diag([1., 6., .2, .05]), np.diag([1., .01])
+    t = lambda a: torch.as_tensor(a, dtype=torch.float64, device=dev)  # noqa: E731
+    H_ex, _ = batched.bicycle_hessian(t(X), t(U), t(pi), p, ts)
+    H_cv, q_cv = batched.bicycle_hessian(t(X), t(U), t(pi), p, ts, Q=t(Q), R=t(R), eps=1e-6)
+    torch.cuda.synchronize()
+    H_ex, H_cv, q_cv = H_ex.cpu().numpy(), H_cv.cpu().numpy(), q_cv.cpu().numpy()
+    Wb = np.zeros((6, 6)); Wb[:4, :4] = Q; Wb[4:, 4:] = R
+    projected = 0
+    for i in range(b):
+        for k in range(N):
+            ev_ex = np.linalg.eigvalsh(Wb + H_ex[i, k])
+            ev_cv = np.linalg.eigvalsh(Wb + H_cv[i, k])
+            assert ev_cv.min() > 1e-6 - 1e-9, ev_cv
+            if ev_ex.min() > 1e-6:
+                assert np.abs(H_cv[i, k] - H_ex[i, k]).max() < 1e-15
+            else:
+                projected += 1
+                # the projection only lifts eigenvalues: W' - W is PSD
+                assert np.linalg.eigvalsh(H_cv[i, k] - H_ex[i, k]).min() > -1e-9
+            w = np.concatenate([X[i, k], U[i, k]])
+            assert np.abs(q_cv[i, k] + H_cv[i, k] @ w).max() < 1e-12 * (1 + np.abs(q_cv[i, k]).max())
+    assert projected > 0
+
+
 def test_hessian_kernel_vs_oracle(dev):
     """mpcqp_bicycle_hessian (analytic second derivatives, bike.hpp) against
     the oracle's complex-step + central-difference curvature."""

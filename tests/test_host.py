@@ -106,8 +106,10 @@ def test_bicycle_batched_matches_numpy_and_fd():
     x = rng.uniform([-1, -0.5, -0.8, -0.3], [1, 0.5, 0.8, 0.3], (16, 4))
     u = rng.uniform([-1, -0.38], [1, 0.38], (16, 2))
     kb = bicycle.KinematicBicycle(p)
-    fb = bicycle.f_batched(torch.tensor(x), torch.tensor(u), p).numpy()
-    A, B, c = bicycle.fe_linearize_batched(torch.tensor(x), torch.tensor(u), p, 0.08)
+    from _torch_bicycle import f_batched, fe_linearize_batched
+
+    fb = f_batched(torch.tensor(x), torch.tensor(u), p).numpy()
+    A, B, c = fe_linearize_batched(torch.tensor(x), torch.tensor(u), p, 0.08)
     for i in range(16):
         assert np.abs(fb[i] - kb(x[i], u[i])).max() < 1e-14
         assert np.abs(fb[i] - ob.f(x[i], u[i])).max() < 1e-14
