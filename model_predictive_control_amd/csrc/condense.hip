@@ -645,12 +645,15 @@ static int launch_condense(CondenseArgs<T> a, hipStream_t st) {
 // i.e. f, F, Phi and xbar come out of one extra 16-column tile, drift
 // included, with no separate adjoint chain.
 //
-// Layout: one instance per wavefront.  Every 16 x 16 operand is an MFMA tile;
-// C/D tiles (lane (g, c): rows 4g..4g+3 of column c) are turned into B
-// operands (lane (g, c): rows g, 4+g, 8+g, 12+g of column c) by a 4 x 4
-// (lane group x register) transpose of two permlane32 + two permlane16
-// swaps -- no LDS round trip on the recursion.  The Gamma block row lives in
-// registers as NT B-operand tiles.  The What_k Gamma~ product (nu <= 16
+// Layout: one instance per wavefront.  Every 16 x 16 operand is an MFMA tile
+// held in C layout (lane (g, c): rows 4g..4g+3 of column c), and every
+// product is written as mfma4(P, Y) = P'Y (mfma.hpp: the K index of chunk s
+// in lane group g is 4g + s): W~A~ = W~'A~ (W~ symmetric), A~'X, B~'W~, and
+// A~ Gamma~ with A~' loaded in C layout.  An MFMA result is then the next
+// product's operand as it stands -- no transpose on the recursion (round 3
+// moved every C tile to a B layout by a 4 x 4 permlane transpose: two per
+// backward stage, one per Gamma tile and stage).  The Gamma block row lives
+// in registers as NT C-layout tiles.  The What_k Gamma~ product (nu <= 16
 // rows) runs on the VALU from the C tile: 16 FMAs per 4 output rows plus the
 // same transpose as a cross-group reduction, which leaves output row g of
 // column c in lane (g, c), so each H row segment is one 64-lane store.
@@ -686,7 +689,7 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
   float one_b[4], one_f[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int p = 4 * s + g;  // backward: row p, column cl (B operand of A~, A operand of B~')
+    const int p = 4 * g + s;  // C layout: register s of lane (g, cl) is row 4g+s, column cl
     oAb[s] = (p < nx && cl < nx) ? 4 * (p * nx + cl) : kOOB;
     oCb[s] = (p < nx && cl == 15) ? 4 * p : kOOB;
     oBb[s] = (p < nx && cl < nu) ? 4 * (p * nu + cl) : kOOB;
@@ -705,8 +708,8 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
   float wB[4], qC[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int p = 4 * s + g;
-    wB[s] = (p < nx && cl < nx) ? a.Qf[(int64_t)b * a.sQf + p * nx + cl] : 0.f;  // symmetric
+    const int p = 4 * g + s;
+    wB[s] = (p < nx && cl < nx) ? a.Qf[(int64_t)b * a.sQf + p * nx + cl] : 0.f;
     const int pc = 4 * g + s;
     qC[s] = (pc < nx && cl < nx) ? a.Q[(int64_t)b * a.sQ + pc * nx + cl] : 0.f;
   }
@@ -738,13 +741,11 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
     // What_k = B~_k' W~_{k+1}: rows 4g+j < nu of lane (g, cl)
     const mf4 w = mfma4(bT, wB, mf4{0.f, 0.f, 0.f, 0.f});
     if (k >= 1) {
-      const mf4 x = mfma4(wB, aT, mf4{0.f, 0.f, 0.f, 0.f});  // X = W~ A~
-      float xv[4] = {x[0], x[1], x[2], x[3]};
-      xpose4(xv);
+      const mf4 x = mfma4(wB, aT, mf4{0.f, 0.f, 0.f, 0.f});  // X = W~' A~ = W~ A~
+      const float xv[4] = {x[0], x[1], x[2], x[3]};
       const mf4 w2 = mfma4(aT, xv, mf4{qC[0], qC[1], qC[2], qC[3]});  // Q~ + A~' X
 #pragma unroll
       for (int s = 0; s < 4; ++s) wB[s] = w2[s];
-      xpose4(wB);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -787,7 +788,7 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
     const float* X0b = a.x0 ? a.x0 + (int64_t)b * a.sX0 : nullptr;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int p = 4 * s + g;
+      const int p = 4 * g + s;
       float v = 0.f;
       if (p < nx && cl < nx) v = (p == cl) ? 1.f : 0.f;
       else if (cl == 15) v = (p < nx) ? (X0b ? X0b[p] : 0.f) : (p == 15 ? 1.f : 0.f);
@@ -885,7 +886,6 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
           if (inblk && i < nu) h += Rs[i * nu + (col - blk0)];
           bst(h, rH, st ? 4 * (R * (R + 1) / 2 + col) : kOOB);
         }
-        xpose4(d);  // B layout for the next stage
       } else if (a.Gam && 16 * t < n) {  // structural zeros of the block row
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -922,7 +922,6 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
           if (a.f) bst(h, rf, (i < nu && cl == 15) ? 4 * R : kOOB);
         }
       }
-      xpose4(d);
 #pragma unroll
       for (int s = 0; s < 4; ++s) eB[s] = d[s];
     }

@@ -90,6 +90,14 @@ __global__ void unskip_list_kernel(const int* cnt, const int* list, int32_t* ski
 
 static size_t al256(size_t v) { return (v + 255) / 256 * 256; }
 
+// workspace of the dense path with its fp64 fallback: [0, max(dense, ipm))
+// holds the dense layout (then, once the product-form kernel is done, the
+// interior point's workspace), followed by the skip words
+static size_t mpc_skip_offset(size_t dense, size_t ipm) { return al256(dense > ipm ? dense : ipm); }
+static size_t mpc_fallback_bytes(int batch, size_t dense, size_t ipm) {
+  return mpc_skip_offset(dense, ipm) + al256((size_t)batch * sizeof(int32_t));
+}
+
 struct MpcWs {
   size_t H, f, Gam, xbar, hl, hu, qp, total;
 };
@@ -165,7 +173,10 @@ extern "C" size_t mpcqp_mpc_qp_workspace(int dtype, int batch, int nx, int nu, i
   const size_t dense = mpcqp::mpc_ws_layout(dtype, batch, nx, nu, N, state_box ? 1 : 0).total;
   // room for either path (the flags are not known here)
   const size_t ipm = mpcqp::ipm_supported(nx, nu) ? mpcqp::ipm_ws_bytes(batch, nx, nu, N) : 0;
-  return mpc_use_ipm(dtype, nx, nu, N, state_box ? 1 : 0, 0) ? ipm : (dense > ipm ? dense : ipm);
+  if (mpc_use_ipm(dtype, nx, nu, N, state_box ? 1 : 0, 0)) return ipm;
+  // the dense path's fp64 fallback: the interior point's workspace over the
+  // dead condensed data, then one skip word per instance
+  return mpcqp::mpc_fallback_bytes(batch, dense, ipm);
 }
 
 extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
@@ -251,19 +262,19 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
     // interior point with its exact polish (status bit
     // MPCQP_STATUS_POLISHED), on the same inputs; it never returns OPTIMAL
     // from the fp32 path uncertified.  The fallback runs over the whole batch
-    // with every other instance skipped, its workspace in the (then free)
-    // dense M0 region.
+    // with every other instance skipped, its workspace over the (then dead)
+    // condensed data.
     const QpWsParts P = qp_ws_parts(w + L.qp, batch, n, m);
-    const bool f64_fb = dyn_ok && mpc_fallback_f64() && ipm_supported(nx, nu) &&
-                        P.m0_bytes >= ipm_ws_bytes(batch, nx, nu, N) &&
-                        P.s0_bytes >= (size_t)batch * sizeof(int32_t);
+    const size_t ipmb = ipm_supported(nx, nu) ? ipm_ws_bytes(batch, nx, nu, N) : 0;
+    const bool f64_fb = dyn_ok && mpc_fallback_f64() && ipmb > 0 &&
+                        ws_bytes >= mpc_fallback_bytes(batch, L.total, ipmb);
     // a missing side of the state box has no finite bound: no row can be
     // active on it, so the residual never reads it
     rc = solve_two_kernel(batch, n, m, Hw, sH, fw, n, Gw, sG, hl, hu, m, lb, strideLb, ub,
                           strideUb, z, y, status, max_iter, tol, w + L.qp, st,
                           dyn_ok ? &d : nullptr, dyn_ok ? mpc_refine() : -1, f64_fb ? 0 : 1);
     if (rc == MPCQP_OK && f64_fb) {
-      int32_t* skip = (int32_t*)P.s0;
+      int32_t* skip = (int32_t*)(w + mpc_skip_offset(L.total, ipmb));
       const dim3 blk(256);
       hipLaunchKernelGGL(skip_all_kernel, dim3((unsigned)((batch + 255) / 256)), blk, 0, st, batch,
                          skip);
@@ -274,7 +285,7 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
       rc = mpc_ipm_impl(MPCQP_F32, batch, nx, nu, N, flags & MPCQP_TV, A, strideA, Bm, strideB, Q,
                         strideQ, R, strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi,
                         strideXb, lb, strideLb, ub, strideUb, nullptr, 0, nullptr, 0, nullptr, 0, z,
-                        y, nullptr, nullptr, nullptr, status, skip, 1, 0, 0.0, P.m0, P.m0_bytes, st);
+                        y, nullptr, nullptr, nullptr, status, skip, 1, 0, 0.0, w, ipmb, st);
     }
   } else if (m == 0) {  // input box only: the wavefront box kernels
     rc = mpcqp_solve_box(dtype, batch, n, Hw, sH, fw, n, lb, strideLb, ub, strideUb, z, status,

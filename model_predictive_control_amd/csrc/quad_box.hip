@@ -146,8 +146,20 @@ struct QMpcOcc {
 // fixed work (Riccati, x-bar/adjoint chains, reductions) doubles per QP, so
 // VALU instructions per QP rose 47 % (PMC SQ_INSTS_VALU) while the two waves
 // per SIMD hid only part of it.
+#ifdef MPCQP_WAVE_CLOCK
+// Debug library only (tools/wave_clock.py): per wave of mpc_group_kernel, the
+// s_memrealtime (100 MHz, chip-wide) at entry and at exit and the largest GI
+// iteration count of the wave's QPs -- the distribution of wave end times
+// against the kernel's slowest wave.
+constexpr int kWaveClockMax = 16384;
+__device__ unsigned long long mpcqp_wave_clock[3 * kWaveClockMax];
+#endif
+
 template <typename T, int NX, int NU, class Mat, int GL, int OCC>
 __global__ __launch_bounds__(64, OCC) void mpc_group_kernel(MpcArgsQ<T> a) {
+#ifdef MPCQP_WAVE_CLOCK
+  const unsigned long long wclk0 = __builtin_amdgcn_s_memrealtime();
+#endif
   using BL = GBoxLds<Mat>;
   constexpr int NV = BL::NV;
   constexpr int RPL = Mat::RPL;
@@ -534,6 +546,22 @@ __global__ __launch_bounds__(64, OCC) void mpc_group_kernel(MpcArgsQ<T> a) {
     }
   }
   if (live && q == 0) a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
+#ifdef MPCQP_WAVE_CLOCK
+  {
+    int itmax = 0;
+#pragma unroll
+    for (int gg = 0; gg < GPW; ++gg) {
+      const int v = __builtin_amdgcn_readlane(iters, gg * GL);
+      itmax = v > itmax ? v : itmax;
+    }
+    const unsigned long long wclk1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && blockIdx.x < kWaveClockMax) {
+      mpcqp_wave_clock[3 * blockIdx.x] = wclk0;
+      mpcqp_wave_clock[3 * blockIdx.x + 1] = wclk1;
+      mpcqp_wave_clock[3 * blockIdx.x + 2] = (unsigned long long)itmax;
+    }
+  }
+#endif
 }
 
 // ------------------------------------------------------------- launchers
@@ -616,6 +644,14 @@ template int mpc_box_quad<double>(const MpcArgsQ<double>&, hipStream_t);
 template int mpc_box_quad<float>(const MpcArgsQ<float>&, hipStream_t);
 
 }  // namespace mpcqp
+
+#ifdef MPCQP_WAVE_CLOCK
+extern "C" int mpcqp_debug_wave_clock(unsigned long long* out, int waves) {
+  const int w = waves < mpcqp::kWaveClockMax ? waves : mpcqp::kWaveClockMax;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcqp::mpcqp_wave_clock),
+                             3 * (size_t)w * sizeof(unsigned long long)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 #ifdef MPCQP_PHASE_TIMING
 // Debug library only: read (and optionally reset) the phase counters.

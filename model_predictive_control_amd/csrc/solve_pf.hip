@@ -1077,24 +1077,106 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
       // DYN: refine from the exact (fp64) residual of the dynamics.  The
       // refinement variable is carried as a float pair (val or mu, and its
       // low part ext), so the fixed point is the fp64 solution on this
-      // active set, not its fp32 rounding: the certificate below then decides
-      // near-degenerate bounds and rows from values accurate to ~1e-10.
-      // The loop stops once a correction is below dyn_stop (relative); the
-      // residual evaluated after that correction is the certificate's.
+      // active set, not its fp32 rounding.
+      //
+      // Certificate of a refined point (at the residual just computed):
+      //   primal: every inactive state row from the fp64 rollout X, every
+      //           free z, within kDynTol (relative, the scan's scales);
+      //   dual:   the exact Lagrangian gradient g of every fixed z has the
+      //           bound's sign, every active row multiplier is >= 0, both
+      //           within kDualTol.
+      // It is decided as soon as it is unambiguous: after a contracting
+      // correction (the residual fell 1000x), every checked quantity whose
+      // margin to its threshold exceeds the point's error -- taken as 10x the
+      // residual norm r (the residual is the error of the point as seen
+      // through the KKT matrix) -- decides the same way at the exact
+      // solution, so one correction usually suffices.  Otherwise the point
+      // is refined until a correction is below dyn_stop, and the
+      // certificate is decided on that converged point.  A refinement that
+      // neither contracts nor converges within a.refine corrections hands
+      // the instance to the fp64 fallback.
       float* ext = reinterpret_cast<float*>(pool + kPool);  // low parts, in LDS
 #pragma unroll
       for (int r = 0; r < NR; ++r) ext[l + kWave * r] = 0.f;
-      bool conv = false;
-      float prev = inf;
+      const double* gx = pool + kDynXd;
+      const double* Xr = pool + kDynX + a.d.nx;  // x_1..x_N, stage-major = row order
+      const float* xlo = a.d.xlo ? a.d.xlo + (int64_t)b * a.d.sXb : nullptr;
+      const float* xhi = a.d.xhi ? a.d.xhi + (int64_t)b * a.d.sXb : nullptr;
+      bool decided = false;
+      float prev = inf, r_prev = inf;
+      float pv = -inf, dv = -inf;
+      int dk = 0;
       for (int it = 0;; ++it) {
         MPCQP_PHASE_D(0);
         float x[NR], w[NR];
         refvar(x);
         dyn_residual<NR, NXP>(a.d, b, n, m, l, x, ext, st, pool, dyn_loaded, w MPCQP_CLK_ARG);
         MPCQP_PHASE_K(0);  // phase timing: the residual is charged with the setup
-        if (it > 0 && !(prev > a.dyn_stop)) {
-          conv = true;
-          break;
+        float rn = 0.f;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) rn = fmaxf(rn, fabsf(w[r]));
+        rn = wave_max(rn);
+        if (it > 0) {
+          // the certificate at this point, with margins tau = 10 r
+          const float tau = 10.f * rn;
+          float pvm = -inf, dvm = -inf;
+          pv = -inf;
+          dv = -inf;
+          dk = 0;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const int i = l + kWave * r;
+            float p = -inf, dd = -inf, pm = -inf, dm = -inf;
+            if (i < n) {
+              if (st[r] == 0) {
+                const float vl = (s_lo[i] - val[r]) * s_sl[i], vu = (val[r] - s_hi[i]) * s_su[i];
+                p = fmaxf(vl, vu);
+                pm = fmaxf(vl + tau * s_sl[i], vu + tau * s_su[i]);
+              } else {
+                const float g = (float)gx[i];
+                const float wg = (st[r] == 1) ? -g : g;  // > 0: wrong sign
+                dd = wg - kDualTol * (1.f + fabsf(fz[r]));
+                dm = wg + tau;
+              }
+            } else if (i < nt) {
+              const int j = i - n;
+              if (st[r] == 0) {
+                const double xv = Xr[j];
+                const bool hl = xlo && finite(s_lo[i]);
+                const bool hh = xhi && finite(s_hi[i]);
+                const float el = hl ? (float)((double)xlo[j] - xv) : -inf;  // > 0: below xlo
+                const float eh = hh ? (float)(xv - (double)xhi[j]) : -inf;  // > 0: above xhi
+                p = fmaxf(el * (hl ? s_sl[i] : 0.f), eh * (hh ? s_su[i] : 0.f));
+                pm = fmaxf((el + tau) * (hl ? s_sl[i] : 0.f), (eh + tau) * (hh ? s_su[i] : 0.f));
+                // the exact row value on the condensed rows' scale
+                val[r] = hl ? s_lo[i] - el : (hh ? s_hi[i] + eh : val[r]);
+              } else if (st[r] == 1 || st[r] == 2) {
+                dd = -mu[r] - kDualTol;
+                dm = -mu[r] + tau;
+              }
+            }
+            pv = fmaxf(pv, p == p ? p : -inf);
+            pvm = fmaxf(pvm, pm == pm ? pm : -inf);
+            dvm = fmaxf(dvm, dm);
+            const bool take = dd > dv;
+            dv = take ? dd : dv;
+            dk = take ? i : dk;
+          }
+          pv = wave_max(pv);
+          pvm = wave_max(pvm);
+          dvm = wave_max(dvm);
+          wave_argmax(dv, dk);
+          dk = uniform(dk);
+          dv = readlane(dv, 0);
+          // unambiguous: all clear by the margin, or a violation beyond it
+          const bool clear = !(pvm > kDynTol) && !(dvm > 0.f);
+          const bool fails = pv > kDynTol + tau || dv > tau;
+          const bool contracting = !(rn > 1e-3f * r_prev);
+          const bool converged = !(prev > a.dyn_stop);
+          if ((contracting && (clear || fails)) || converged) {
+            decided = true;
+            break;
+          }
         }
         if (it >= a.refine) break;
         float sv[NR];
@@ -1112,87 +1194,26 @@ __global__ __launch_bounds__(64, 2) void qp_pf_kernel(PfArgs a) {
           const float xh = (float)xf;
           ext[i] = ref ? (float)(xf - (double)xh) : 0.f;
           val[r] = (isz && st[r] == 0) ? xh : val[r];
-          val[r] = (!isz && st[r] == 0) ? val[r] - sv[r] : val[r];  // row values G z (re-set below)
+          val[r] = (!isz && st[r] == 0) ? val[r] - sv[r] : val[r];  // row values G z (re-set above)
           mu[r] = (!isz && act) ? sside * xh : mu[r];
           dmax = ref ? fmaxf(dmax, fabsf(sv[r]) / (1.f + fabsf(xh))) : dmax;
         }
         prev = wave_max(dmax);
+        r_prev = rn;
 #ifdef MPCQP_PF_DEBUG
-        {
-          float rz = 0.f, rr = 0.f;
-#pragma unroll
-          for (int r = 0; r < NR; ++r) {
-            const int i = l + kWave * r;
-            const bool act = st[r] == 1 || st[r] == 2;
-            if (i < n && st[r] == 0) rz = fmaxf(rz, fabsf(w[r]));
-            if (i >= n && i < nt && act) rr = fmaxf(rr, fabsf(w[r]));
-          }
-          rz = wave_max(rz);
-          rr = wave_max(rr);
-          if (l == 0)
-            printf("pf b=%d round=%d it=%d |g_free|=%.3e |row_res|=%.3e dmax=%.3e nP=%d\n", b, round,
-                   it, rz, rr, prev, __builtin_popcountll(used));
-        }
+        if (l == 0)
+          printf("pf b=%d round=%d it=%d |r|=%.3e dmax=%.3e nP=%d\n", b, round, it, rn, prev,
+                 __builtin_popcountll(used));
 #endif
         MPCQP_PHASE_D(5);
-      }
-      // ---- certificate of the refined point (the last residual is at it):
-      //   primal: every inactive state row from the fp64 rollout X, every
-      //           free z, within kDynTol (relative, the scan's scales);
-      //   dual:   the exact Lagrangian gradient g of every fixed z has the
-      //           bound's sign, every active row multiplier is >= 0, both
-      //           within kDualTol.
-      // The rows' values are re-set from X, so a violation is seen by the
-      // next round's tight scan with its exact size.
-      float pv = -inf, dv = -inf;
-      int dk = 0;
-      {
-        const double* gx = pool + kDynXd;
-        const double* Xr = pool + kDynX + a.d.nx;  // x_1..x_N, stage-major = row order
-        const float* xlo = a.d.xlo ? a.d.xlo + (int64_t)b * a.d.sXb : nullptr;
-        const float* xhi = a.d.xhi ? a.d.xhi + (int64_t)b * a.d.sXb : nullptr;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-          const int i = l + kWave * r;
-          float p = -inf, dd = -inf;
-          if (i < n) {
-            if (st[r] == 0) {
-              p = fmaxf((s_lo[i] - val[r]) * s_sl[i], (val[r] - s_hi[i]) * s_su[i]);
-            } else {
-              const float g = (float)gx[i];
-              dd = ((st[r] == 1) ? -g : g) - kDualTol * (1.f + fabsf(fz[r]));
-            }
-          } else if (i < nt) {
-            const int j = i - n;
-            if (st[r] == 0) {
-              const double xv = Xr[j];
-              const bool hl = xlo && finite(s_lo[i]);
-              const bool hh = xhi && finite(s_hi[i]);
-              const float el = hl ? (float)((double)xlo[j] - xv) : -inf;  // > 0: below xlo
-              const float eh = hh ? (float)(xv - (double)xhi[j]) : -inf;  // > 0: above xhi
-              p = fmaxf(el * (hl ? s_sl[i] : 0.f), eh * (hh ? s_su[i] : 0.f));
-              // the exact row value on the condensed rows' scale
-              val[r] = hl ? s_lo[i] - el : (hh ? s_hi[i] + eh : val[r]);
-            } else if (st[r] == 1 || st[r] == 2) {
-              dd = -mu[r] - kDualTol;
-            }
-          }
-          pv = fmaxf(pv, p == p ? p : -inf);
-          const bool take = dd > dv;
-          dv = take ? dd : dv;
-          dk = take ? i : dk;
-        }
-        pv = wave_max(pv);
-        wave_argmax(dv, dk);
-        dk = uniform(dk);
-        dv = readlane(dv, 0);
       }
       MPCQP_PHASE_D(6);
 #ifdef MPCQP_PF_DEBUG
       if (l == 0)
-        printf("pf b=%d round=%d cert conv=%d pv=%.3e dv=%.3e (at %d) code=%d\n", b, round, (int)conv,
-               pv, dv, dk, code);
+        printf("pf b=%d round=%d cert decided=%d pv=%.3e dv=%.3e (at %d) code=%d\n", b, round,
+               (int)decided, pv, dv, dk, code);
 #endif
+      const bool conv = decided;
       if (code != MPCQP_STATUS_OPTIMAL) break;
       if (conv && !(pv > kDynTol) && !(dv > 0.f)) break;  // certified optimal
       // not certified: a refinement that does not contract, or no round
