@@ -131,6 +131,13 @@ static bool mpc_dyn() {
   return v ? atoi(v) != 0 : true;
 }
 
+// MPCQP_MPC_ZF=0 keeps configs of the z-space kernel (solve_zf.hip) on the
+// dense sweep + product-form path (A/B)
+static bool mpc_zf() {
+  const char* v = getenv("MPCQP_MPC_ZF");
+  return v ? atoi(v) != 0 : true;
+}
+
 // MPCQP_MPC_FALLBACK=wg sends uncertified instances to the fp32 workgroup
 // kernel (flagged MPCQP_STATUS_UNREFINED) instead of the fp64 interior point
 static bool mpc_fallback_f64() {
@@ -220,12 +227,71 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
   const int tv = (flags & MPCQP_TV) ? 1 : 0;
   void* Hw = w + L.H;
   void* fw = w + L.f;
-  void* Gw = sbox ? w + L.Gam : nullptr;
-  void* xbw = sbox ? w + L.xbar : nullptr;
+  const size_t qpb = qp_ws_bytes(dtype, batch, n, m);
+  const int64_t sH = (int64_t)n * (n + 1) / 2, sG = (int64_t)m * n;
+  PfDyn d{};
+  const bool dyn_ok = dtype == MPCQP_F32 && qpb > 0 && mpc_dyn() && dyn_nxp(nx, nu) > 0 &&
+                      dyn_chunk_stages(nx, nu, N) >= 1;
+  if (dyn_ok) {
+    d.nx = nx; d.nu = nu; d.N = N; d.tv = tv;
+    d.A = (const float*)A; d.sA = strideA;
+    d.B = (const float*)Bm; d.sB = strideB;
+    d.c = (const float*)c; d.sC = strideC;
+    d.x0 = (const float*)x0; d.sX0 = strideX0;
+    d.Q = (const float*)Q; d.sQ = strideQ;
+    d.R = (const float*)R; d.sR = strideR;
+    d.Qf = (const float*)Qf; d.sQf = strideQf;
+    d.xlo = (const float*)xlo; d.xhi = (const float*)xhi; d.sXb = strideXb;
+  }
+  // An instance the fp32 kernels hand back -- more than 64 active
+  // constraints, a non-finite state, or (DYN) a refined point they could not
+  // certify as the QP's KKT point -- is solved again by the stage-wise fp64
+  // interior point with its exact polish (status bit MPCQP_STATUS_POLISHED),
+  // on the same inputs; it never returns OPTIMAL from the fp32 path
+  // uncertified.  The fallback runs over the whole batch with every other
+  // instance skipped, its workspace over the (then dead) condensed data.
+  const QpWsParts P = qp_ws_parts(w + L.qp, batch, n, m);
+  const size_t ipmb = ipm_supported(nx, nu) ? ipm_ws_bytes(batch, nx, nu, N) : 0;
+  const bool f64_fb = dyn_ok && mpc_fallback_f64() && ipmb > 0 &&
+                      ws_bytes >= mpc_fallback_bytes(batch, L.total, ipmb);
+  auto fallback_f64 = [&]() -> int {
+    int32_t* skip = (int32_t*)(w + mpc_skip_offset(L.total, ipmb));
+    const dim3 blk(256);
+    hipLaunchKernelGGL(skip_all_kernel, dim3((unsigned)((batch + 255) / 256)), blk, 0, st, batch,
+                       skip);
+    MPCQP_CHECK_LAUNCH("skip_all_kernel");
+    hipLaunchKernelGGL(unskip_list_kernel, dim3((unsigned)((batch + 255) / 256)), blk, 0, st,
+                       P.cnt, P.list, skip);
+    MPCQP_CHECK_LAUNCH("unskip_list_kernel");
+    return mpc_ipm_impl(MPCQP_F32, batch, nx, nu, N, flags & MPCQP_TV, A, strideA, Bm, strideB, Q,
+                        strideQ, R, strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi,
+                        strideXb, lb, strideLb, ub, strideUb, nullptr, 0, nullptr, 0, nullptr, 0, z,
+                        y, nullptr, nullptr, nullptr, status, skip, 1, 0, 0.0, w, ipmb, st);
+  };
+  // fp32 with n <= 64 (config 3): H^-1 on chip, rows from the dynamics --
+  // only H and f are condensed
+  const bool zf = dyn_ok && f64_fb && mpc_zf() && zf_supported(n, m, nx, nu, N);
+  void* Gw = (sbox && !zf) ? w + L.Gam : nullptr;
+  void* xbw = (sbox && !zf) ? w + L.xbar : nullptr;
   int rc = mpcqp_condense(dtype, batch, nx, nu, N, flags, A, strideA, Bm, strideB, Q, strideQ, R,
                           strideR, Qf, strideQf, c, strideC, x0, strideX0, Hw, nullptr, fw, Gw,
                           nullptr, xbw, stream);
   if (rc != MPCQP_OK) return rc;
+  if (zf) {
+    hipError_t e = hipMemsetAsync(P.cnt, 0, sizeof(int), st);
+    if (e != hipSuccess) return hip_fail(e, "mpcqp_mpc_qp: hipMemsetAsync");
+    const int mi = max_iter > 0 ? max_iter : 3 * (n + m) + 30;
+    const float tl = tol > 0 ? (float)tol : 1e-6f;
+    rc = launch_zf(batch, n, m, (const float*)Hw, sH, (const float*)fw, n, (const float*)lb,
+                   strideLb, (const float*)ub, strideUb, (float*)z, (float*)y, status, P.cnt,
+                   P.list, mi, mpc_refine(), tl, d, st);
+    if (rc == MPCQP_OK) rc = fallback_f64();
+    if (rc != MPCQP_OK) return rc;
+    if (X)
+      rc = launch_states<float>(batch, nx, nu, N, tv, A, strideA, Bm, strideB, c, strideC, x0,
+                                strideX0, z, X, st);
+    return rc;
+  }
   void* hl = sbox ? w + L.hl : nullptr;
   void* hu = sbox ? w + L.hu : nullptr;
   if (sbox) {
@@ -240,53 +306,13 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
                          (const float*)xhi, strideXb, (const float*)xbw, (float*)hl, (float*)hu);
     MPCQP_CHECK_LAUNCH("rows_kernel");
   }
-  const size_t qpb = qp_ws_bytes(dtype, batch, n, m);
-  const int64_t sH = (int64_t)n * (n + 1) / 2, sG = (int64_t)m * n;
   if (qpb > 0) {
-    PfDyn d{};
-    const bool dyn_ok = mpc_dyn() && dyn_nxp(nx, nu) > 0 && dyn_chunk_stages(nx, nu, N) >= 1;
-    if (dyn_ok) {
-      d.nx = nx; d.nu = nu; d.N = N; d.tv = tv;
-      d.A = (const float*)A; d.sA = strideA;
-      d.B = (const float*)Bm; d.sB = strideB;
-      d.c = (const float*)c; d.sC = strideC;
-      d.x0 = (const float*)x0; d.sX0 = strideX0;
-      d.Q = (const float*)Q; d.sQ = strideQ;
-      d.R = (const float*)R; d.sR = strideR;
-      d.Qf = (const float*)Qf; d.sQf = strideQf;
-      d.xlo = (const float*)xlo; d.xhi = (const float*)xhi; d.sXb = strideXb;
-    }
-    // An instance the product-form kernel hands back -- more than 64 active
-    // constraints, a non-finite state, or (DYN) a refined point it could not
-    // certify as the QP's KKT point -- is solved again by the stage-wise fp64
-    // interior point with its exact polish (status bit
-    // MPCQP_STATUS_POLISHED), on the same inputs; it never returns OPTIMAL
-    // from the fp32 path uncertified.  The fallback runs over the whole batch
-    // with every other instance skipped, its workspace over the (then dead)
-    // condensed data.
-    const QpWsParts P = qp_ws_parts(w + L.qp, batch, n, m);
-    const size_t ipmb = ipm_supported(nx, nu) ? ipm_ws_bytes(batch, nx, nu, N) : 0;
-    const bool f64_fb = dyn_ok && mpc_fallback_f64() && ipmb > 0 &&
-                        ws_bytes >= mpc_fallback_bytes(batch, L.total, ipmb);
     // a missing side of the state box has no finite bound: no row can be
     // active on it, so the residual never reads it
     rc = solve_two_kernel(batch, n, m, Hw, sH, fw, n, Gw, sG, hl, hu, m, lb, strideLb, ub,
                           strideUb, z, y, status, max_iter, tol, w + L.qp, st,
                           dyn_ok ? &d : nullptr, dyn_ok ? mpc_refine() : -1, f64_fb ? 0 : 1);
-    if (rc == MPCQP_OK && f64_fb) {
-      int32_t* skip = (int32_t*)(w + mpc_skip_offset(L.total, ipmb));
-      const dim3 blk(256);
-      hipLaunchKernelGGL(skip_all_kernel, dim3((unsigned)((batch + 255) / 256)), blk, 0, st, batch,
-                         skip);
-      MPCQP_CHECK_LAUNCH("skip_all_kernel");
-      hipLaunchKernelGGL(unskip_list_kernel, dim3((unsigned)((batch + 255) / 256)), blk, 0, st,
-                         P.cnt, P.list, skip);
-      MPCQP_CHECK_LAUNCH("unskip_list_kernel");
-      rc = mpc_ipm_impl(MPCQP_F32, batch, nx, nu, N, flags & MPCQP_TV, A, strideA, Bm, strideB, Q,
-                        strideQ, R, strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi,
-                        strideXb, lb, strideLb, ub, strideUb, nullptr, 0, nullptr, 0, nullptr, 0, z,
-                        y, nullptr, nullptr, nullptr, status, skip, 1, 0, 0.0, w, ipmb, st);
-    }
+    if (rc == MPCQP_OK && f64_fb) rc = fallback_f64();
   } else if (m == 0) {  // input box only: the wavefront box kernels
     rc = mpcqp_solve_box(dtype, batch, n, Hw, sH, fw, n, lb, strideLb, ub, strideUb, z, status,
                          max_iter, tol, stream);

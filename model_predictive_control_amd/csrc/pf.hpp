@@ -64,6 +64,13 @@ __host__ __device__ inline int dyn_nxp(int nx, int nu) {
   return w <= 4 ? 4 : (w <= 8 ? 8 : (w <= 12 ? 12 : (w <= 16 ? 16 : 0)));
 }
 
+// solve_zf.hip: the z-space product form with H^-1 on chip (fp32, DYN only)
+bool zf_supported(int n, int m, int nx, int nu, int N);
+int launch_zf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
+              const float* lb, int64_t sLb, const float* ub, int64_t sUb, float* z, float* y,
+              int32_t* status, int* retry_count, int* retry_list, int max_iter, int refine,
+              float tol, const PfDyn& dyn, hipStream_t st);
+
 int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
               const float* G, int64_t sG, const float* hl, const float* hu, int64_t sh,
               const float* lb, int64_t sLb, const float* ub, int64_t sUb, const float* M0,

@@ -1,0 +1,822 @@
+// solve_zf.hip -- the per-step QP of the state-box MPC (MPCController.solve,
+// session_4/main.py:115-116 on the OCP of main.py:41-113: input box
+// main.py:68-69, state box main.py:58-61) in fp32, n = N nu <= 64 inputs
+// (BASELINE config 3: N = 30, nu = 2), by a dual active set (Goldfarb-Idnani)
+// in product form over the INPUTS only, with everything it iterates on held on
+// chip.  One QP instance per wavefront.
+//
+// The dense path (sweep.hip -> solve_pf.hip) works in the (n + m)-dimensional
+// KKT space: it writes the swept matrix M0 ((n+m)^2 floats, 130 KB per
+// config-3 instance) and re-reads its columns every iteration, so both
+// kernels are bound by HBM round trips.  Here the constraints are kept as
+// normals in z-space: a bound z_i >= lb_i has n = e_i, a state row
+// x_j(z) >= xlo_j has n = Gamma_j (row j of the condensed Gamma); upper sides
+// are negated.  With the working set P (normals N_P, multipliers u >= 0) and
+// S = N_P' H^-1 N_P, adding a violated constraint p (slack s_p < 0) moves
+//     z += t dz,  u -= t r,  u_p += t,     dz = H^-1 (n_p - N_P r),
+//     r = S^-1 N_P' H^-1 n_p,  s_p grows by sigma = n_p' dz per unit t,
+// with the full step t2 = -s_p / sigma and the partial (dual) step t1 =
+// min u_s / r_s over r_s > 0 (a blocking constraint is dropped), S^-1 updated
+// by a bordered rank-1 step (add) or a Schur rank-1 step (drop).  Every
+// product is with H^-1 (n x n, one row per lane in registers: a lane-local
+// 64-FMA dot with a broadcast vector) or S^-1 (one slot per lane, as in
+// solve_pf.hip): no memory traffic in the iteration at all.
+//
+// The state rows are checked lazily: the z bounds are scanned every
+// iteration; when none is violated the states x(z) are rolled out through
+// the dynamics (fp64, pfdyn.hpp) and the most violated row enters; its normal
+// Gamma_j comes from the adjoint recursion over the stages (on chip).  Any
+// violated constraint may enter a dual active set, so this order keeps its
+// convergence.  H^-1 is computed in the kernel from the condensed H by a
+// symmetric Gauss-Jordan sweep (rows in registers, the pivot row through
+// LDS), so the step reads H, f and the dynamics and writes z, y, status.
+//
+// Refinement and certificate as in solve_pf.hip: the KKT residual of the
+// working set from the dynamics in fp64, Newton corrections in product form
+// (float pairs), the exact certificate (primal rows from the fp64 rollout,
+// dual signs from the exact gradient), releases of wrong-signed constraints,
+// and an uncertified instance handed to the fp64 interior point
+// (kStatusRetry).
+#include <cstdlib>
+
+#include "pfdyn.hpp"
+
+namespace mpcqp {
+
+struct ZfArgs {
+  int batch, n, m;
+  const float* H; int64_t sH;   // packed lower n x n
+  const float* f; int64_t sf;
+  const float* lb; int64_t sLb;
+  const float* ub; int64_t sUb;
+  float* z; float* y; int32_t* status;
+  int* retry_count; int* retry_list;
+  int max_iter, refine;
+  float tol, dyn_stop;
+  PfDyn d;
+};
+
+constexpr int kZfRowBufs = 16;  // normals of active state rows held in LDS
+
+__device__ __forceinline__ float wave_sum(float v) {
+  v += lane_step<1>(v);
+  v += lane_step<2>(v);
+  v += lane_step<4>(v);
+  v += lane_step<8>(v);
+  v += lane_step<16>(v);
+  v += lane_step<32>(v);
+  return v;
+}
+
+template <int NXP>
+__global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
+  constexpr int NR = 3;  // the (n + m) index space of the dynamics residual: n <= 64, m <= 128
+  constexpr int kExtD = NR * kWave / 2;
+  __shared__ double pool[kPool + kExtD];  // DYN layout, then the low parts (floats)
+  __shared__ __attribute__((aligned(16))) float pubA[kWave];
+  __shared__ __attribute__((aligned(16))) float pubB[kWave];
+  __shared__ __attribute__((aligned(16))) float sx[kSlots];
+  __shared__ __attribute__((aligned(16))) float nrm[kZfRowBufs][kWave];
+  __shared__ float r0[2 * kWave];   // x_j(z0): the rows at the unconstrained minimiser
+  __shared__ float rmu[2 * kWave];  // signed row multipliers by row (residual input)
+  __shared__ float ew[2 * kWave];   // row residuals by row (refinement)
+  __shared__ float zmu[kWave];      // signed bound multipliers by z index
+  __shared__ int rst[2 * kWave];    // row status: 0 inactive, 1 at xlo, 2 at xhi
+  const int b = blockIdx.x, l = threadIdx.x;
+  const int n = a.n, m = a.m, nt = n + m;
+  const PfDyn& d = a.d;
+  const int nx = d.nx;
+  const float inf = Lim<float>::inf();
+  float* ext = reinterpret_cast<float*>(pool + kPool);
+  const float* xlo = d.xlo ? d.xlo + (int64_t)b * d.sXb : nullptr;
+  const float* xhi = d.xhi ? d.xhi + (int64_t)b * d.sXb : nullptr;
+
+  // ------------------------------------------------------------ per z index
+  const bool zl_ok = l < n;
+  float zlo = -inf, zhi = inf, fl = 0.f;
+  if (zl_ok) {
+    if (a.lb) zlo = a.lb[(int64_t)b * a.sLb + l];
+    if (a.ub) zhi = a.ub[(int64_t)b * a.sUb + l];
+    fl = a.f[(int64_t)b * a.sf + l];
+  }
+  const float zsl = finite(zlo) ? 1.f / (1.f + fabsf(zlo)) : 0.f;
+  const float zsu = finite(zhi) ? 1.f / (1.f + fabsf(zhi)) : 0.f;
+  bool bad = zl_ok && (!(zlo <= zhi) || zlo == inf || zhi == -inf);
+  bool nonfin = !finite(fl);
+  for (int j = l; j < 2 * kWave; j += kWave) {
+    rst[j] = 0;
+    rmu[j] = 0.f;
+    ew[j] = 0.f;
+    if (j < m) {
+      const float lo = xlo ? xlo[j] : -inf, hi = xhi ? xhi[j] : inf;
+      bad |= !(lo <= hi) || lo == inf || hi == -inf;
+    }
+  }
+  zmu[l] = 0.f;
+  int code = MPCQP_STATUS_OPTIMAL, iters = 0;
+  if (__builtin_amdgcn_ballot_w64(nonfin)) code = MPCQP_STATUS_NONFINITE;
+  else if (__builtin_amdgcn_ballot_w64(bad)) code = MPCQP_STATUS_INFEASIBLE;
+  float Hi[kWave];  // row l of H^-1 (rows/columns >= n: identity)
+  float Srow[kSlots];  // row l of S^-1 (slot l); zeroed once H^-1 is formed
+  float z = 0.f, z0 = 0.f;
+  int zst = zl_ok ? 0 : 3;
+  // slot state (lane = slot): type -1 empty, 0 bound (z index sidx), 1 row (row
+  // index sidx, normal buffer sbuf); ssgn +1 lower side, -1 upper side; su >= 0
+  int stype = -1, sidx = 0, sbuf = 0;
+  float ssgn = 1.f, su = 0.f, sul = 0.f;
+  uint64_t used = 0;
+  unsigned bufs = 0;
+  int loaded = -1;
+  if (code != MPCQP_STATUS_OPTIMAL) goto out;
+
+  {
+    // ----------------------------------------------------- H^-1 on chip
+    // packed H into LDS (the pool is free until the dynamics are loaded)
+    {
+      float* Hp = reinterpret_cast<float*>(pool);
+      const int nh = n * (n + 1) / 2;
+      lds_copy3(Hp, a.H + (int64_t)b * a.sH, nh, nullptr, 0, nullptr, 0, l);
+      wave_lds_sync();
+#pragma unroll
+      for (int k = 0; k < kWave; ++k) {
+        const int hi_ = l > k ? l : k, lo_ = l > k ? k : l;
+        const bool in = l < n && k < n;
+        Hi[k] = in ? Hp[hi_ * (hi_ + 1) / 2 + lo_] : (l == k ? 1.f : 0.f);
+        nonfin |= !finite(Hi[k]);
+      }
+      wave_lds_sync();
+    }
+    if (__builtin_amdgcn_ballot_w64(nonfin)) {
+      code = MPCQP_STATUS_NONFINITE;
+      goto out;
+    }
+    // symmetric sweep of every pivot: M = SWEEP(H) = -H^-1.  Pivot k: row k
+    // (= column k) through LDS; M[i][j] -= M[i][k] M[k][j] / M[k][k],
+    // M[i][k] = M[k][i] = M[i][k] / M[k][k], M[k][k] = -1 / M[k][k]
+    for (int k = 0; k < n; ++k) {
+      wave_lds_sync();
+      if (l == k) {
+#pragma unroll
+        for (int j4 = 0; j4 < kWave / 4; ++j4)
+          *reinterpret_cast<float4*>(&pubA[4 * j4]) =
+              float4{Hi[4 * j4], Hi[4 * j4 + 1], Hi[4 * j4 + 2], Hi[4 * j4 + 3]};
+      }
+      wave_lds_sync();
+      const float dkk = pubA[k];
+      if (!(dkk > 0.f)) {  // H not positive definite (in fp32)
+        code = MPCQP_STATUS_NOT_CONVEX;
+        goto out;
+      }
+      const float inv = 1.f / dkk;
+      const float c = pubA[l] * inv;
+      const bool me = l == k;
+#pragma unroll
+      for (int j4 = 0; j4 < kWave / 4; ++j4) {
+        const float4 pk = *reinterpret_cast<const float4*>(&pubA[4 * j4]);
+        const float pj[4] = {pk.x, pk.y, pk.z, pk.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = 4 * j4 + e;
+          float v = me ? pj[e] * inv : fmaf(-c, pj[e], Hi[j]);
+          v = (j == k) ? (me ? -inv : c) : v;
+          Hi[j] = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kWave; ++j) Hi[j] = -Hi[j];  // H^-1
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) Srow[j] = 0.f;
+    // lane-local products with H^-1: out_l = sum_j Hi[j] v_j, v broadcast
+    auto hmul = [&](const float* v) __attribute__((always_inline)) -> float {
+      float acc = 0.f;
+#pragma unroll
+      for (int j4 = 0; j4 < kWave / 4; ++j4) {
+        const float4 vv = *reinterpret_cast<const float4*>(&v[4 * j4]);
+        acc = fmaf(Hi[4 * j4], vv.x, acc);
+        acc = fmaf(Hi[4 * j4 + 1], vv.y, acc);
+        acc = fmaf(Hi[4 * j4 + 2], vv.z, acc);
+        acc = fmaf(Hi[4 * j4 + 3], vv.w, acc);
+      }
+      return acc;
+    };
+    // z0 = -H^-1 f
+    wave_lds_sync();
+    pubA[l] = zl_ok ? fl : 0.f;
+    wave_lds_sync();
+    z0 = zl_ok ? -hmul(pubA) : 0.f;
+    z = z0;
+
+    // ----------------------------------------------------- helpers
+    auto bcast_slots = [&](float t) __attribute__((always_inline)) {
+      wave_lds_sync();
+      sx[l] = t;
+      wave_lds_sync();
+    };
+    auto smul = [&](float t) __attribute__((always_inline)) -> float {  // (S^-1 t)_l
+      bcast_slots(t);
+      float q = 0.f;
+#pragma unroll
+      for (int j4 = 0; j4 < kSlots / 4; ++j4) {
+        const float4 tv = *reinterpret_cast<const float4*>(&sx[4 * j4]);
+        q = fmaf(Srow[4 * j4 + 0], tv.x, q);
+        q = fmaf(Srow[4 * j4 + 1], tv.y, q);
+        q = fmaf(Srow[4 * j4 + 2], tv.z, q);
+        q = fmaf(Srow[4 * j4 + 3], tv.w, q);
+      }
+      return q;
+    };
+    auto s_add = [&](float w, float sigma) __attribute__((always_inline)) {
+      const float wi = w / sigma;
+      bcast_slots(w);
+#pragma unroll
+      for (int j4 = 0; j4 < kSlots / 4; ++j4) {
+        const float4 wv = *reinterpret_cast<const float4*>(&sx[4 * j4]);
+        Srow[4 * j4 + 0] = fmaf(wi, wv.x, Srow[4 * j4 + 0]);
+        Srow[4 * j4 + 1] = fmaf(wi, wv.y, Srow[4 * j4 + 1]);
+        Srow[4 * j4 + 2] = fmaf(wi, wv.z, Srow[4 * j4 + 2]);
+        Srow[4 * j4 + 3] = fmaf(wi, wv.w, Srow[4 * j4 + 3]);
+      }
+    };
+    // drop slot q: S^-1 -= S^-1[:,q] S^-1[q,:] / S^-1[q][q]; row/column q zero
+    auto s_drop = [&](int q) __attribute__((always_inline)) -> bool {
+      wave_lds_sync();
+      if (l == q) {
+#pragma unroll
+        for (int j4 = 0; j4 < kSlots / 4; ++j4)
+          *reinterpret_cast<float4*>(&sx[4 * j4]) =
+              float4{Srow[4 * j4], Srow[4 * j4 + 1], Srow[4 * j4 + 2], Srow[4 * j4 + 3]};
+      }
+      wave_lds_sync();
+      const float dqq = sx[q];
+      if (!(dqq > 0.f)) return false;
+      const float c = -sx[l] / dqq;
+#pragma unroll
+      for (int j4 = 0; j4 < kSlots / 4; ++j4) {
+        const float4 rv = *reinterpret_cast<const float4*>(&sx[4 * j4]);
+        const float r4[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = 4 * j4 + e;
+          Srow[j] = (l == q || j == q) ? 0.f : fmaf(c, r4[e], Srow[j]);
+        }
+      }
+      return true;
+    };
+    // b_s = n_s' v for every slot (v published in pubB by the caller)
+    auto slot_dots = [&]() __attribute__((always_inline)) -> float {
+      float bs = 0.f;
+      if (stype == 0) {
+        bs = ssgn * pubB[sidx];
+      } else if (stype == 1) {
+        const float* nv = nrm[sbuf];
+        float acc = 0.f;
+#pragma unroll
+        for (int j4 = 0; j4 < kWave / 4; ++j4) {
+          const float4 a4 = *reinterpret_cast<const float4*>(&nv[4 * j4]);
+          const float4 v4 = *reinterpret_cast<const float4*>(&pubB[4 * j4]);
+          acc = fmaf(a4.x, v4.x, fmaf(a4.y, v4.y, fmaf(a4.z, v4.z, fmaf(a4.w, v4.w, acc))));
+        }
+        bs = ssgn * acc;
+      }
+      return bs;
+    };
+    // (N_P c)_l into pubA: bound slots scatter, row slots add c_s n_s
+    auto nmul = [&](float cs) __attribute__((always_inline)) {
+      wave_lds_sync();
+      pubA[l] = 0.f;
+      wave_lds_sync();
+      if (stype == 0) pubA[sidx] = ssgn * cs;  // distinct z indices
+      uint64_t rows = __builtin_amdgcn_ballot_w64(stype == 1);
+      float acc = 0.f;
+      while (rows) {
+        const int s = __builtin_ctzll(rows);
+        rows &= rows - 1;
+        const float coef = readlane(ssgn * cs, s);
+        const int bb = readlane(sbuf, s);
+        acc = fmaf(coef, nrm[bb][l], acc);
+      }
+      wave_lds_sync();
+      pubA[l] += acc;
+      wave_lds_sync();
+    };
+    // row normal Gamma_j (x_j = x_{s+1}[c] with j = s nx + c) into buffer bb,
+    // by the adjoint recursion over the resident stages (fp32, every lane
+    // runs it; lane k*nu + a keeps dx_{s+1}[c] / du_k[a])
+    auto row_normal = [&](int j, int bb) __attribute__((always_inline)) {
+      const DynChunk C = dyn_chunk(d, pool);
+      const int nu = d.nu;
+      const int s = j / nx, cc = j - s * nx;
+      float lam[NXP];
+#pragma unroll
+      for (int q = 0; q < NXP; ++q) lam[q] = (q == cc) ? 1.f : 0.f;
+      float mine = 0.f;
+      for (int k = s; k >= 0; --k) {
+        const float* Ak = C.A(k);
+        const float* Bk = C.B(k);
+        const int kk = l - k * nu;  // this lane's input offset in stage k
+#pragma unroll
+        for (int q = 0; q < NXP; ++q) {
+          if (q < nu) {
+            float o = 0.f;
+#pragma unroll
+            for (int r = 0; r < NXP; ++r)
+              if (r < nx) o = fmaf(Bk[r * nu + q], lam[r], o);
+            mine = (kk == q) ? o : mine;
+          }
+        }
+        float ln[NXP];
+#pragma unroll
+        for (int q = 0; q < NXP; ++q) {
+          float o = 0.f;
+#pragma unroll
+          for (int r = 0; r < NXP; ++r)
+            if (r < nx && q < nx) o = fmaf(Ak[r * nx + q], lam[r], o);
+          ln[q] = o;
+        }
+#pragma unroll
+        for (int q = 0; q < NXP; ++q) lam[q] = ln[q];
+      }
+      wave_lds_sync();
+      nrm[bb][l] = l < n ? mine : 0.f;
+      wave_lds_sync();
+    };
+    // fp64 rollout of the current z -> X (pool); the stage data are resident
+    // after the first (setup) rollout
+    auto rollout = [&](bool with_ext) __attribute__((always_inline)) {
+      float x[NR], wdummy[NR];
+      int stv[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        x[r] = (r == 0 && zl_ok) ? z : 0.f;
+        stv[r] = 0;
+        wdummy[r] = 0.f;
+      }
+      if (!with_ext) {
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) ext[l + kWave * r] = 0.f;
+      }
+      dyn_residual<NR, NXP, true, true>(d, b, n, m, l, x, ext, stv, pool, loaded, wdummy);
+    };
+    const double* Xr = pool + kDynX + nx;  // x_1..x_N (rows j = s nx + c)
+
+    // the dynamics into LDS (resident from here on) and the rows at z0
+    // (refresh needs them)
+    {
+      float x[NR], wdummy[NR];
+      int stv[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        x[r] = (r == 0 && zl_ok) ? z0 : 0.f;
+        stv[r] = 0;
+        wdummy[r] = 0.f;
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int r = 0; r < NR; ++r) ext[l + kWave * r] = 0.f;
+      dyn_residual<NR, NXP, true>(d, b, n, m, l, x, ext, stv, pool, loaded, wdummy);
+      for (int j = l; j < m; j += kWave) r0[j] = (float)Xr[j];
+    }
+    wave_lds_sync();
+
+    // refresh: the equality-QP solution of the working set from z0:
+    // u = S^-1 c, c_s = -(n_s' z0 - b_s); z = z0 + H^-1 N_P u
+    auto refresh = [&]() __attribute__((always_inline)) {
+      float cs = 0.f;
+      wave_lds_sync();
+      pubB[l] = z0;
+      wave_lds_sync();
+      // bound slot: c = -ssgn (z0_i - bound_i); row slot: -ssgn (x_j(z0) - bound_j)
+      if (stype == 0) {
+        const float z0i = pubB[sidx];
+        const float bi = ssgn > 0.f ? (a.lb ? a.lb[(int64_t)b * a.sLb + sidx] : -inf)
+                                    : (a.ub ? a.ub[(int64_t)b * a.sUb + sidx] : inf);
+        cs = -ssgn * (z0i - bi);
+      } else if (stype == 1) {
+        const float bj = ssgn > 0.f ? xlo[sidx] : xhi[sidx];
+        cs = -ssgn * (r0[sidx] - bj);
+      }
+      const float us = smul(cs);
+      su = stype >= 0 ? us : 0.f;
+      sul = 0.f;
+      nmul(su);
+      const float dzv = hmul(pubA);
+      z = (zst == 0) ? z0 + dzv : (zst == 1 ? zlo : (zst == 2 ? zhi : 0.f));
+    };
+
+    // ------------------------------------------------- the dual active set
+    const float dep_tol = 1e-6f;
+    bool gi_skip = false;
+    for (int round = 0; round < kDynRounds; ++round) {
+      if (!gi_skip) {
+        while (true) {
+          // the most violated free z bound
+          float viol = -inf;
+          {
+            const float vl = (zlo - z) * zsl, vu = (z - zhi) * zsu;
+            float v = (zst == 0) ? fmaxf(vl, vu) : -inf;
+            viol = (v == v) ? v : -inf;
+          }
+          int p = l;
+          wave_argmax(viol, p);
+          p = uniform(p);
+          viol = readlane(viol, 0);
+          bool isrow = false;
+          int pj = 0, side = 0;
+          float sp = 0.f;
+          const float tolc = round > 0 ? kDynTol : a.tol;
+          if (viol > tolc) {
+            const float zp = readlane(z, p);
+            const float lop = readlane(zlo, p), hip = readlane(zhi, p);
+            side = (zp < lop) ? 1 : 2;
+            sp = side == 1 ? zp - lop : hip - zp;
+          } else if (m > 0) {
+            // lazy row check: roll the states out at the current z
+            rollout(false);
+            float rv = -inf;
+            int rj = 0;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+              const int j = l + kWave * r;
+              if (j < m && rst[j] == 0) {
+                const double xv = Xr[j];
+                const float lo = xlo ? xlo[j] : -inf, hi = xhi ? xhi[j] : inf;
+                const float el = finite(lo) ? (float)((double)lo - xv) / (1.f + fabsf(lo)) : -inf;
+                const float eh = finite(hi) ? (float)(xv - (double)hi) / (1.f + fabsf(hi)) : -inf;
+                const float v = fmaxf(el, eh);
+                if (v > rv) {
+                  rv = v;
+                  rj = j;
+                }
+              }
+            }
+            wave_argmax(rv, rj);
+            rj = uniform(rj);
+            rv = readlane(rv, 0);
+            if (!(rv > tolc)) break;  // optimal on the current working set
+            isrow = true;
+            pj = rj;
+            const double xv = Xr[pj];
+            const float lo = xlo ? xlo[pj] : -inf, hi = xhi ? xhi[pj] : inf;
+            side = (finite(lo) && xv < (double)lo) ? 1 : 2;
+            sp = side == 1 ? (float)(xv - (double)lo) : (float)((double)hi - xv);
+          } else {
+            break;
+          }
+          const float psgn = side == 1 ? 1.f : -1.f;
+          int pb = 0;
+          if (isrow) {
+            if (bufs == (1u << kZfRowBufs) - 1) {
+              code = kStatusRetry;
+              goto out;
+            }
+            pb = __builtin_ctz(~bufs);
+            row_normal(pj, pb);
+          }
+          // a = H^-1 n_p
+          float av;
+          if (!isrow) {
+            wave_lds_sync();
+            if (l == p) {
+#pragma unroll
+              for (int j4 = 0; j4 < kWave / 4; ++j4)
+                *reinterpret_cast<float4*>(&pubA[4 * j4]) =
+                    float4{Hi[4 * j4], Hi[4 * j4 + 1], Hi[4 * j4 + 2], Hi[4 * j4 + 3]};
+            }
+            wave_lds_sync();
+            av = psgn * pubA[l];
+          } else {
+            av = psgn * hmul(nrm[pb]);
+          }
+          // n_p' a
+          const float npa = isrow ? psgn * wave_sum(nrm[pb][l] * av) : psgn * readlane(av, p);
+          float tau = 0.f;
+          bool added = false;
+          while (!added) {
+            if (++iters > a.max_iter) {
+              code = MPCQP_STATUS_MAXITER;
+              goto out;
+            }
+            wave_lds_sync();
+            pubB[l] = av;
+            wave_lds_sync();
+            const float bs = slot_dots();
+            const float rs = smul(bs);
+            nmul(rs);
+            const float dz = (zst == 0) ? av - hmul(pubA) : 0.f;
+            const float sig = isrow ? psgn * wave_sum(zl_ok ? nrm[pb][l] * dz : 0.f)
+                                    : psgn * readlane(dz, p);
+            const bool dep = !(sig > dep_tol * npa);
+            const float t2 = dep ? inf : -sp / sig;
+            float t1 = (stype >= 0 && rs > 0.f) ? su / rs : inf;
+            t1 = (t1 == t1) ? t1 : inf;
+            int k = l;
+            wave_argmin(t1, k);
+            k = uniform(k);
+            t1 = readlane(t1, 0);
+            if (!(t1 < inf) && !(t2 < inf)) {
+              code = MPCQP_STATUS_INFEASIBLE;
+              goto out;
+            }
+            const bool partial = t1 < t2;
+            const float t = partial ? t1 : t2;
+            z = (zst == 0) ? fmaf(t, dz, z) : z;
+            su = (stype >= 0) ? fmaxf(fmaf(-t, rs, su), 0.f) : su;
+            tau += t;
+            sp = fmaf(t, sig, sp);
+            if (partial) {
+              // slot k leaves the working set
+              const int kt = readlane(stype, k), ki = readlane(sidx, k), kb = readlane(sbuf, k);
+              if (!s_drop(k)) {
+                code = MPCQP_STATUS_NOT_CONVEX;
+                goto out;
+              }
+              used &= ~(1ull << k);
+              if (kt == 0 && l == ki) zst = 0;
+              if (kt == 1) {
+                if (l == 0) rst[ki] = 0;
+                bufs &= ~(1u << kb);
+              }
+              if (l == k) {
+                stype = -1;
+                su = 0.f;
+              }
+            } else {
+              // p joins the working set: w = [-r; 1] / sigma
+              if (!(sig > 0.f)) {
+                code = MPCQP_STATUS_NOT_CONVEX;
+                goto out;
+              }
+              if (~used == 0) {
+                code = kStatusRetry;
+                goto out;
+              }
+              const int snew = __builtin_ctzll(~used);
+              s_add((l == snew) ? 1.f : -rs, sig);
+              used |= 1ull << snew;
+              if (l == snew) {
+                stype = isrow ? 1 : 0;
+                sidx = isrow ? pj : p;
+                sbuf = pb;
+                ssgn = psgn;
+                su = tau;
+                sul = 0.f;
+              }
+              if (!isrow && l == p) {
+                zst = side;
+                z = side == 1 ? zlo : zhi;
+              }
+              if (isrow) {
+                if (l == 0) rst[pj] = side;
+                bufs |= 1u << pb;
+              }
+              added = true;
+            }
+          }
+        }
+      }
+      gi_skip = false;
+      if (a.refine <= 0) break;
+
+      // ------------------------------------------ refinement + certificate
+      // residual input: z (free: float pair), signed row multipliers
+      // mu_j = -ssgn u (lower: -u, upper: +u) by row; bound multipliers by z
+      auto publish_mults = [&]() __attribute__((always_inline)) {
+        wave_lds_sync();
+        zmu[l] = 0.f;
+        wave_lds_sync();
+        if (stype == 0) zmu[sidx] = ssgn * su;
+        if (stype == 1) {
+          rmu[sidx] = -ssgn * su;
+          ext[n + sidx] = -ssgn * sul;
+        }
+        wave_lds_sync();
+      };
+      {
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) ext[l + kWave * r] = 0.f;
+        for (int j = l; j < m; j += kWave) rmu[j] = 0.f;
+        wave_lds_sync();
+      }
+      float zl_ext = 0.f;  // low part of z (free z)
+      bool decided = false;
+      float prev = inf, r_prev = inf;
+      float pv = -inf, dv = -inf;
+      int dk = 0;
+      const double* gx = pool + kDynXd;
+      for (int it = 0;; ++it) {
+        publish_mults();
+        if (zl_ok) ext[l] = zst == 0 ? zl_ext : 0.f;
+        float x[NR], w[NR];
+        int stv[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int i = l + kWave * r;
+          if (i < n) {
+            x[r] = z;
+            stv[r] = zst;
+          } else if (i < nt) {
+            x[r] = rmu[i - n];
+            stv[r] = rst[i - n];
+          } else {
+            x[r] = 0.f;
+            stv[r] = 3;
+          }
+        }
+        dyn_residual<NR, NXP, false, true>(d, b, n, m, l, x, ext, stv, pool, loaded, w);
+        // stationarity rho = g - N_P u on z; active-row residuals by row
+        const float g = zl_ok ? (float)gx[l] : 0.f;
+        const float rho = zl_ok ? (zst == 0 ? g : g - zmu[l]) : 0.f;
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int i = l + kWave * r;
+          if (i >= n && i < nt) ew[i - n] = w[r];
+        }
+        wave_lds_sync();
+        float rn = fabsf(rho);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int i = l + kWave * r;
+          if (i >= n && i < nt) rn = fmaxf(rn, fabsf(w[r]));
+        }
+        rn = wave_max(rn);
+        if (it > 0) {
+          const float tau = 10.f * rn;
+          float pvm = -inf, dvm = -inf;
+          pv = -inf;
+          dv = -inf;
+          dk = -1;  // encoded: z index i -> i, row j -> 64 + j (slot found below)
+          // free z: primal; fixed z: dual sign of the exact multiplier (g)
+          if (zl_ok) {
+            if (zst == 0) {
+              const float vl = (zlo - z) * zsl, vu = (z - zhi) * zsu;
+              pv = fmaxf(vl, vu);
+              pvm = fmaxf(vl + tau * zsl, vu + tau * zsu);
+            } else {
+              const float wg = (zst == 1) ? -g : g;  // > 0: wrong sign
+              dv = wg - kDualTol * (1.f + fabsf(fl));
+              dvm = wg + tau;
+              dk = l;
+            }
+          }
+          // rows: inactive primal from X, active multipliers
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const int j = l + kWave * r;
+            if (j < m) {
+              if (rst[j] == 0) {
+                const double xv = Xr[j];
+                const float lo = xlo ? xlo[j] : -inf, hi = xhi ? xhi[j] : inf;
+                const float sl = finite(lo) ? 1.f / (1.f + fabsf(lo)) : 0.f;
+                const float su_ = finite(hi) ? 1.f / (1.f + fabsf(hi)) : 0.f;
+                const float el = finite(lo) ? (float)((double)lo - xv) : -inf;
+                const float eh = finite(hi) ? (float)(xv - (double)hi) : -inf;
+                const float pp = fmaxf(el * sl, eh * su_);
+                pv = fmaxf(pv, pp == pp ? pp : -inf);
+                const float pm = fmaxf((el + tau) * sl, (eh + tau) * su_);
+                pvm = fmaxf(pvm, pm == pm ? pm : -inf);
+              } else {
+                const float u = (rst[j] == 1 ? -1.f : 1.f) * rmu[j];  // u >= 0
+                const float dd = -u - kDualTol;
+                if (dd > dv) {
+                  dv = dd;
+                  dk = kWave + j;
+                }
+                dvm = fmaxf(dvm, -u + tau);
+              }
+            }
+          }
+          pv = wave_max(pv);
+          pvm = wave_max(pvm);
+          dvm = wave_max(dvm);
+          wave_argmax(dv, dk);
+          dk = uniform(dk);
+          dv = readlane(dv, 0);
+          const bool clear = !(pvm > kDynTol) && !(dvm > 0.f);
+          const bool fails = pv > kDynTol + tau || dv > tau;
+          const bool contracting = !(rn > 1e-3f * r_prev);
+          const bool converged = !(prev > a.dyn_stop);
+          if ((contracting && (clear || fails)) || converged) {
+            decided = true;
+            break;
+          }
+        }
+        if (it >= a.refine) break;
+        // Newton correction on the working set (product form):
+        //   a = H^-1 rho, b_s = n_s' a - e_s, du = S^-1 b, dz = H^-1 N_P du - a
+        wave_lds_sync();
+        pubA[l] = rho;
+        wave_lds_sync();
+        const float ar = zl_ok ? hmul(pubA) : 0.f;
+        wave_lds_sync();
+        pubB[l] = ar;
+        wave_lds_sync();
+        float bs = slot_dots();
+        if (stype == 1) bs -= ssgn * ew[sidx];
+        const float du = smul(stype >= 0 ? bs : 0.f);
+        nmul(du);
+        const float dzv = (zst == 0) ? hmul(pubA) - ar : 0.f;
+        float dmax = 0.f;
+        if (zst == 0) {
+          const double xf = (double)z + (double)zl_ext + (double)dzv;
+          const float xh = (float)xf;
+          zl_ext = (float)(xf - (double)xh);
+          dmax = fabsf(dzv) / (1.f + fabsf(xh));
+          z = xh;
+        }
+        if (stype >= 0) {
+          const double uf = (double)su + (double)sul + (double)du;
+          const float uh = (float)uf;
+          sul = (float)(uf - (double)uh);
+          dmax = fmaxf(dmax, fabsf(du) / (1.f + fabsf(uh)));
+          su = uh;
+        }
+        prev = wave_max(dmax);
+        r_prev = rn;
+      }
+      if (code != MPCQP_STATUS_OPTIMAL) break;
+      if (decided && !(pv > kDynTol) && !(dv > 0.f)) break;  // certified
+      if (!decided || round + 1 >= kDynRounds) {
+        code = kStatusRetry;
+        break;
+      }
+      if (dv > 0.f) {
+        // release the worst wrong-signed constraint, refresh, refine first
+        const bool isz = dk < kWave;
+        const int key = isz ? dk : dk - kWave;
+        const int want = isz ? 0 : 1;
+        const int q = uniform(__builtin_ctzll(__builtin_amdgcn_ballot_w64(stype == want && sidx == key) | (1ull << 63)));
+        if (q == 63 && !(readlane(stype, 63) == want && readlane(sidx, 63) == key)) {
+          code = kStatusRetry;
+          break;
+        }
+        const int qb = readlane(sbuf, q);
+        if (!s_drop(q)) {
+          code = kStatusRetry;
+          break;
+        }
+        used &= ~(1ull << q);
+        if (isz && l == key) zst = 0;
+        if (!isz) {
+          if (l == 0) rst[key] = 0;
+          bufs &= ~(1u << qb);
+        }
+        if (l == q) {
+          stype = -1;
+          su = 0.f;
+          sul = 0.f;
+        }
+        wave_lds_sync();
+        refresh();
+        gi_skip = true;
+      }
+      // else: a primal violation; the next round's active set adds it
+    }
+    // a non-finite final state: the fp64 fallback
+    if (code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER) {
+      const bool nf = !finite(z) || !finite(su);
+      if (__builtin_amdgcn_ballot_w64(nf)) code = kStatusRetry;
+    }
+  }
+out:
+  {
+    const bool ok = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
+    if (code != kStatusRetry) {
+      if (zl_ok) a.z[(int64_t)b * n + l] = ok ? fminf(fmaxf(z, zlo), zhi) : __builtin_nanf("");
+      if (a.y) {
+        // row multipliers by row (> 0 at xhi): y_j = -ssgn u for row slots
+        wave_lds_sync();
+        for (int j = l; j < m; j += kWave) rmu[j] = 0.f;
+        wave_lds_sync();
+        if (stype == 1) rmu[sidx] = -ssgn * su;
+        wave_lds_sync();
+        for (int j = l; j < m; j += kWave) a.y[(int64_t)b * m + j] = ok ? rmu[j] : __builtin_nanf("");
+      }
+    }
+    if (l == 0) {
+      a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
+      if (code == kStatusRetry) a.retry_list[atomicAdd(a.retry_count, 1)] = b;
+    }
+  }
+}
+
+bool zf_supported(int n, int m, int nx, int nu, int N) {
+  return n <= kWave && m <= 2 * kWave && dyn_nxp(nx, nu) == 4 && dyn_chunk_stages(nx, nu, N) >= N;
+}
+
+int launch_zf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
+              const float* lb, int64_t sLb, const float* ub, int64_t sUb, float* z, float* y,
+              int32_t* status, int* retry_count, int* retry_list, int max_iter, int refine,
+              float tol, const PfDyn& dyn, hipStream_t st) {
+  ZfArgs a{batch, n, m, H, sH, f, sf, lb, sLb, ub, sUb, z, y, status, retry_count, retry_list,
+           max_iter, refine, tol, kDynStop, dyn};
+  if (const char* e = getenv("MPCQP_DYN_STOP")) a.dyn_stop = (float)atof(e);
+  hipLaunchKernelGGL((qp_zf_kernel<4>), dim3(batch), dim3(kWave), 0, st, a);
+  MPCQP_CHECK_LAUNCH("qp_zf_kernel");
+  return MPCQP_OK;
+}
+
+}  // namespace mpcqp
