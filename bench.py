@@ -780,7 +780,7 @@ class ConfigNLP:
         return {"workload": f"nlp: converged MPCController.solve (main.py controller, N={self.N}, "
                             f"ts=0.08, input + state box) by SQP on device, at most {self.iters} "
                             f"iterations per solve from U=0 (Gauss-Newton, then the exact "
-                            f"Hessian, convexified per stage), x0 ~ U(+-.8, +-.4, +-.5, +-.2); "
+                            f"Hessian, projected per stage after a non-convex QP), x0 ~ U(+-.8, +-.4, +-.5, +-.2); "
                             f"value counts only solves that reached KKT <= 1e-9",
                 "horizon": self.N, "nx": 4, "nu": 2, "sqp_iters": self.iters}
 

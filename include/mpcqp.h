@@ -359,7 +359,8 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
  *   X ((N+1) x 4), U (N x 2), pi (N x 4) per instance.
  * mpcqp_bicycle_sqp_step: per instance not yet MPCQP_SQP_DONE: step d = Z - U
  *   (Z the QP solution; an instance whose qp_status is not OPTIMAL takes no
- *   step: in exact-Hessian mode its damping mu grows x4, in Gauss-Newton mode
+ *   step: in exact-Hessian mode it switches to the projected curvature
+ *   (MPCQP_SQP_PROJ) and, if that QP fails too, its damping mu grows x4; in Gauss-Newton mode
  *   three failures in a row stop it with flags DONE | MPCQP_SQP_FAIL and the
  *   QP's status code in bits 28..30), L1 merit 1/2 J + rho |state-box violation|_1 with
  *   rho >= 2 max|yq|, Armijo backtracking by quadratic interpolation; then
@@ -380,6 +381,7 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
 #define MPCQP_SQP_DONE 1
 #define MPCQP_SQP_EXACT 2
 #define MPCQP_SQP_FAIL 4  /* with DONE: stopped by failing QPs; QP status in bits 28..30 */
+#define MPCQP_SQP_PROJ 8  /* projected curvature for the next steps (bits 24..27 count) */
 /* prediction models (integrator argument) */
 #define MPCQP_MODEL_FE 0  /* fwd_euler, main.py:132-135 */
 #define MPCQP_MODEL_RK4 1 /* runge_kutta4, main.py:138-147 (template.py:141) */
@@ -399,12 +401,15 @@ int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* 
                           const double* mu, void* H2, void* q2, void* stream);
 /*
  * mpcqp_bicycle_hessian_convex: mpcqp_bicycle_hessian with a per-stage
- * convexification: where the stage's QP Hessian W_k = blkdiag(Q, R) + H2_k
- * (Q 4 x 4, R 2 x 2 shared, the stage weights) is not positive definite, its
- * eigenvalues are lifted to eps and H2_k = W_k' - blkdiag(Q, R) (eigenvalue
- * projection; stages with W_k > 0 keep the exact curvature), then + mu I.
- * The SQP's QPs are convex by construction (no inertia correction, no
- * rejected QP), and the exact Hessian is kept wherever it is convex.
+ * convexification for the instances whose flags carry MPCQP_SQP_PROJ (all
+ * when flags is NULL): where the stage's QP Hessian W_k = blkdiag(Q, R) +
+ * H2_k (Q 4 x 4, R 2 x 2 shared, the stage weights) is not positive definite,
+ * its eigenvalues are lifted to eps and H2_k = W_k' - blkdiag(Q, R)
+ * (eigenvalue projection; stages with W_k > 0 keep the exact curvature), then
+ * + mu I.  mpcqp_bicycle_sqp_step sets MPCQP_SQP_PROJ when an exact-Hessian QP
+ * fails (non-convex) and clears it after four full steps, so the exact
+ * curvature (Newton's rate) is used wherever its QP is convex and a convex
+ * QP is taken instead of a rejected one where it is not.
  */
 int mpcqp_bicycle_hessian_convex(int dtype, int batch, int N, double ts, const double* params,
                                  const void* X, const void* U, const void* pi,

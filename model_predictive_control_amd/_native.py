@@ -25,6 +25,7 @@ STATUS_UNREFINED = 1 << 25
 SQP_DONE = 1
 SQP_EXACT = 2
 SQP_FAIL = 4
+SQP_PROJ = 8
 MODEL_FE = 0
 MODEL_RK4 = 1
 PLANT_FE = 0

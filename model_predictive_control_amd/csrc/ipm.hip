@@ -28,6 +28,12 @@ namespace mpcqp {
 
 template <typename T, int NX, int NU>
 __global__ __launch_bounds__(64) void ipm_kernel(ipm::Args<T> a) {
+  if (a.list) {
+    const int cnt = *a.list_count;
+    for (int k = blockIdx.x * 64 + threadIdx.x; k < cnt; k += gridDim.x * 64)
+      ipm::solve_lane<T, NX, NU>(a, a.list[k]);
+    return;
+  }
   const int b = blockIdx.x * 64 + threadIdx.x;
   if (b >= a.batch) return;
   ipm::solve_lane<T, NX, NU>(a, b);
@@ -42,8 +48,15 @@ template <typename T, int NX, int NU, int G>
 __global__ __launch_bounds__(64) void ipm_lds_kernel(ipm::Args<T> a) {
   extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
   const int lane = threadIdx.x;
+  if (lane >= G) return;
+  if (a.list) {
+    const int cnt = *a.list_count;
+    for (int k = blockIdx.x * G + lane; k < cnt; k += gridDim.x * G)
+      ipm::solve_lane<T, NX, NU, G>(a, a.list[k], ipm_lds + lane);
+    return;
+  }
   const int b = blockIdx.x * G + lane;
-  if (lane >= G || b >= a.batch) return;
+  if (b >= a.batch) return;
   ipm::solve_lane<T, NX, NU, G>(a, b, ipm_lds + lane);
 }
 
@@ -53,12 +66,26 @@ template <typename T, int G>
 __global__ __launch_bounds__(64, 1) void ipm_quad_kernel(ipm::Args<T> a) {
   extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
   const int g = threadIdx.x >> 2;
+  if (g >= G) return;
+  if (a.list) {
+    // the group's four lanes take the same entries (uniform trip count)
+    const int cnt = *a.list_count;
+    for (int k = blockIdx.x * G + g; k < cnt; k += gridDim.x * G)
+      ipmq::solve_quad<T, G>(a, a.list[k], ipm_lds + g);
+    return;
+  }
   const int b = blockIdx.x * G + g;
-  if (g >= G || b >= a.batch) return;
+  if (b >= a.batch) return;
   ipmq::solve_quad<T, G>(a, b, ipm_lds + g);
 }
 
 static int64_t ipm_ldb(int batch) { return ((int64_t)batch + 63) / 64 * 64; }
+
+// list mode: workgroups of the launch (each loops over its share of the list)
+constexpr int kListGrid = 1024;
+static unsigned ipm_grid(const int64_t units, bool list) {
+  return (unsigned)(list && units > kListGrid ? kListGrid : units);
+}
 
 // LDS variant: instances per workgroup (1, 2 or 4; 0 = the global-workspace
 // kernel), within the 160 KB of one CU.  MPCQP_IPM_LDS=0/1 forces the choice.
@@ -114,7 +141,7 @@ static int ipm_quad_launch(ipm::Args<T>& a, hipStream_t st) {
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
       if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(ipm_quad)");
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)((a.batch + G - 1) / G)), dim3(64), bytes, st, a);
+    hipLaunchKernelGGL(kern, dim3(ipm_grid((a.batch + G - 1) / G, a.list)), dim3(64), bytes, st, a);
     MPCQP_CHECK_LAUNCH("ipm_quad_kernel");
     return MPCQP_OK;
   };
@@ -147,7 +174,7 @@ static int ipm_launch_t(ipm::Args<T>& a, hipStream_t st) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(ipm_lds)");
       }
-      hipLaunchKernelGGL(kern, dim3((unsigned)((a.batch + G - 1) / G)), blk, bytes, st, a);
+      hipLaunchKernelGGL(kern, dim3(ipm_grid((a.batch + G - 1) / G, a.list)), blk, bytes, st, a);
       MPCQP_CHECK_LAUNCH("ipm_lds_kernel");
       return MPCQP_OK;
     };
@@ -155,8 +182,8 @@ static int ipm_launch_t(ipm::Args<T>& a, hipStream_t st) {
     if (G == 2) return launch(ipm_lds_kernel<T, NX, NU, 2>);
     return launch(ipm_lds_kernel<T, NX, NU, 1>);
   }
-  hipLaunchKernelGGL((ipm_kernel<T, NX, NU>), dim3((unsigned)((a.batch + 63) / 64)), blk, 0, st,
-                     a);
+  hipLaunchKernelGGL((ipm_kernel<T, NX, NU>), dim3(ipm_grid((a.batch + 63) / 64, a.list)), blk, 0,
+                     st, a);
   MPCQP_CHECK_LAUNCH("ipm_kernel");
   return MPCQP_OK;
 }
@@ -176,7 +203,7 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
                  int64_t sU0, const void* H2, int64_t sH2, const void* q2, int64_t sq2, void* z,
                  void* y, void* X, void* lam_u, void* pi, int32_t* status,
                  const int32_t* skip, int32_t skip_mask, int max_iter, double tol, void* ws,
-                 size_t ws_bytes, hipStream_t st) {
+                 size_t ws_bytes, hipStream_t st, const int* list, const int* list_count) {
   const size_t need = ipm_ws_bytes(batch, nx, nu, N);
   MPCQP_CHECK_ARG(ws && ws_bytes >= need, "mpcqp_mpc_ipm: workspace %zu bytes < %zu", ws_bytes,
                   need);
@@ -199,6 +226,7 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
     a.z = (T*)z; a.y = (T*)y; a.X = (T*)X; a.lam_u = (T*)lam_u; a.pi = (T*)pi; a.status = status;
     a.skip = skip; a.skip_mask = skip_mask;
     a.ws = (double*)ws;
+    a.list = list; a.list_count = list_count;
   };
   if (dtype == MPCQP_F64) {
     ipm::Args<double> a;
@@ -247,5 +275,5 @@ extern "C" int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int fl
                       strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi, strideXb, lb,
                       strideLb, ub, strideUb, U0, strideU0, H2, strideH2, q2, strideq2, z, y, X,
                       lam_u, pi, status, skip, skip_mask, max_iter, tol, ws, ws_bytes,
-                      (hipStream_t)stream);
+                      (hipStream_t)stream, nullptr, nullptr);
 }

@@ -116,6 +116,10 @@ struct Args {
   // (outputs and status keep their values; e.g. the SQP's converged ones)
   const int32_t* skip; int32_t skip_mask;
   double* ws;
+  // optional: solve only the instances list[0 .. *list_count) (device
+  // memory; the fp64 fallback of mpcqp_mpc_qp), on a grid sized for a few
+  // of them -- an empty list costs one short launch, not one per instance
+  const int* list; const int* list_count;
 };
 
 constexpr double kInf = __builtin_huge_val();

@@ -77,26 +77,11 @@ __global__ void states_kernel(int batch, int nx, int nu, int N, int tv, const T*
   }
 }
 
-// skip[b] = 1 for every instance except the hand-offs of the product-form
-// kernel (list[0..cnt)), which the fp64 fallback then solves
-__global__ void skip_all_kernel(int batch, int32_t* skip) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < batch) skip[b] = 1;
-}
-__global__ void unskip_list_kernel(const int* cnt, const int* list, int32_t* skip) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < *cnt) skip[list[j]] = 0;
-}
-
 static size_t al256(size_t v) { return (v + 255) / 256 * 256; }
 
-// workspace of the dense path with its fp64 fallback: [0, max(dense, ipm))
-// holds the dense layout (then, once the product-form kernel is done, the
-// interior point's workspace), followed by the skip words
-static size_t mpc_skip_offset(size_t dense, size_t ipm) { return al256(dense > ipm ? dense : ipm); }
-static size_t mpc_fallback_bytes(int batch, size_t dense, size_t ipm) {
-  return mpc_skip_offset(dense, ipm) + al256((size_t)batch * sizeof(int32_t));
-}
+// workspace of the dense path with its fp64 fallback: the dense layout (the
+// hand-off list is in it), then the interior point's workspace
+static size_t mpc_fallback_bytes(size_t dense, size_t ipm) { return al256(dense) + ipm; }
 
 struct MpcWs {
   size_t H, f, Gam, xbar, hl, hu, qp, total;
@@ -183,7 +168,7 @@ extern "C" size_t mpcqp_mpc_qp_workspace(int dtype, int batch, int nx, int nu, i
   if (mpc_use_ipm(dtype, nx, nu, N, state_box ? 1 : 0, 0)) return ipm;
   // the dense path's fp64 fallback: the interior point's workspace over the
   // dead condensed data, then one skip word per instance
-  return mpcqp::mpc_fallback_bytes(batch, dense, ipm);
+  return mpcqp::mpc_fallback_bytes(dense, ipm);
 }
 
 extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
@@ -253,25 +238,20 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
   const QpWsParts P = qp_ws_parts(w + L.qp, batch, n, m);
   const size_t ipmb = ipm_supported(nx, nu) ? ipm_ws_bytes(batch, nx, nu, N) : 0;
   const bool f64_fb = dyn_ok && mpc_fallback_f64() && ipmb > 0 &&
-                      ws_bytes >= mpc_fallback_bytes(batch, L.total, ipmb);
+                      ws_bytes >= mpc_fallback_bytes(L.total, ipmb);
+  // the interior point in list mode: only the handed-back instances, read
+  // from the device list (an empty list costs one short launch)
   auto fallback_f64 = [&]() -> int {
-    int32_t* skip = (int32_t*)(w + mpc_skip_offset(L.total, ipmb));
-    const dim3 blk(256);
-    hipLaunchKernelGGL(skip_all_kernel, dim3((unsigned)((batch + 255) / 256)), blk, 0, st, batch,
-                       skip);
-    MPCQP_CHECK_LAUNCH("skip_all_kernel");
-    hipLaunchKernelGGL(unskip_list_kernel, dim3((unsigned)((batch + 255) / 256)), blk, 0, st,
-                       P.cnt, P.list, skip);
-    MPCQP_CHECK_LAUNCH("unskip_list_kernel");
     return mpc_ipm_impl(MPCQP_F32, batch, nx, nu, N, flags & MPCQP_TV, A, strideA, Bm, strideB, Q,
                         strideQ, R, strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi,
                         strideXb, lb, strideLb, ub, strideUb, nullptr, 0, nullptr, 0, nullptr, 0, z,
-                        y, nullptr, nullptr, nullptr, status, skip, 1, 0, 0.0, w, ipmb, st);
+                        y, nullptr, nullptr, nullptr, status, nullptr, 0, 0, 0.0,
+                        w + al256(L.total), ipmb, st, P.list, P.cnt);
   };
-  // fp32 with n <= 64 (config 3): H^-1 on chip, rows from the dynamics --
-  // only H and f are condensed
+  // fp32 with 48 < n <= 64 (config 3): the z-space product form -- H and f
+  // (and Gamma for the row normals) are condensed, H^-1 by the MFMA sweep
   const bool zf = dyn_ok && f64_fb && mpc_zf() && zf_supported(n, m, nx, nu, N);
-  void* Gw = (sbox && !zf) ? w + L.Gam : nullptr;
+  void* Gw = sbox ? w + L.Gam : nullptr;
   void* xbw = (sbox && !zf) ? w + L.xbar : nullptr;
   int rc = mpcqp_condense(dtype, batch, nx, nu, N, flags, A, strideA, Bm, strideB, Q, strideQ, R,
                           strideR, Qf, strideQf, c, strideC, x0, strideX0, Hw, nullptr, fw, Gw,
@@ -282,9 +262,11 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
     if (e != hipSuccess) return hip_fail(e, "mpcqp_mpc_qp: hipMemsetAsync");
     const int mi = max_iter > 0 ? max_iter : 3 * (n + m) + 30;
     const float tl = tol > 0 ? (float)tol : 1e-6f;
-    rc = launch_zf(batch, n, m, (const float*)Hw, sH, (const float*)fw, n, (const float*)lb,
-                   strideLb, (const float*)ub, strideUb, (float*)z, (float*)y, status, P.cnt,
-                   P.list, mi, mpc_refine(), tl, d, st);
+    rc = sweep_hinv(batch, n, Hw, sH, fw, n, P.m0, P.s0, status, st);
+    if (rc != MPCQP_OK) return rc;
+    rc = launch_zf(batch, n, m, (const float*)P.m0, (const float*)P.s0, (const float*)Gw,
+                   (const float*)fw, n, (const float*)lb, strideLb, (const float*)ub, strideUb,
+                   (float*)z, (float*)y, status, P.cnt, P.list, mi, mpc_refine(), tl, d, st);
     if (rc == MPCQP_OK) rc = fallback_f64();
     if (rc != MPCQP_OK) return rc;
     if (X)

@@ -66,10 +66,13 @@ __host__ __device__ inline int dyn_nxp(int nx, int nu) {
 
 // solve_zf.hip: the z-space product form with H^-1 on chip (fp32, DYN only)
 bool zf_supported(int n, int m, int nx, int nu, int N);
-int launch_zf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
-              const float* lb, int64_t sLb, const float* ub, int64_t sUb, float* z, float* y,
-              int32_t* status, int* retry_count, int* retry_list, int max_iter, int refine,
-              float tol, const PfDyn& dyn, hipStream_t st);
+int launch_zf(int batch, int n, int m, const float* M, const float* s0, const float* Gam,
+              const float* f, int64_t sf, const float* lb, int64_t sLb, const float* ub,
+              int64_t sUb, float* z, float* y, int32_t* status, int* retry_count, int* retry_list,
+              int max_iter, int refine, float tol, const PfDyn& dyn, hipStream_t st);
+// sweep.hip: -H^-1 (n x n full) and s0 = -H^-1 f for 48 < n <= 64
+int sweep_hinv(int batch, int n, const void* H, int64_t sH, const void* f, int64_t sf, void* M,
+               void* s0, int32_t* status, hipStream_t st);
 
 int launch_pf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
               const float* G, int64_t sG, const float* hl, const float* hu, int64_t sh,

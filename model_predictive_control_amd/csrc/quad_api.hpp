@@ -72,7 +72,8 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
                  int64_t sU0, const void* H2, int64_t sH2, const void* q2, int64_t sq2, void* z,
                  void* y, void* X, void* lam_u, void* pi, int32_t* status,
                  const int32_t* skip, int32_t skip_mask, int max_iter, double tol, void* ws,
-                 size_t ws_bytes, hipStream_t st);
+                 size_t ws_bytes, hipStream_t st, const int* list = nullptr,
+                 const int* list_count = nullptr);
 size_t qp_ws_bytes(int dtype, int batch, int n, int m);
 struct PfDyn;
 // dyn != NULL: refine from the dynamics (pf.hpp); refine < 0: default steps;

@@ -39,13 +39,16 @@
 // (kStatusRetry).
 #include <cstdlib>
 
+#include "mfma.hpp"
 #include "pfdyn.hpp"
 
 namespace mpcqp {
 
 struct ZfArgs {
   int batch, n, m;
-  const float* H; int64_t sH;   // packed lower n x n
+  const float* M;               // -H^-1, n x n row-major per instance (sweep_hinv)
+  const float* s0;              // -H^-1 f (n per instance)
+  const float* Gam;             // condensed Gamma, m x n row-major (row normals)
   const float* f; int64_t sf;
   const float* lb; int64_t sLb;
   const float* ub; int64_t sUb;
@@ -57,6 +60,7 @@ struct ZfArgs {
 };
 
 constexpr int kZfRowBufs = 16;  // normals of active state rows held in LDS
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float wave_sum(float v) {
   v += lane_step<1>(v);
@@ -84,6 +88,9 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
   __shared__ int rst[2 * kWave];    // row status: 0 inactive, 1 at xlo, 2 at xhi
   const int b = blockIdx.x, l = threadIdx.x;
   const int n = a.n, m = a.m, nt = n + m;
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
   const PfDyn& d = a.d;
   const int nx = d.nx;
   const float inf = Lim<float>::inf();
@@ -114,8 +121,12 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
   }
   zmu[l] = 0.f;
   int code = MPCQP_STATUS_OPTIMAL, iters = 0;
-  if (__builtin_amdgcn_ballot_w64(nonfin)) code = MPCQP_STATUS_NONFINITE;
-  else if (__builtin_amdgcn_ballot_w64(bad)) code = MPCQP_STATUS_INFEASIBLE;
+  {
+    const int pre = a.status[b];  // the sweep's (non-finite data, non-PD pivot)
+    if (pre) code = pre;
+    else if (__builtin_amdgcn_ballot_w64(nonfin)) code = MPCQP_STATUS_NONFINITE;
+    else if (__builtin_amdgcn_ballot_w64(bad)) code = MPCQP_STATUS_INFEASIBLE;
+  }
   float Hi[kWave];  // row l of H^-1 (rows/columns >= n: identity)
   float Srow[kSlots];  // row l of S^-1 (slot l); zeroed once H^-1 is formed
   float z = 0.f, z0 = 0.f;
@@ -130,82 +141,52 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
   if (code != MPCQP_STATUS_OPTIMAL) goto out;
 
   {
-    // ----------------------------------------------------- H^-1 on chip
-    // packed H into LDS (the pool is free until the dynamics are loaded)
+    // ----------------------------------------------------- H^-1 rows
+    // row l of H^-1 = -M[l][:] (sweep_hinv: MFMA, square-root form); rows
+    // and columns past n are zero
     {
-      float* Hp = reinterpret_cast<float*>(pool);
-      const int nh = n * (n + 1) / 2;
-      lds_copy3(Hp, a.H + (int64_t)b * a.sH, nh, nullptr, 0, nullptr, 0, l);
-      wave_lds_sync();
+      // 16-byte loads through a range-checked descriptor: a row's last load
+      // may run into the next row (masked below), past the instance's end it
+      // reads 0; rows >= n load nothing
+      const rsrc_t rMi = mk_rsrc(a.M + (int64_t)b * n * n, (int64_t)n * n * 4);
+      float4 v4[kWave / 4];
 #pragma unroll
-      for (int k = 0; k < kWave; ++k) {
-        const int hi_ = l > k ? l : k, lo_ = l > k ? k : l;
-        const bool in = l < n && k < n;
-        Hi[k] = in ? Hp[hi_ * (hi_ + 1) / 2 + lo_] : (l == k ? 1.f : 0.f);
-        nonfin |= !finite(Hi[k]);
+      for (int k4 = 0; k4 < kWave / 4; ++k4) {
+        const int off = (l < n && 4 * k4 < n) ? 4 * (l * n + 4 * k4) : kOOB;
+        v4[k4] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rMi, off, 0, 0));
       }
-      wave_lds_sync();
+#pragma unroll
+      for (int k4 = 0; k4 < kWave / 4; ++k4) {
+        const float e[4] = {v4[k4].x, v4[k4].y, v4[k4].z, v4[k4].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Hi[4 * k4 + q] = (4 * k4 + q < n) ? -e[q] : 0.f;
+      }
     }
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) Srow[j] = 0.f;
+    MPCQP_PHASE(1);
+    // lane-local products with H^-1: out_l = sum_j Hi[j] v_j, v broadcast
+    // (two packed float2 chains: v_pk_fma_f32, half the issue of a scalar chain)
+    auto hmul = [&](const float* v) __attribute__((always_inline)) -> float {
+      f2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f};
+#pragma unroll
+      for (int j4 = 0; j4 < kWave / 4; ++j4) {
+        const float4 vv = *reinterpret_cast<const float4*>(&v[4 * j4]);
+        a01 = __builtin_elementwise_fma(f2{Hi[4 * j4], Hi[4 * j4 + 1]}, f2{vv.x, vv.y}, a01);
+        a23 = __builtin_elementwise_fma(f2{Hi[4 * j4 + 2], Hi[4 * j4 + 3]}, f2{vv.z, vv.w}, a23);
+      }
+      return (a01.x + a01.y) + (a23.x + a23.y);
+    };
+    // z0 = -H^-1 f (the sweep's s0)
+    z0 = zl_ok ? a.s0[(int64_t)b * n + l] : 0.f;
+    z = z0;
+    nonfin = !finite(z0);
+#pragma unroll
+    for (int k = 0; k < kWave; ++k) nonfin |= !finite(Hi[k]);
     if (__builtin_amdgcn_ballot_w64(nonfin)) {
       code = MPCQP_STATUS_NONFINITE;
       goto out;
     }
-    // symmetric sweep of every pivot: M = SWEEP(H) = -H^-1.  Pivot k: row k
-    // (= column k) through LDS; M[i][j] -= M[i][k] M[k][j] / M[k][k],
-    // M[i][k] = M[k][i] = M[i][k] / M[k][k], M[k][k] = -1 / M[k][k]
-    for (int k = 0; k < n; ++k) {
-      wave_lds_sync();
-      if (l == k) {
-#pragma unroll
-        for (int j4 = 0; j4 < kWave / 4; ++j4)
-          *reinterpret_cast<float4*>(&pubA[4 * j4]) =
-              float4{Hi[4 * j4], Hi[4 * j4 + 1], Hi[4 * j4 + 2], Hi[4 * j4 + 3]};
-      }
-      wave_lds_sync();
-      const float dkk = pubA[k];
-      if (!(dkk > 0.f)) {  // H not positive definite (in fp32)
-        code = MPCQP_STATUS_NOT_CONVEX;
-        goto out;
-      }
-      const float inv = 1.f / dkk;
-      const float c = pubA[l] * inv;
-      const bool me = l == k;
-#pragma unroll
-      for (int j4 = 0; j4 < kWave / 4; ++j4) {
-        const float4 pk = *reinterpret_cast<const float4*>(&pubA[4 * j4]);
-        const float pj[4] = {pk.x, pk.y, pk.z, pk.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int j = 4 * j4 + e;
-          float v = me ? pj[e] * inv : fmaf(-c, pj[e], Hi[j]);
-          v = (j == k) ? (me ? -inv : c) : v;
-          Hi[j] = v;
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kWave; ++j) Hi[j] = -Hi[j];  // H^-1
-#pragma unroll
-    for (int j = 0; j < kSlots; ++j) Srow[j] = 0.f;
-    // lane-local products with H^-1: out_l = sum_j Hi[j] v_j, v broadcast
-    auto hmul = [&](const float* v) __attribute__((always_inline)) -> float {
-      float acc = 0.f;
-#pragma unroll
-      for (int j4 = 0; j4 < kWave / 4; ++j4) {
-        const float4 vv = *reinterpret_cast<const float4*>(&v[4 * j4]);
-        acc = fmaf(Hi[4 * j4], vv.x, acc);
-        acc = fmaf(Hi[4 * j4 + 1], vv.y, acc);
-        acc = fmaf(Hi[4 * j4 + 2], vv.z, acc);
-        acc = fmaf(Hi[4 * j4 + 3], vv.w, acc);
-      }
-      return acc;
-    };
-    // z0 = -H^-1 f
-    wave_lds_sync();
-    pubA[l] = zl_ok ? fl : 0.f;
-    wave_lds_sync();
-    z0 = zl_ok ? -hmul(pubA) : 0.f;
-    z = z0;
 
     // ----------------------------------------------------- helpers
     auto bcast_slots = [&](float t) __attribute__((always_inline)) {
@@ -215,16 +196,14 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
     };
     auto smul = [&](float t) __attribute__((always_inline)) -> float {  // (S^-1 t)_l
       bcast_slots(t);
-      float q = 0.f;
+      f2 q01 = {0.f, 0.f}, q23 = {0.f, 0.f};
 #pragma unroll
       for (int j4 = 0; j4 < kSlots / 4; ++j4) {
         const float4 tv = *reinterpret_cast<const float4*>(&sx[4 * j4]);
-        q = fmaf(Srow[4 * j4 + 0], tv.x, q);
-        q = fmaf(Srow[4 * j4 + 1], tv.y, q);
-        q = fmaf(Srow[4 * j4 + 2], tv.z, q);
-        q = fmaf(Srow[4 * j4 + 3], tv.w, q);
+        q01 = __builtin_elementwise_fma(f2{Srow[4 * j4], Srow[4 * j4 + 1]}, f2{tv.x, tv.y}, q01);
+        q23 = __builtin_elementwise_fma(f2{Srow[4 * j4 + 2], Srow[4 * j4 + 3]}, f2{tv.z, tv.w}, q23);
       }
-      return q;
+      return (q01.x + q01.y) + (q23.x + q23.y);
     };
     auto s_add = [&](float w, float sigma) __attribute__((always_inline)) {
       const float wi = w / sigma;
@@ -300,45 +279,11 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
       pubA[l] += acc;
       wave_lds_sync();
     };
-    // row normal Gamma_j (x_j = x_{s+1}[c] with j = s nx + c) into buffer bb,
-    // by the adjoint recursion over the resident stages (fp32, every lane
-    // runs it; lane k*nu + a keeps dx_{s+1}[c] / du_k[a])
+    // row normal Gamma_j (row j of the condensed Gamma) into buffer bb
     auto row_normal = [&](int j, int bb) __attribute__((always_inline)) {
-      const DynChunk C = dyn_chunk(d, pool);
-      const int nu = d.nu;
-      const int s = j / nx, cc = j - s * nx;
-      float lam[NXP];
-#pragma unroll
-      for (int q = 0; q < NXP; ++q) lam[q] = (q == cc) ? 1.f : 0.f;
-      float mine = 0.f;
-      for (int k = s; k >= 0; --k) {
-        const float* Ak = C.A(k);
-        const float* Bk = C.B(k);
-        const int kk = l - k * nu;  // this lane's input offset in stage k
-#pragma unroll
-        for (int q = 0; q < NXP; ++q) {
-          if (q < nu) {
-            float o = 0.f;
-#pragma unroll
-            for (int r = 0; r < NXP; ++r)
-              if (r < nx) o = fmaf(Bk[r * nu + q], lam[r], o);
-            mine = (kk == q) ? o : mine;
-          }
-        }
-        float ln[NXP];
-#pragma unroll
-        for (int q = 0; q < NXP; ++q) {
-          float o = 0.f;
-#pragma unroll
-          for (int r = 0; r < NXP; ++r)
-            if (r < nx && q < nx) o = fmaf(Ak[r * nx + q], lam[r], o);
-          ln[q] = o;
-        }
-#pragma unroll
-        for (int q = 0; q < NXP; ++q) lam[q] = ln[q];
-      }
+      const float v = l < n ? a.Gam[((int64_t)b * m + j) * n + l] : 0.f;
       wave_lds_sync();
-      nrm[bb][l] = l < n ? mine : 0.f;
+      nrm[bb][l] = v;
       wave_lds_sync();
     };
     // fp64 rollout of the current z -> X (pool); the stage data are resident
@@ -357,7 +302,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
 #pragma unroll
         for (int r = 0; r < NR; ++r) ext[l + kWave * r] = 0.f;
       }
-      dyn_residual<NR, NXP, true, true>(d, b, n, m, l, x, ext, stv, pool, loaded, wdummy);
+      dyn_residual<NR, NXP, true, true>(d, b, n, m, l, x, ext, stv, pool, loaded, wdummy MPCQP_CLK_ARG);
     };
     const double* Xr = pool + kDynX + nx;  // x_1..x_N (rows j = s nx + c)
 
@@ -375,10 +320,11 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
       wave_lds_sync();
 #pragma unroll
       for (int r = 0; r < NR; ++r) ext[l + kWave * r] = 0.f;
-      dyn_residual<NR, NXP, true>(d, b, n, m, l, x, ext, stv, pool, loaded, wdummy);
+      dyn_residual<NR, NXP, true>(d, b, n, m, l, x, ext, stv, pool, loaded, wdummy MPCQP_CLK_ARG);
       for (int j = l; j < m; j += kWave) r0[j] = (float)Xr[j];
     }
     wave_lds_sync();
+    MPCQP_PHASE(2);
 
     // refresh: the equality-QP solution of the working set from z0:
     // u = S^-1 c, c_s = -(n_s' z0 - b_s); z = z0 + H^-1 N_P u
@@ -411,6 +357,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
     for (int round = 0; round < kDynRounds; ++round) {
       if (!gi_skip) {
         while (true) {
+          MPCQP_PHASE(4);
           // the most violated free z bound
           float viol = -inf;
           {
@@ -493,6 +440,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
           const float npa = isrow ? psgn * wave_sum(nrm[pb][l] * av) : psgn * readlane(av, p);
           float tau = 0.f;
           bool added = false;
+          MPCQP_PHASE(3);
           while (!added) {
             if (++iters > a.max_iter) {
               code = MPCQP_STATUS_MAXITER;
@@ -573,6 +521,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
               }
               added = true;
             }
+            MPCQP_PHASE(4);
           }
         }
       }
@@ -601,7 +550,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
         wave_lds_sync();
       }
       float zl_ext = 0.f;  // low part of z (free z)
-      bool decided = false;
+      bool decided = false, polish = false;
       float prev = inf, r_prev = inf;
       float pv = -inf, dv = -inf;
       int dk = 0;
@@ -625,7 +574,9 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
             stv[r] = 3;
           }
         }
-        dyn_residual<NR, NXP, false, true>(d, b, n, m, l, x, ext, stv, pool, loaded, w);
+        MPCQP_PHASE(6);
+        dyn_residual<NR, NXP, false, true>(d, b, n, m, l, x, ext, stv, pool, loaded, w MPCQP_CLK_ARG);
+        MPCQP_PHASE(5);
         // stationarity rho = g - N_P u on z; active-row residuals by row
         const float g = zl_ok ? (float)gx[l] : 0.f;
         const float rho = zl_ok ? (zst == 0 ? g : g - zmu[l]) : 0.f;
@@ -701,10 +652,13 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
           const bool converged = !(prev > a.dyn_stop);
           if ((contracting && (clear || fails)) || converged) {
             decided = true;
-            break;
+            // certified: one more correction from this residual (cheap here:
+            // no memory traffic) takes the output a contraction closer
+            if (pv > kDynTol || dv > 0.f) break;
+            polish = true;
           }
         }
-        if (it >= a.refine) break;
+        if (!polish && it >= a.refine) break;
         // Newton correction on the working set (product form):
         //   a = H^-1 rho, b_s = n_s' a - e_s, du = S^-1 b, dz = H^-1 N_P du - a
         wave_lds_sync();
@@ -736,6 +690,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
         }
         prev = wave_max(dmax);
         r_prev = rn;
+        if (polish) break;
       }
       if (code != MPCQP_STATUS_OPTIMAL) break;
       if (decided && !(pv > kDynTol) && !(dv > 0.f)) break;  // certified
@@ -782,6 +737,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
     }
   }
 out:
+  MPCQP_PHASE(6);
   {
     const bool ok = code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER;
     if (code != kStatusRetry) {
@@ -801,18 +757,22 @@ out:
       if (code == kStatusRetry) a.retry_list[atomicAdd(a.retry_count, 1)] = b;
     }
   }
+  MPCQP_PHASE(7);
+#ifdef MPCQP_PHASE_TIMING
+  mpcqp_clk.flush();
+#endif
 }
 
 bool zf_supported(int n, int m, int nx, int nu, int N) {
-  return n <= kWave && m <= 2 * kWave && dyn_nxp(nx, nu) == 4 && dyn_chunk_stages(nx, nu, N) >= N;
+  return n > 48 && n <= kWave && m <= 2 * kWave && dyn_nxp(nx, nu) == 4 && dyn_chunk_stages(nx, nu, N) >= N;
 }
 
-int launch_zf(int batch, int n, int m, const float* H, int64_t sH, const float* f, int64_t sf,
-              const float* lb, int64_t sLb, const float* ub, int64_t sUb, float* z, float* y,
-              int32_t* status, int* retry_count, int* retry_list, int max_iter, int refine,
-              float tol, const PfDyn& dyn, hipStream_t st) {
-  ZfArgs a{batch, n, m, H, sH, f, sf, lb, sLb, ub, sUb, z, y, status, retry_count, retry_list,
-           max_iter, refine, tol, kDynStop, dyn};
+int launch_zf(int batch, int n, int m, const float* M, const float* s0, const float* Gam,
+              const float* f, int64_t sf, const float* lb, int64_t sLb, const float* ub,
+              int64_t sUb, float* z, float* y, int32_t* status, int* retry_count, int* retry_list,
+              int max_iter, int refine, float tol, const PfDyn& dyn, hipStream_t st) {
+  ZfArgs a{batch, n, m, M, s0, Gam, f, sf, lb, sLb, ub, sUb, z, y, status, retry_count,
+           retry_list, max_iter, refine, tol, kDynStop, dyn};
   if (const char* e = getenv("MPCQP_DYN_STOP")) a.dyn_stop = (float)atof(e);
   hipLaunchKernelGGL((qp_zf_kernel<4>), dim3(batch), dim3(kWave), 0, st, a);
   MPCQP_CHECK_LAUNCH("qp_zf_kernel");
@@ -820,3 +780,7 @@ int launch_zf(int batch, int n, int m, const float* H, int64_t sH, const float* 
 }
 
 }  // namespace mpcqp
+
+#ifdef MPCQP_PHASE_TIMING
+MPCQP_DEBUG_PHASE_READER(mpcqp_debug_phase_cycles_zf)
+#endif

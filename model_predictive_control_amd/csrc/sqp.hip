@@ -20,7 +20,11 @@
 
 namespace mpcqp {
 
-constexpr int kSqpDone = 1, kSqpExact = 2, kSqpFail = 4;
+constexpr int kSqpDone = 1, kSqpExact = 2, kSqpFail = 4, kSqpProj = 8;
+// an exact-Hessian QP that is not convex switches the instance to the
+// per-stage projected curvature (mpcqp_bicycle_hessian_convex) for this many
+// full steps (bits 24..27 count down), then the exact curvature is tried again
+constexpr int kSqpProjSteps = 4;
 // a Gauss-Newton QP (convex by construction) that fails this many times in a
 // row stops the instance: DONE | FAIL, the QP's status code in bits 28..30
 constexpr int kSqpMaxFails = 3;
@@ -153,6 +157,7 @@ __global__ __launch_bounds__(256) void bike_hess_kernel(int batch, int N, Bike p
   double* H = H2 + e * 36;
   double* q = q2 + e * 6;
   const bool exact = flags == nullptr || (flags[b] & kSqpExact);
+  const bool proj = Qw && Rw && (flags == nullptr || (flags[b] & kSqpProj));
   if (!exact) {
     for (int i = 0; i < 36; ++i) H[i] = 0.0;
     for (int i = 0; i < 6; ++i) q[i] = 0.0;
@@ -164,7 +169,7 @@ __global__ __launch_bounds__(256) void bike_hess_kernel(int batch, int N, Bike p
   const BikePt pt = bike_pt(p, x, u);
   double Hl[36];
   bike_lag_hess(p, pt, x, lam, Hl);
-  if (Qw && Rw) project_stage(Hl, Qw, Rw, eps);
+  if (proj) project_stage(Hl, Qw, Rw, eps);
   if (mu)
     for (int i = 0; i < 6; ++i) Hl[i * 6 + i] += mu[b];
   const double w[6] = {x[0], x[1], x[2], x[3], u[0], u[1]};
@@ -255,9 +260,14 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
     const int iters = ((fl >> 8) & 0xFFFF) + 1;
     const int fails = ((fl >> 24) & 0xF) + 1;
     const int code = a.qp_status[b] & 0x7;
-    if (fl & kSqpExact) {
+    if ((fl & kSqpExact) && !(fl & kSqpProj)) {
+      // the exact curvature made the QP fail (non-convex): the projected one
+      // next (mpcqp_bicycle_hessian_convex; a caller of the plain
+      // mpcqp_bicycle_hessian gets the damping below at the next failure)
+      a.flags[b] = (iters << 8) | kSqpExact | kSqpProj | (kSqpProjSteps << 24);
+    } else if (fl & kSqpExact) {
       a.mu[b] = fmax(4.0 * a.mu[b], kMuFloor);
-      a.flags[b] = (iters << 8) | kSqpExact;
+      a.flags[b] = (iters << 8) | (fl & (kSqpExact | kSqpProj | (0xF << 24)));
     } else if (fails >= kSqpMaxFails) {
       a.flags[b] = (iters << 8) | kSqpDone | kSqpFail | (code << 28);
     } else {
@@ -413,7 +423,11 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
   }
   const int iters = ((fl >> 8) & 0xFFFF) + 1;
   const bool exact = (fl & kSqpExact) || r < kSqpSwitch;  // sticky
-  fl = (iters << 8) | (r <= a.tol ? kSqpDone : 0) | (exact ? kSqpExact : 0);
+  // projected curvature: count full steps down, then back to the exact one
+  int pc = (fl & kSqpProj) ? ((fl >> 24) & 0xF) : 0;
+  if (pc > 0 && alpha == 1.0) --pc;
+  fl = (iters << 8) | (r <= a.tol ? kSqpDone : 0) | (exact ? kSqpExact : 0) |
+       (pc > 0 ? kSqpProj | (pc << 24) : 0);
   a.flags[b] = fl;
   a.rho[b] = rho;
   a.kkt[b] = r;

@@ -592,6 +592,27 @@ int sweep_tiles(int dtype, int n, int m) {
   return (T >= 5 && T <= 12) ? T : 0;
 }
 
+// -H^-1 (n x n, row-major full) and s0 = -H^-1 f for 48 < n <= 64 (four
+// z tiles, no rows): the inverse the z-space kernel (solve_zf.hip) iterates
+// with, on MFMA in square-root form
+int sweep_hinv(int batch, int n, const void* H, int64_t sH, const void* f, int64_t sf, void* M,
+               void* s0, int32_t* status, hipStream_t st) {
+  if (n <= 48 || n > 64) {
+    set_error("sweep_hinv: n = %d outside 49..64", n);
+    return MPCQP_ENOTSUP;
+  }
+  SweepArgs a;
+  a.batch = batch; a.n = n; a.m = 0; a.full = 1;
+  a.f = (const float*)f; a.sf = sf; a.s0 = (float*)s0;
+  a.np = 64;
+  a.kp = 4;
+  a.H = (const float*)H; a.sH = sH;
+  a.G = nullptr; a.sG = 0;
+  a.M = (float*)M;
+  a.status = status;
+  return launch_sweep_t<4>(a, st);
+}
+
 int sweep_launch(int batch, int n, int m, const void* H, int64_t sH, const void* G, int64_t sG,
                  void* M, int full, int32_t* status, hipStream_t st, const void* f, int64_t sf,
                  void* s0) {

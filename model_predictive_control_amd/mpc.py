@@ -332,10 +332,10 @@ class SqpSolver:
             A, B, c, Xr = batched.bicycle_rti(X0, self.U, ctl.params, ctl.ts, states=True)
         H2 = q2 = None
         if ctl.hessian != "gauss-newton":
-            # "exact": the Lagrangian curvature, projected per stage where the
-            # stage Hessian is not positive definite (convex QPs); "exact-raw":
-            # unprojected, the interior point's inertia correction and the
-            # damping mu handle indefiniteness
+            # "exact": the Lagrangian curvature; after a QP that it made
+            # non-convex, projected per stage for a few steps (flag SQP_PROJ,
+            # set by the step kernel); "exact-raw": never projected, the
+            # damping mu handles indefiniteness
             cw = dict(Q=ctl.Q, R=ctl.R) if ctl.hessian == "exact" else {}
             H2, q2 = batched.bicycle_hessian(Xr, self.U, self.pi, ctl.params, ctl.ts,
                                              flags=self.flags, mu=self.mu, **cw)

@@ -291,8 +291,9 @@ def test_mpc_qp_handoff(dev, monkeypatch, fallback):
     flag = nat.STATUS_POLISHED if fallback == "f64" else nat.STATUS_UNREFINED
     assert st[0] & flag and not st[1] & (nat.STATUS_UNREFINED | nat.STATUS_POLISHED), st
     zn = z.cpu().numpy()
-    d = oc.condense(np.array([[0.9]]), np.array([[1.0, 1.0]]), np.eye(1), np.eye(2), np.eye(1),
-                    N, x0=np.array([5.0]))
+    # the oracle on the values the device sees (0.9 rounded to fp32)
+    d = oc.condense(np.array([[float(np.float32(0.9))]]), np.array([[1.0, 1.0]]), np.eye(1),
+                    np.eye(2), np.eye(1), N, x0=np.array([5.0]))
     zr = oq.box_qp(d["H"], d["f"], -1e-3, 1e-3)[0]
     assert (np.abs(zr) > 1e-3 - 1e-12).sum() > 64       # the hand-off case: > 64 active
     # fp64 fallback: the fp64 solution (to the fp32 output rounding); the

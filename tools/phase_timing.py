@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CS = os.environ.get("PT_CS", os.path.join(ROOT, "model_predictive_control_amd", "csrc"))
 LIB = os.path.join(ROOT, "model_predictive_control_amd", "lib", "libmpcqp_timing.so")
 SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.hip", "quad_box.hip",
-        "solve_qp.hip", "sweep.hip", "solve_pf.hip", "mpc_qp.hip", "bicycle.hip", "misc.hip",
+        "solve_qp.hip", "sweep.hip", "solve_pf.hip", "solve_zf.hip", "mpc_qp.hip", "bicycle.hip", "misc.hip",
         "ipm.hip", "sqp.hip", "loop_box.hip"]
 PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/recheck", "GI: scan+argmax", "GI: pivot col+ratio", "GI: sweep"]
 
@@ -45,8 +45,9 @@ from model_predictive_control_amd import _native, batched  # noqa: E402
 
 lib = _native.load()
 arg = sys.argv[1] if len(sys.argv) > 1 else "2"
+zf = arg.startswith("zf")
 pf = arg.startswith("pf") or arg.startswith("dyn")
-cfg = int(arg[3:] if arg.startswith("dyn") else (arg[2:] if pf else arg))
+cfg = int(arg[2:]) if zf else int(arg[3:] if arg.startswith("dyn") else (arg[2:] if pf else arg))
 reader = lib.mpcqp_debug_phase_cycles if cfg == 2 else lib.mpcqp_debug_phase_cycles_qp
 reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = (ctypes.c_ulonglong * 8)()
@@ -92,6 +93,17 @@ elif cfg == 33:
     w = bench.Config3(a, torch.device("cuda"), 0)
     run = lambda: batched.condense(w.A[0], w.B[0], w.Q_t, w.R_t, w.QN_t, w.N, x0=w.X0_t[0],  # noqa: E731
                                    c=w.c[0], tv=True, outputs=("H", "f", "Gam", "xbar"))
+    waves = a.batch * R
+elif zf:
+    # qp_zf_kernel of config 3 (one mpc_qp step; the zf kernel's clock only)
+    reader = lib.mpcqp_debug_phase_cycles_zf
+    reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    PHASES = ["setup: loads, H rows", "H^-1 sweep", "z0 + first rollout", "GI: scan, rows, a",
+              "GI: iteration body", "refine: residual", "refine: cert + correction", "output"]
+    a = A(); a.batch = int(os.environ.get("PT_BATCH", 65536)); a.slots = 1; a.horizon = 0
+    a.reps = 1; a.check = 0
+    w = bench.CONFIGS["3"](a, torch.device("cuda"), 0)
+    run = lambda: w.step(0)  # noqa: E731
     waves = a.batch * R
 elif pf:
     # qp_pf_kernel of config 3 / 5 (one wave per instance)
