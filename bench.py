@@ -806,7 +806,7 @@ class ConfigNLP:
     def kernels(self, traffic):
         """One SQP iteration's launches timed separately, on the state of slot
         0 after 3 iterations from U = 0 (every instance still iterating): the
-        interior point as SqpSolver runs it (strict, QP_MAX_ITER), no skip."""
+        interior point as SqpSolver runs it (STRICT, QP_MAX_ITER), no skip."""
         from model_predictive_control_amd.mpc import SqpSolver
 
         R = self.args.reps
@@ -821,16 +821,17 @@ class ConfigNLP:
                           self.dev)
         cw = dict(Q=ctl.Q, R=ctl.R) if ctl.hessian == "exact" else {}
         t_h = time_kernel(lambda: batched.bicycle_hessian(Xr, sqp.U, sqp.pi, ctl.params, ctl.ts,
-                                                          flags=sqp.flags, mu=sqp.mu, **cw), R,
+                                                          flags=sqp.flags, mu=sqp.mu, fix=sqp.fix,
+                                                          **cw), R,
                           self.dev)
         H2, q2 = batched.bicycle_hessian(Xr, sqp.U, sqp.pi, ctl.params, ctl.ts, flags=sqp.flags,
-                                         mu=sqp.mu, **cw)
+                                         mu=sqp.mu, fix=sqp.fix, **cw)
         box = ctl._box()
         qp = {}
 
         def ipm():  # the outputs allocated once, then written in place
             qp.update(batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, x0, lb=ctl.lbz, ub=ctl.ubz,
-                                      c=c, tv=True, H2=H2, q2=q2, strict=True,
+                                      c=c, tv=True, H2=H2, q2=q2, strict=SqpSolver.STRICT,
                                       max_iter=SqpSolver.QP_MAX_ITER, out=qp or None, **box))
         t_i = time_kernel(ipm, R, self.dev)
         torch.cuda.synchronize()

@@ -356,7 +356,10 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
  *   instance's Levenberg-Marquardt damping, NULL = 0) and q2_k = -H2_k w_k,
  *   so that the QP's extra cost is 1/2 (w - w_k)'H2_k (w - w_k); zeros for
  *   instances whose flags lack MPCQP_SQP_EXACT (flags NULL = all exact).
- *   X ((N+1) x 4), U (N x 2), pi (N x 4) per instance.
+ *   fix (NULL = none): one int32 per instance and stage, bit q set = input
+ *   q is held at its bound: its diagonal gets a proximal 1e6 (the input
+ *   stays where it is in the QP).  X ((N+1) x 4), U (N x 2), pi (N x 4) per
+ *   instance.
  * mpcqp_bicycle_sqp_step: per instance not yet MPCQP_SQP_DONE: step d = Z - U
  *   (Z the QP solution; an instance whose qp_status is not OPTIMAL takes no
  *   step: in exact-Hessian mode it switches to the projected curvature
@@ -368,8 +371,11 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
  *   ((N+1) x 4) at the new U and the first-order optimality residual of the
  *   NLP there (projected gradient of the Lagrangian on the input box,
  *   state-box violation, complementarity of y) -> kkt.  flags: DONE when
- *   kkt <= tol; EXACT (use the exact Hessian from now on) once kkt < 1e-2;
- *   bits 8..23 count the iterations.  mu (Levenberg-Marquardt damping of the
+ *   kkt <= tol; EXACT (use the exact Hessian from now on) once kkt < 0.3
+ *   or after 15 Gauss-Newton iterations;
+ *   bits 8..23 count the iterations.  fix (NULL = not written; batch x N
+ *   int32, for mpcqp_bicycle_hessian): bit q of stage k set when u_k,q sits
+ *   at a bound that its NLP gradient pushes against by more than 1e-6.  mu (Levenberg-Marquardt damping of the
  *   exact-Hessian QPs, caller-initialised, e.g. 0.1): divided by 4 after a
  *   full step (to 0 below 1e-11), multiplied by 4 (at least 1e-3) after a
  *   step that needed backtracking or a failed QP.  rho, mu, kkt: one double
@@ -398,7 +404,7 @@ int mpcqp_bicycle_linearise(int dtype, int batch, int N, double ts, const double
                             int64_t strideU, void* X, void* A, void* B, void* c, void* stream);
 int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
                           const void* X, const void* U, const void* pi, const int32_t* flags,
-                          const double* mu, void* H2, void* q2, void* stream);
+                          const double* mu, const int32_t* fix, void* H2, void* q2, void* stream);
 /*
  * mpcqp_bicycle_hessian_convex: mpcqp_bicycle_hessian with a per-stage
  * convexification for the instances whose flags carry MPCQP_SQP_PROJ (all
@@ -413,15 +419,17 @@ int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* 
  */
 int mpcqp_bicycle_hessian_convex(int dtype, int batch, int N, double ts, const double* params,
                                  const void* X, const void* U, const void* pi,
-                                 const int32_t* flags, const double* mu, const void* Q,
-                                 const void* R, double eps, void* H2, void* q2, void* stream);
+                                 const int32_t* flags, const double* mu, const int32_t* fix,
+                                 const void* Q, const void* R, double eps, void* H2, void* q2,
+                                 void* stream);
 int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts, const double* params,
                            int integrator, const void* x0, int64_t strideX0, const void* Q, const void* R,
                            const void* Qf, const void* xlo, const void* xhi, int64_t strideXb,
                            const void* lb, const void* ub, int64_t strideLb, void* U,
                            const void* Z, const void* yq, const void* piq,
                            const int32_t* qp_status, void* y, void* pi, void* X, double* rho,
-                           double* kkt, double* mu, int32_t* flags, double tol, void* stream);
+                           double* kkt, double* mu, int32_t* flags, int32_t* fix, double tol,
+                           void* stream);
 
 /*
  * The receding-horizon loop on device (rcracers.simulate(x0, dynamics,

@@ -717,13 +717,15 @@ def _bike_params(params):
 
 
 def bicycle_hessian(X, U, pi, params, ts: float, flags=None, mu=None,
-                    out: tuple | None = None, Q=None, R=None, eps: float = 1e-6):
+                    out: tuple | None = None, Q=None, R=None, eps: float = 1e-6, fix=None):
     """Per stage, the curvature of the dynamics weighted by the costates plus
     a proximal mu I (include/mpcqp.h ``mpcqp_bicycle_hessian``): X (b, N+1,
     4), U (b, N, 2), pi (b, N, 4) fp64, mu (b,) or None -> H2 (b, N, 6, 6),
     q2 (b, N, 6); zeros where flags (b,) lacks SQP_EXACT.  With the stage
     weights Q (4, 4) and R (2, 2): ``mpcqp_bicycle_hessian_convex``, the
-    curvature projected so that blkdiag(Q, R) + H2 >= eps I per stage."""
+    curvature projected so that blkdiag(Q, R) + H2 >= eps I per stage.
+    fix (b, N) int32 or None: inputs held at their bound (bits written by
+    bicycle_sqp_step) get a proximal 1e6 on their diagonal."""
     b, N = int(U.shape[0]), int(U.shape[1])
     if out is None:
         H2 = torch.empty((b, N, 6, 6), dtype=torch.float64, device=U.device)
@@ -735,12 +737,12 @@ def bicycle_hessian(X, U, pi, params, ts: float, flags=None, mu=None,
         Rc = R.to(torch.float64).contiguous()
         rc = _lib().mpcqp_bicycle_hessian_convex(nat.F64, b, N, float(ts), _bike_params(params),
                                                  _ptr(X), _ptr(U), _ptr(pi), _ptr(flags), _ptr(mu),
-                                                 _ptr(Qc), _ptr(Rc), float(eps), _ptr(H2),
+                                                 _ptr(fix), _ptr(Qc), _ptr(Rc), float(eps), _ptr(H2),
                                                  _ptr(q2), _stream())
         nat.check(rc, "mpcqp_bicycle_hessian_convex")
         return H2, q2
     rc = _lib().mpcqp_bicycle_hessian(nat.F64, b, N, float(ts), _bike_params(params), _ptr(X),
-                                      _ptr(U), _ptr(pi), _ptr(flags), _ptr(mu), _ptr(H2),
+                                      _ptr(U), _ptr(pi), _ptr(flags), _ptr(mu), _ptr(fix), _ptr(H2),
                                       _ptr(q2), _stream())
     nat.check(rc, "mpcqp_bicycle_hessian")
     return H2, q2
@@ -751,7 +753,8 @@ def bicycle_sqp_step(x0, U, Z, yq, piq, y, pi, X, state: dict, params, ts: float
                      integrator: int = 0):
     """Line search + update + NLP optimality residual (include/mpcqp.h
     ``mpcqp_bicycle_sqp_step``), in place on U, y, pi, X and ``state``
-    (rho, kkt, mu float64 (b,), flags int32 (b,)).  Bounds: xlo/xhi (N*4,)
+    (rho, kkt, mu float64 (b,), flags int32 (b,), optional fix int32 (b, N):
+    the inputs to hold at their bound in the next exact-Hessian QP).  Bounds: xlo/xhi (N*4,)
     shared or (b, N*4); lb/ub (N*2,) shared or (b, N*2)."""
     b, N = int(U.shape[0]), int(U.shape[1])
     sxb = 0 if xlo is None or xlo.ndim == 1 else 4 * N
@@ -765,7 +768,7 @@ def bicycle_sqp_step(x0, U, Z, yq, piq, y, pi, X, state: dict, params, ts: float
         _ptr(R), _ptr(Qf),
         _ptr(xlo), _ptr(xhi), sxb, _ptr(lb), _ptr(ub), slb, _ptr(U), _ptr(Z), _ptr(yq), _ptr(piq),
         _ptr(qp_status), _ptr(y), _ptr(pi), _ptr(X), _ptr(state["rho"]), _ptr(state["kkt"]), _ptr(state["mu"]),
-        _ptr(state["flags"]), float(tol), _stream())
+        _ptr(state["flags"]), _ptr(state.get("fix")), float(tol), _stream())
     nat.check(rc, "mpcqp_bicycle_sqp_step")
 
 

@@ -195,6 +195,16 @@ static int ipm_launch(ipm::Args<T>& a, hipStream_t st) {
   return NX == 2 ? ipm_launch_t<T, 2, 1>(a, st) : ipm_launch_t<T, 4, 2>(a, st);
 }
 
+// inertia corrections a strict QP may take before NOT_CONVEX (6; the
+// environment variable MPCQP_IPM_STRICT overrides it for experiments)
+static int strict_corrections() {
+  static const int n = [] {
+    const char* e = getenv("MPCQP_IPM_STRICT");
+    return e ? atoi(e) : 6;
+  }();
+  return n;
+}
+
 int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const void* A,
                  int64_t sA, const void* Bm, int64_t sB, const void* Q, int64_t sQ, const void* R,
                  int64_t sR, const void* Qf, int64_t sQf, const void* c, int64_t sC,
@@ -211,7 +221,7 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
     using T = decltype(tp);
     a.batch = batch; a.nx = nx; a.nu = nu; a.N = N; a.tv = (flags & MPCQP_TV) ? 1 : 0;
     a.max_iter = max_iter > 0 ? max_iter : 100;
-    a.strict = (flags & MPCQP_STRICT) ? 6 : 0;  // inertia corrections before NOT_CONVEX
+    a.strict = (flags & MPCQP_STRICT) ? strict_corrections() : 0;  // before NOT_CONVEX
     a.tol = tol > 0 ? tol : 1e-10;
     a.tol_mu = 1e-2 * a.tol;
     a.tol_polish = 1e-6;

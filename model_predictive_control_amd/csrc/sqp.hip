@@ -11,11 +11,17 @@
 //                          the first-order optimality (KKT) residual of the
 //                          NLP at the new point -- the stopping test.
 // Far from a solution the QP uses the Gauss-Newton Hessian (positive
-// definite, globally well behaved); once the KKT residual is below 1e-2 the
-// exact Hessian of the Lagrangian takes over (quadratic local convergence),
-// damped Levenberg-Marquardt style by a proximal term mu/2 |w - w_k|^2 per
-// stage: a full step divides mu by 4 (down to 0), a step that needs
-// backtracking or a QP that fails multiplies it by 4 (at least 1e-3).
+// definite, globally well behaved); once the KKT residual is below 0.3 (or
+// after 15 Gauss-Newton iterations) the exact Hessian of the Lagrangian
+// takes over (quadratic local convergence), damped Levenberg-Marquardt style
+// by a proximal term mu/2 |w - w_k|^2 per stage: a full step divides mu by 4
+// (down to 0), a step that needs backtracking multiplies it by 4 (at least
+// 1e-4).  An exact-Hessian QP that fails switches the instance to the
+// per-stage projected curvature for a few steps.  Inputs at a bound their
+// gradient pushes against are held there in the next exact-Hessian QP (a
+// proximal term on them, their search direction zero): the full Hessian is
+// indefinite along them even at the solution, while second-order
+// optimality only needs it positive definite on the free inputs.
 #include "bike.hpp"
 
 namespace mpcqp {
@@ -29,11 +35,25 @@ constexpr int kSqpProjSteps = 4;
 // row stops the instance: DONE | FAIL, the QP's status code in bits 28..30
 constexpr int kSqpMaxFails = 3;
 // KKT residual below which the exact Hessian is used (Gauss-Newton before:
-// far from a solution the costates that weight the curvature are poor)
-constexpr double kSqpSwitch = 1.0;
+// far from a solution the costates that weight the curvature are poor, and
+// the Gauss-Newton path picks the same local minimum as the oracle's)
+constexpr double kSqpSwitch = 0.3;
+// ... or after this many Gauss-Newton iterations (a large-residual instance
+// converges only linearly under Gauss-Newton)
+constexpr int kSqpGnMax = 15;
 // Levenberg-Marquardt damping of the exact-Hessian QPs: x4 after a failed QP
 // or a shortened step (at least kMuFloor), x1/4 after a full step
 constexpr double kMuFloor = 1e-4, kMuDec = 0.25;
+constexpr double kFixRho = 1e2;
+// Inputs held at their bound: an input at a bound whose NLP gradient pushes
+// against it by more than kFixGrad (the bound is strongly active) gets the
+// proximal curvature kFixRho in the next exact-Hessian QP, so the QP keeps it
+// there.  The full Hessian of this NLP is indefinite along such inputs (the
+// steering saturates where turning the other way would also pay); without
+// the term the QP, started inside the box, may run to the far bound and
+// its step is rejected, while the Hessian on the free inputs -- the one
+// second-order optimality needs -- is positive definite.
+constexpr double kFixGrad = 1e-6;
 
 // Symmetric eigen-decomposition of a 6 x 6 matrix by cyclic Jacobi sweeps,
 // fully unrolled (every index a compile-time constant: the matrix and the
@@ -148,8 +168,8 @@ __device__ __forceinline__ void project_stage(double* Hl, const double* Qw, cons
 
 __global__ __launch_bounds__(256) void bike_hess_kernel(int batch, int N, Bike p, const double* X, const double* U,
                                  const double* pi, const int32_t* flags, const double* mu,
-                                 const double* Qw, const double* Rw, double eps, double* H2,
-                                 double* q2) {
+                                 const int32_t* fix, double fix_rho, const double* Qw,
+                                 const double* Rw, double eps, double* H2, double* q2) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (int64_t)batch * N) return;
   const int64_t b = e / N;
@@ -172,6 +192,11 @@ __global__ __launch_bounds__(256) void bike_hess_kernel(int batch, int N, Bike p
   if (proj) project_stage(Hl, Qw, Rw, eps);
   if (mu)
     for (int i = 0; i < 6; ++i) Hl[i * 6 + i] += mu[b];
+  if (fix) {
+    const int32_t fb = fix[e];
+    for (int q = 0; q < 2; ++q)
+      if ((fb >> q) & 1) Hl[(4 + q) * 6 + 4 + q] += fix_rho;
+  }
   const double w[6] = {x[0], x[1], x[2], x[3], u[0], u[1]};
   // 1/2 (w - wbar)' H (w - wbar) = 1/2 w'H w - (H wbar)'w + const
   for (int i = 0; i < 6; ++i) {
@@ -195,7 +220,14 @@ struct SqpArgs {
   double *y, *pi, *X;
   double *rho, *kkt, *mu;
   int32_t* flags;
+  int32_t* fix;  // (batch, N): bit q = input q held at its bound (nullable)
   double tol;
+  int proj_steps;  // kSqpProjSteps (MPCQP_SQP_PROJ_STEPS overrides; 0: damping only)
+  int fix_mode;    // 1 (MPCQP_SQP_FIX=0 disables holding inputs at their bounds)
+  double fix_grad; // kFixGrad (MPCQP_SQP_FIX_GRAD overrides)
+  double sw;       // kSqpSwitch (MPCQP_SQP_SWITCH overrides)
+  double mu_dec;   // kMuDec (MPCQP_SQP_MU_DEC overrides)
+  int gn_max;      // kSqpGnMax (MPCQP_SQP_GN_MAX overrides)
 };
 
 // 1/2 J(U) and the l1 violation of the state box along a rollout
@@ -223,17 +255,25 @@ __device__ double box_viol(const SqpArgs& a, int64_t b, int k, const double* x) 
   return v;
 }
 
-// rollout of U + alpha d (d = Z - U), merit terms only
+// Search direction component i of instance b: Z - U, except for an input
+// the QP held at its bound (fix bit set when the QP was built), which stays
+// put -- the interior-point QP leaves such an input a barrier gap inside.
+__device__ __forceinline__ double sqp_dir(const SqpArgs& a, int64_t b, int i) {
+  const int64_t o = b * a.N * 2 + i;
+  if (a.fix && ((a.fix[b * a.N + (i >> 1)] >> (i & 1)) & 1)) return 0.0;
+  return a.Z[o] - a.U[o];
+}
+
+// rollout of U + alpha d (d = sqp_dir), merit terms only
 __device__ Merit merit_at(const SqpArgs& a, int64_t b, double alpha) {
   const int N = a.N;
   const double* U = a.U + b * N * 2;
-  const double* Z = a.Z + b * N * 2;
   double x[4];
   for (int i = 0; i < 4; ++i) x[i] = a.x0[b * a.sX0 + i];
   Merit m{0.0, 0.0};
   for (int k = 0; k < N; ++k) {
     double u[2];
-    for (int r = 0; r < 2; ++r) u[r] = fma(alpha, Z[k * 2 + r] - U[k * 2 + r], U[k * 2 + r]);
+    for (int r = 0; r < 2; ++r) u[r] = fma(alpha, sqp_dir(a, b, k * 2 + r), U[k * 2 + r]);
     m.J += 0.5 * (sq_form(a.Q, 4, x) + sq_form(a.R, 2, u));
     double xn[4];
     model_step(a.p, a.integ, x, u, xn);
@@ -260,11 +300,11 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
     const int iters = ((fl >> 8) & 0xFFFF) + 1;
     const int fails = ((fl >> 24) & 0xF) + 1;
     const int code = a.qp_status[b] & 0x7;
-    if ((fl & kSqpExact) && !(fl & kSqpProj)) {
+    if ((fl & kSqpExact) && !(fl & kSqpProj) && a.proj_steps > 0) {
       // the exact curvature made the QP fail (non-convex): the projected one
       // next (mpcqp_bicycle_hessian_convex; a caller of the plain
       // mpcqp_bicycle_hessian gets the damping below at the next failure)
-      a.flags[b] = (iters << 8) | kSqpExact | kSqpProj | (kSqpProjSteps << 24);
+      a.flags[b] = (iters << 8) | kSqpExact | kSqpProj | (a.proj_steps << 24);
     } else if (fl & kSqpExact) {
       a.mu[b] = fmax(4.0 * a.mu[b], kMuFloor);
       a.flags[b] = (iters << 8) | (fl & (kSqpExact | kSqpProj | (0xF << 24)));
@@ -276,7 +316,6 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
     return;
   }
   double* U = a.U + b * N * 2;
-  const double* Z = a.Z + b * N * 2;
   const double* yq = a.yq + b * N * 4;
   const double* piq = a.piq + b * N * 4;
   double* y = a.y + b * N * 4;
@@ -287,7 +326,7 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
   double ymax = 0.0, dmax = 0.0, umax = 0.0;
   for (int i = 0; i < 4 * N; ++i) ymax = fmax(ymax, fabs(yq[i]));
   for (int i = 0; i < 2 * N; ++i) {
-    dmax = fmax(dmax, fabs(Z[i] - U[i]));
+    dmax = fmax(dmax, fabs(sqp_dir(a, b, i)));
     umax = fmax(umax, fabs(U[i]));
   }
   const double rho = fmax(a.rho[b], 2.0 * ymax);
@@ -298,7 +337,7 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
     for (int i = 0; i < 4; ++i) x[i] = a.x0[b * a.sX0 + i];
     for (int k = 0; k < N; ++k) {
       const double u[2] = {U[2 * k], U[2 * k + 1]};
-      const double d[2] = {Z[2 * k] - u[0], Z[2 * k + 1] - u[1]};
+      const double d[2] = {sqp_dir(a, b, 2 * k), sqp_dir(a, b, 2 * k + 1)};
       m0.J += 0.5 * (sq_form(a.Q, 4, x) + sq_form(a.R, 2, u));
       for (int i = 0; i < 4; ++i) {
         double t = 0.0;
@@ -347,7 +386,16 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
       if (alpha < 1e-10) break;
     }
   }
-  for (int i = 0; i < 2 * N; ++i) U[i] = fma(alpha, Z[i] - U[i], U[i]);
+  // inputs within 1e-9 (relative) of a bound are put on it: an interior-point
+  // QP that ends unpolished leaves its active inputs that far inside, and
+  // the projected gradient would count the gap as a residual
+  for (int i = 0; i < 2 * N; ++i) {
+    double u = fma(alpha, sqp_dir(a, b, i), U[i]);
+    const int64_t o = b * a.sLb + i;
+    if (a.lb && u <= a.lb[o] + 1e-9 * (1.0 + fabs(a.lb[o]))) u = a.lb[o];
+    if (a.ub && u >= a.ub[o] - 1e-9 * (1.0 + fabs(a.ub[o]))) u = a.ub[o];
+    U[i] = u;
+  }
   for (int i = 0; i < 4 * N; ++i) {
     y[i] = fma(alpha, yq[i] - y[i], y[i]);
     pi[i] = fma(alpha, piq[i] - pi[i], pi[i]);
@@ -380,16 +428,21 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
       const double u[2] = {U[2 * k], U[2 * k + 1]};
       double A[4][4], B[4][2], xn[4];
       model_step_jac(a.p, a.integ, x, u, xn, A, B);
+      int32_t fb = 0;
       for (int q = 0; q < 2; ++q) {
         double g = 0.0;
         for (int j = 0; j < 2; ++j) g = fma(a.R[q * 2 + j], u[j], g);
         for (int i = 0; i < 4; ++i) g = fma(B[i][q], lam[i], g);
         const int64_t o = b * a.sLb + (int64_t)k * 2 + q;
-        double t = u[q] - g;
-        if (a.lb) t = fmax(t, a.lb[o]);
-        if (a.ub) t = fmin(t, a.ub[o]);
+        const double lo = a.lb ? a.lb[o] : -Lim<double>::inf();
+        const double hi = a.ub ? a.ub[o] : Lim<double>::inf();
+        const double t = fmin(fmax(u[q] - g, lo), hi);
         r = fmax(r, fabs(u[q] - t));
+        if ((u[q] <= lo + 1e-9 * (1.0 + fabs(lo)) && g > a.fix_grad) ||
+            (u[q] >= hi - 1e-9 * (1.0 + fabs(hi)) && g < -a.fix_grad))
+          fb |= 1 << q;
       }
+      if (a.fix) a.fix[b * N + k] = a.fix_mode ? fb : 0;
       // state x_{k+1}: feasibility and complementarity of y_k
       const double* xk1 = X + (k + 1) * 4;
       for (int i = 0; i < 4; ++i) {
@@ -418,11 +471,11 @@ __global__ __launch_bounds__(64) void sqp_step_kernel(SqpArgs a) {
   // ---------------------------------------------------- Hessian mode, flags
   if (fl & kSqpExact) {
     double mu = a.mu[b];
-    mu = alpha == 1.0 ? (mu > 4e-12 ? kMuDec * mu : 0.0) : fmax(4.0 * mu, kMuFloor);
+    mu = alpha == 1.0 ? (mu > 4e-12 ? a.mu_dec * mu : 0.0) : fmax(4.0 * mu, kMuFloor);
     a.mu[b] = mu;
   }
   const int iters = ((fl >> 8) & 0xFFFF) + 1;
-  const bool exact = (fl & kSqpExact) || r < kSqpSwitch;  // sticky
+  const bool exact = (fl & kSqpExact) || r < a.sw || iters >= a.gn_max;  // sticky
   // projected curvature: count full steps down, then back to the exact one
   int pc = (fl & kSqpProj) ? ((fl >> 24) & 0xF) : 0;
   if (pc > 0 && alpha == 1.0) --pc;
@@ -568,11 +621,21 @@ static Bike bike_of(double ts, const double* prm) {
   return p;
 }
 
+// proximal curvature of an input held at its bound (kFixRho; the
+// environment variable MPCQP_SQP_FIX_RHO overrides it for experiments)
+static double fix_rho() {
+  static const double r = [] {
+    const char* e = getenv("MPCQP_SQP_FIX_RHO");
+    return e ? atof(e) : mpcqp::kFixRho;
+  }();
+  return r;
+}
+
 static int bicycle_hessian_impl(const char* fn, int dtype, int batch, int N, double ts,
                                 const double* params, const void* X, const void* U,
                                 const void* pi, const int32_t* flags, const double* mu,
-                                const void* Q, const void* R, double eps, void* H2, void* q2,
-                                void* stream) {
+                                const int32_t* fix, const void* Q, const void* R, double eps,
+                                void* H2, void* q2, void* stream) {
   using namespace mpcqp;
   MPCQP_CHECK_ARG(dtype == MPCQP_F64, "%s: MPCQP_F64 only", fn);
   MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "%s: bad sizes", fn);
@@ -582,7 +645,7 @@ static int bicycle_hessian_impl(const char* fn, int dtype, int batch, int N, dou
   const int64_t total = (int64_t)batch * N;
   hipLaunchKernelGGL(bike_hess_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, batch, N, bike_of(ts, params), (const double*)X,
-                     (const double*)U, (const double*)pi, flags, mu, (const double*)Q,
+                     (const double*)U, (const double*)pi, flags, mu, fix, fix_rho(), (const double*)Q,
                      (const double*)R, eps, (double*)H2, (double*)q2);
   MPCQP_CHECK_LAUNCH("bike_hess_kernel");
   return MPCQP_OK;
@@ -590,20 +653,21 @@ static int bicycle_hessian_impl(const char* fn, int dtype, int batch, int N, dou
 
 extern "C" int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
                                      const void* X, const void* U, const void* pi,
-                                     const int32_t* flags, const double* mu, void* H2, void* q2,
-                                     void* stream) {
+                                     const int32_t* flags, const double* mu, const int32_t* fix,
+                                     void* H2, void* q2, void* stream) {
   return bicycle_hessian_impl("mpcqp_bicycle_hessian", dtype, batch, N, ts, params, X, U, pi,
-                              flags, mu, nullptr, nullptr, 0.0, H2, q2, stream);
+                              flags, mu, fix, nullptr, nullptr, 0.0, H2, q2, stream);
 }
 
 extern "C" int mpcqp_bicycle_hessian_convex(int dtype, int batch, int N, double ts,
                                             const double* params, const void* X, const void* U,
                                             const void* pi, const int32_t* flags,
-                                            const double* mu, const void* Q, const void* R,
-                                            double eps, void* H2, void* q2, void* stream) {
+                                            const double* mu, const int32_t* fix, const void* Q,
+                                            const void* R, double eps, void* H2, void* q2,
+                                            void* stream) {
   MPCQP_CHECK_ARG(Q && R && eps > 0.0, "mpcqp_bicycle_hessian_convex: Q, R and eps > 0 required");
   return bicycle_hessian_impl("mpcqp_bicycle_hessian_convex", dtype, batch, N, ts, params, X, U,
-                              pi, flags, mu, Q, R, eps, H2, q2, stream);
+                              pi, flags, mu, fix, Q, R, eps, H2, q2, stream);
 }
 
 extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,
@@ -615,7 +679,7 @@ extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,
                                       const void* Z, const void* yq, const void* piq,
                                       const int32_t* qp_status, void* y, void* pi, void* X,
                                       double* rho, double* kkt, double* mu, int32_t* flags,
-                                      double tol, void* stream) {
+                                      int32_t* fix, double tol, void* stream) {
   using namespace mpcqp;
   MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_bicycle_sqp_step: MPCQP_F64 only");
   MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "mpcqp_bicycle_sqp_step: bad sizes");
@@ -639,6 +703,37 @@ extern "C" int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts,
   a.qp_status = qp_status;
   a.y = (double*)y; a.pi = (double*)pi; a.X = (double*)X;
   a.rho = rho; a.kkt = kkt; a.mu = mu; a.flags = flags; a.tol = tol > 0 ? tol : 1e-9;
+  static const int proj_steps = [] {
+    const char* e = getenv("MPCQP_SQP_PROJ_STEPS");
+    return e ? std::min(15, std::max(0, atoi(e))) : kSqpProjSteps;
+  }();
+  a.proj_steps = proj_steps;
+  static const int fix_mode = [] {
+    const char* e = getenv("MPCQP_SQP_FIX");
+    return e ? atoi(e) : 1;
+  }();
+  a.fix = fix;
+  a.fix_mode = fix_mode;
+  static const double fix_grad = [] {
+    const char* e = getenv("MPCQP_SQP_FIX_GRAD");
+    return e ? atof(e) : kFixGrad;
+  }();
+  a.fix_grad = fix_grad;
+  static const double sw = [] {
+    const char* e = getenv("MPCQP_SQP_SWITCH");
+    return e ? atof(e) : kSqpSwitch;
+  }();
+  a.sw = sw;
+  static const double mu_dec = [] {
+    const char* e = getenv("MPCQP_SQP_MU_DEC");
+    return e ? atof(e) : kMuDec;
+  }();
+  a.mu_dec = mu_dec;
+  static const int gn_max = [] {
+    const char* e = getenv("MPCQP_SQP_GN_MAX");
+    return e ? atoi(e) : kSqpGnMax;
+  }();
+  a.gn_max = gn_max;
   hipLaunchKernelGGL(sqp_step_kernel, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0,
                      (hipStream_t)stream, a);
   MPCQP_CHECK_LAUNCH("sqp_step_kernel");

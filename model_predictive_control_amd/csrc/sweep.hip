@@ -326,7 +326,7 @@ void sweep_rows_kernel(SweepArgs a) {
 #endif
   const int b = blockIdx.x;
   const int l = threadIdx.x, g = l >> 4, c = l & 15;
-  const int n = a.n, m = a.m, np = a.np, nt = n + m;
+  const int n = a.n, m = a.m, nt = n + m;
   const int tr = (m + 15) / 16;
   const float* Hb = a.H + (int64_t)b * a.sH;
   const float* Gb = a.G + (int64_t)b * a.sG;

@@ -289,9 +289,15 @@ class SqpSolver:
 
     MU0 = 1e-3  # initial Levenberg-Marquardt damping of the exact-Hessian QPs
     # interior-point budget of one QP: a convex one takes 6-10 iterations; one
-    # that is not (strict: first non-positive pivot) or stalls is abandoned
-    # and the step kernel raises the damping instead
+    # that stalls is abandoned and the step kernel switches to the projected
+    # curvature or raises the damping instead
     QP_MAX_ITER = 40
+    # the QP takes as many inertia corrections as it needs (not strict): the
+    # exact-Hessian QP is often non-convex away from its active face while
+    # the barrier terms of the active bounds are still small; the inputs the
+    # step kernel holds at their bounds (fix) remove the directions along
+    # which it is non-convex at the solution
+    STRICT = False
 
     def __init__(self, ctl: "MPCController", b: int):
         self.ctl, self.b = ctl, b
@@ -305,11 +311,12 @@ class SqpSolver:
         self.kkt = torch.full((b,), float("inf"), **f64)
         self.mu = torch.full((b,), self.MU0, **f64)
         self.flags = torch.zeros(b, dtype=torch.int32, device=dev)
+        self.fix = torch.zeros((b, N), dtype=torch.int32, device=dev)
         self.qp = None
         self.box = ctl._box()
 
     def state(self) -> dict:
-        return dict(rho=self.rho, kkt=self.kkt, mu=self.mu, flags=self.flags)
+        return dict(rho=self.rho, kkt=self.kkt, mu=self.mu, flags=self.flags, fix=self.fix)
 
     def reset(self, U0=None):
         """Cold (U0 None: zeros) or warm start; multipliers and state cleared."""
@@ -323,6 +330,7 @@ class SqpSolver:
         self.kkt.fill_(float("inf"))
         self.mu.fill_(self.MU0)
         self.flags.zero_()
+        self.fix.zero_()
 
     def iterate(self, X0):
         ctl, N, box = self.ctl, self.ctl.N, self.box
@@ -338,9 +346,9 @@ class SqpSolver:
             # damping mu handles indefiniteness
             cw = dict(Q=ctl.Q, R=ctl.R) if ctl.hessian == "exact" else {}
             H2, q2 = batched.bicycle_hessian(Xr, self.U, self.pi, ctl.params, ctl.ts,
-                                             flags=self.flags, mu=self.mu, **cw)
+                                             flags=self.flags, mu=self.mu, fix=self.fix, **cw)
         self.qp = batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, X0, lb=ctl.lbz, ub=ctl.ubz,
-                                  c=c, tv=True, H2=H2, q2=q2, strict=True, skip=self.flags,
+                                  c=c, tv=True, H2=H2, q2=q2, strict=self.STRICT, skip=self.flags,
                                   skip_mask=SQP_DONE, max_iter=self.QP_MAX_ITER, out=self.qp,
                                   **box)
         batched.bicycle_sqp_step(X0, self.U, self.qp["z"], self.qp["y"], self.qp["pi"], self.y,
