@@ -755,7 +755,7 @@ class ConfigNLP:
     dname = "f64"
     default_batch = 4096
     default_slots = 2
-    default_sqp_iters = 30
+    default_sqp_iters = 60
     default_steps = (5, 1)  # (steps, warmup) when not given: one step is ~30 SQP iterations
 
     def __init__(self, args, dev, rank):
@@ -901,7 +901,7 @@ class ConfigLoop:
     dname = "f64"
     default_batch = 1024
     default_slots = 2
-    default_sqp_iters = 8   # per sample, warm-started from the shifted solution
+    default_sqp_iters = 12  # per sample, warm-started from the shifted solution
     default_steps = (3, 1)  # one step is a whole episode
 
     def __init__(self, args, dev, rank):
@@ -925,11 +925,13 @@ class ConfigLoop:
     def workload(self):
         return {"workload": f"loop: on-device receding-horizon loop, main.py controller (N={self.N}, "
                             f"ts=0.08, input + state box, SQP warm-started from the shifted "
-                            f"solution, at most {self.args.sqp_iters} iterations per sample) on a "
+                            f"solution, at most {self.args.sqp_iters} iterations per sample, "
+                            f"{self.loop.iters_first} for the cold first one) on a "
                             f"forward-Euler plant, {self.T} samples per episode; value counts "
                             f"only the samples whose controller call converged (KKT <= 1e-9)",
                 "horizon": self.N, "nx": 4, "nu": 2, "samples": self.T,
-                "sqp_iters_per_sample": self.args.sqp_iters}
+                "sqp_iters_per_sample": self.args.sqp_iters,
+                "sqp_iters_first_sample": self.loop.iters_first}
 
     def step(self, s):
         b = self.bufs[s]
@@ -942,6 +944,11 @@ class ConfigLoop:
     def status(self):
         return self.ST
 
+    def optimal_frac(self):
+        """Fraction of the controller calls (instance x sample, all slots)
+        that converged."""
+        return float(sum(float(b["success"].double().mean()) for b in self.bufs) / len(self.bufs))
+
     def counted_units(self, steps):
         """Closed-loop samples whose controller call converged, over the
         timed episodes."""
@@ -952,6 +959,7 @@ class ConfigLoop:
     def kernels(self, traffic):
         b = self.bufs[0]
         extra = {"success_frac_per_sample": float(b["success"].double().mean()),
+                 "episodes_all_converged_frac": float(b["success"].all(0).double().mean()),
                  "iters_per_sample_mean": float(b["iters"].double().mean()),
                  "iters_per_sample_max": int(b["iters"].max())}
         return None, {}, extra
@@ -988,7 +996,7 @@ def main():
                     help="BASELINE configs 2-5 (2 = the headline), nlp (converged "
                          "MPCController.solve), loop (on-device receding-horizon loop)")
     ap.add_argument("--sqp-iters", type=int, default=0,
-                    help="nlp: SQP iterations per solve (default 30); loop: per sample (8)")
+                    help="nlp: SQP iterations per solve (default 60); loop: per sample (12)")
     ap.add_argument("--loop-steps", type=int, default=0,
                     help="loop / 2loop: closed-loop steps per episode (default 20 / 50)")
     ap.add_argument("--gather", action="store_true",
@@ -1127,6 +1135,8 @@ def main():
     st = wl.status()
     code = batched.status_code(st)
     opt_frac = float((code == 0).double().mean())
+    if hasattr(wl, "optimal_frac"):  # the loop: per controller call, not per episode
+        opt_frac = wl.optimal_frac()
     iters = batched.status_iters(st).double()
 
     out = None

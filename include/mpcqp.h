@@ -352,13 +352,15 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
  *   mpcqp_bicycle_rti (linearise at U, states X) -> [mpcqp_bicycle_hessian]
  *   -> mpcqp_mpc_ipm (H2, q2; outputs z, y, pi) -> mpcqp_bicycle_sqp_step.
  * mpcqp_bicycle_hessian: per instance and stage, H2_k = sum_i pi_{k+1,i}
- *   d2 fe_i / d(x,u)2 at (x_k, u_k) + mu I (6 x 6 over [x; u]; mu the
+ *   d2 F_i / d(x,u)2 at (x_k, u_k) (F the prediction model's step:
+ *   integrator MPCQP_MODEL_FE or MPCQP_MODEL_RK4, the latter by the
+ *   second-order adjoint through its four stages) + mu I (6 x 6 over [x; u]; mu the
  *   instance's Levenberg-Marquardt damping, NULL = 0) and q2_k = -H2_k w_k,
  *   so that the QP's extra cost is 1/2 (w - w_k)'H2_k (w - w_k); zeros for
  *   instances whose flags lack MPCQP_SQP_EXACT (flags NULL = all exact).
  *   fix (NULL = none): one int32 per instance and stage, bit q set = input
- *   q is held at its bound: its diagonal gets a proximal 1e6 (the input
- *   stays where it is in the QP).  X ((N+1) x 4), U (N x 2), pi (N x 4) per
+ *   q is held at its bound: its diagonal gets a proximal 100 (the QP keeps
+ *   the input at its bound; the step kernel gives it no search direction).  X ((N+1) x 4), U (N x 2), pi (N x 4) per
  *   instance.
  * mpcqp_bicycle_sqp_step: per instance not yet MPCQP_SQP_DONE: step d = Z - U
  *   (Z the QP solution; an instance whose qp_status is not OPTIMAL takes no
@@ -381,8 +383,8 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
  *   step that needed backtracking or a failed QP.  rho, mu, kkt: one double
  *   per instance (rho initialised to 0).  Q, R, Qf shared (4x4, 2x2, 4x4);
  *   bounds as in mpcqp_mpc_qp (lb/ub stride strideLb).  integrator: the
- *   prediction model of the NLP (MPCQP_MODEL_FE / MPCQP_MODEL_RK4; the
- *   exact Hessian of mpcqp_bicycle_hessian is the FE model's).  fp64.
+ *   prediction model of the NLP (MPCQP_MODEL_FE / MPCQP_MODEL_RK4; pass
+ *   the same one to mpcqp_bicycle_hessian).  fp64.
  */
 #define MPCQP_SQP_DONE 1
 #define MPCQP_SQP_EXACT 2
@@ -403,7 +405,7 @@ int mpcqp_bicycle_linearise(int dtype, int batch, int N, double ts, const double
                             int integrator, const void* x0, int64_t strideX0, const void* U,
                             int64_t strideU, void* X, void* A, void* B, void* c, void* stream);
 int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
-                          const void* X, const void* U, const void* pi, const int32_t* flags,
+                          int integrator, const void* X, const void* U, const void* pi, const int32_t* flags,
                           const double* mu, const int32_t* fix, void* H2, void* q2, void* stream);
 /*
  * mpcqp_bicycle_hessian_convex: mpcqp_bicycle_hessian with a per-stage
@@ -418,7 +420,7 @@ int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* 
  * QP is taken instead of a rejected one where it is not.
  */
 int mpcqp_bicycle_hessian_convex(int dtype, int batch, int N, double ts, const double* params,
-                                 const void* X, const void* U, const void* pi,
+                                 int integrator, const void* X, const void* U, const void* pi,
                                  const int32_t* flags, const double* mu, const int32_t* fix,
                                  const void* Q, const void* R, double eps, void* H2, void* q2,
                                  void* stream);

@@ -86,10 +86,10 @@ SIGNATURES = {
                            _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int32, _i, _d, _vp,
                            ctypes.c_size_t, _vp]),
     "mpcqp_mpc_box_loop": (_i, [_i] * 6 + [_vp, _i64] * 7 + [_vp] * 3 + [_vp, _i, _d, _vp]),
-    "mpcqp_bicycle_hessian": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _vp, _vp,
-                                   _vp, _vp, _vp, _vp, _vp, _vp]),
-    "mpcqp_bicycle_hessian_convex": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _vp, _vp,
-                                          _vp, _vp, _vp, _vp, _vp, _vp, _d, _vp, _vp, _vp]),
+    "mpcqp_bicycle_hessian": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp, _vp,
+                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "mpcqp_bicycle_hessian_convex": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp,
+                                          _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _vp, _vp, _vp]),
     "mpcqp_bicycle_linearise": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp,
                                      _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "mpcqp_bicycle_sqp_step": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp, _i64,

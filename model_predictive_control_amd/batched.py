@@ -717,7 +717,8 @@ def _bike_params(params):
 
 
 def bicycle_hessian(X, U, pi, params, ts: float, flags=None, mu=None,
-                    out: tuple | None = None, Q=None, R=None, eps: float = 1e-6, fix=None):
+                    out: tuple | None = None, Q=None, R=None, eps: float = 1e-6, fix=None,
+                    integrator: int = 0):
     """Per stage, the curvature of the dynamics weighted by the costates plus
     a proximal mu I (include/mpcqp.h ``mpcqp_bicycle_hessian``): X (b, N+1,
     4), U (b, N, 2), pi (b, N, 4) fp64, mu (b,) or None -> H2 (b, N, 6, 6),
@@ -725,7 +726,8 @@ def bicycle_hessian(X, U, pi, params, ts: float, flags=None, mu=None,
     weights Q (4, 4) and R (2, 2): ``mpcqp_bicycle_hessian_convex``, the
     curvature projected so that blkdiag(Q, R) + H2 >= eps I per stage.
     fix (b, N) int32 or None: inputs held at their bound (bits written by
-    bicycle_sqp_step) get a proximal 1e6 on their diagonal."""
+    bicycle_sqp_step) get a proximal term on their diagonal.  integrator:
+    the prediction model (0 forward Euler, 1 RK4)."""
     b, N = int(U.shape[0]), int(U.shape[1])
     if out is None:
         H2 = torch.empty((b, N, 6, 6), dtype=torch.float64, device=U.device)
@@ -736,12 +738,13 @@ def bicycle_hessian(X, U, pi, params, ts: float, flags=None, mu=None,
         Qc = Q.to(torch.float64).contiguous()
         Rc = R.to(torch.float64).contiguous()
         rc = _lib().mpcqp_bicycle_hessian_convex(nat.F64, b, N, float(ts), _bike_params(params),
-                                                 _ptr(X), _ptr(U), _ptr(pi), _ptr(flags), _ptr(mu),
+                                                 int(integrator), _ptr(X), _ptr(U), _ptr(pi), _ptr(flags), _ptr(mu),
                                                  _ptr(fix), _ptr(Qc), _ptr(Rc), float(eps), _ptr(H2),
                                                  _ptr(q2), _stream())
         nat.check(rc, "mpcqp_bicycle_hessian_convex")
         return H2, q2
-    rc = _lib().mpcqp_bicycle_hessian(nat.F64, b, N, float(ts), _bike_params(params), _ptr(X),
+    rc = _lib().mpcqp_bicycle_hessian(nat.F64, b, N, float(ts), _bike_params(params),
+                                      int(integrator), _ptr(X),
                                       _ptr(U), _ptr(pi), _ptr(flags), _ptr(mu), _ptr(fix), _ptr(H2),
                                       _ptr(q2), _stream())
     nat.check(rc, "mpcqp_bicycle_hessian")

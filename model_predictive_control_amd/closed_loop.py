@@ -35,13 +35,15 @@ class ClosedLoop:
 
     ``controller.mode == "sqp"``: each step runs ``iters_per_step`` SQP
     iterations from the shifted previous solution (instances that reach the
-    KKT tolerance earlier are frozen by the step kernel); ``"rti"``: each
-    step runs the controller's ``sqp_iters`` linearise + QP steps.
+    KKT tolerance earlier are frozen by the step kernel), the first step --
+    a cold start from U = 0 -- ``iters_first`` (default: the controller's
+    ``max_iter``, at most 60); ``"rti"``: each step runs the controller's
+    ``sqp_iters`` linearise + QP steps.
     """
 
     def __init__(self, controller: MPCController, plant: str = "fe",
                  plant_params: VehicleParameters | None = None, substeps: int = 20,
-                 iters_per_step: int = 10, graph: bool = True):
+                 iters_per_step: int = 10, graph: bool = True, iters_first: int | None = None):
         if plant not in PLANTS:
             raise ValueError(f"plant must be one of {sorted(PLANTS)}, got {plant!r}")
         self.ctl = controller
@@ -49,6 +51,8 @@ class ClosedLoop:
         self.plant_params = plant_params or controller.params
         self.substeps = int(substeps)
         self.iters = int(iters_per_step)
+        self.iters_first = int(iters_first) if iters_first is not None else \
+            max(self.iters, min(controller.max_iter, 60))
         self.graph = graph
         self._graphs: dict = {}
 
@@ -79,7 +83,7 @@ class ClosedLoop:
             sqp.X[:, 1:].copy_(X)
             s["success"][t].copy_(batched.status_code(st) == 0)
             return
-        for _ in range(self.iters):
+        for _ in range(self.iters_first if t == 0 else self.iters):
             sqp.iterate(x0)
         s["success"][t].copy_(sqp.done())
         s["iters"][t].copy_(sqp.iters())

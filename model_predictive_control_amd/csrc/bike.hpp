@@ -1,6 +1,6 @@
-// bike.hpp -- the forward-Euler kinematic bicycle of session_4 as scalar
-// device functions (one instance per lane): the step, its Jacobians and the
-// curvature sum_i lam_i d2 fe_i / d(x,u)2 an exact-Hessian SQP needs.
+// bike.hpp -- the kinematic bicycle of session_4 (forward Euler and RK4) as
+// scalar device functions (one instance per lane): the step, its Jacobians
+// and the curvature sum_i lam_i d2 x+_i / d(x,u)2 an exact-Hessian SQP needs.
 // Model (rcracers is absent; restated from parameters.py:7-8,47-48 -- parity
 // unpinned), x = [p_x, p_y, psi, v], u = [a, delta]:
 //   beta = atan(k tan delta), k = l_r / (l_f + l_r)
@@ -155,6 +155,89 @@ __device__ __forceinline__ void bike_rk4_step_jac(const Bike& p, const double* x
       B[i][0] = dacc[i][4];
       B[i][1] = dacc[i][5];
     }
+}
+
+// sum_i lam_i d2 F_i / dw2 (6 x 6, row-major) of one RK4 step F(x, u) by the
+// second-order adjoint of its computational graph: with stage points z_j =
+// (s_j, u), s_j = x + c_j k_{j-1}, k_j = f(z_j) and F = x + sum_j w_j k_j,
+//   d2 (lam'F) = sum_j Dz_j' [sum_i rho_j,i d2 f_i(z_j)] Dz_j,
+// rho_j the adjoint of k_j (rho_4 = w_4 lam, rho_j = w_j lam + c_{j+1}
+// Jx_{j+1}' rho_{j+1}) and Dz_j = d z_j / dw (the forward sensitivities of
+// bike_rk4_step_jac); the continuous curvature is bike_lag_hess at ts = 1.
+__device__ __forceinline__ void bike_rk4_lag_hess(const Bike& p, const double* x, const double* u,
+                                                  const double* lam, double* H) {
+  const double h = p.ts;
+  const double cw[4] = {h / 6.0, h / 3.0, h / 3.0, h / 6.0};
+  const double cs[4] = {0.0, 0.5 * h, 0.5 * h, h};
+  double zs[4][4], S[4][4][6], J[4][4][4];
+  double k[4] = {0, 0, 0, 0}, dk[4][6];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 6; ++j) dk[i][j] = 0.0;
+  for (int s = 0; s < 4; ++s) {
+    for (int i = 0; i < 4; ++i) {
+      zs[s][i] = x[i] + cs[s] * k[i];
+      for (int j = 0; j < 6; ++j) S[s][i][j] = ((j == i) ? 1.0 : 0.0) + cs[s] * dk[i][j];
+    }
+    double f[4], Ju[4][2];
+    bike_f_jac(p, zs[s], u, f, J[s], Ju);
+    for (int i = 0; i < 4; ++i) {
+      k[i] = f[i];
+      for (int j = 0; j < 6; ++j) {
+        double t = j >= 4 ? Ju[i][j - 4] : 0.0;
+        for (int q = 0; q < 4; ++q) t = fma(J[s][i][q], S[s][q][j], t);
+        dk[i][j] = t;
+      }
+    }
+  }
+  Bike pc = p;
+  pc.ts = 1.0;
+  for (int i = 0; i < 36; ++i) H[i] = 0.0;
+  double rho[4];
+  for (int i = 0; i < 4; ++i) rho[i] = cw[3] * lam[i];
+  for (int s = 3; s >= 0; --s) {
+    // W = sum_i rho_i d2 f_i at z_s: non-zero only on (psi, v, delta)
+    double W[36];
+    const BikePt q = bike_pt(pc, zs[s], u);
+    bike_lag_hess(pc, q, zs[s], rho, W);
+    // G: the rows psi, v, delta of Dz_s (3 x 6)
+    double G[3][6];
+    for (int j = 0; j < 6; ++j) {
+      G[0][j] = S[s][2][j];
+      G[1][j] = S[s][3][j];
+      G[2][j] = j == 5 ? 1.0 : 0.0;
+    }
+    const int id[3] = {2, 3, 5};
+    double Wc[3][3];
+    for (int a = 0; a < 3; ++a)
+      for (int c = 0; c < 3; ++c) Wc[a][c] = W[id[a] * 6 + id[c]];
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 6; ++j) {
+        double t = 0.0;
+        for (int a = 0; a < 3; ++a)
+          for (int c = 0; c < 3; ++c) t = fma(G[a][i] * Wc[a][c], G[c][j], t);
+        H[i * 6 + j] += t;
+      }
+    if (s > 0) {  // rho_{s-1} = w_{s-1} lam + c_s J_s' rho_s
+      double rn[4];
+      for (int i = 0; i < 4; ++i) {
+        double t = 0.0;
+        for (int q2 = 0; q2 < 4; ++q2) t = fma(J[s][q2][i], rho[q2], t);
+        rn[i] = fma(cs[s], t, cw[s - 1] * lam[i]);
+      }
+      for (int i = 0; i < 4; ++i) rho[i] = rn[i];
+    }
+  }
+}
+
+// sum_i lam_i d2 x+_i / dw2 of the prediction model (integ as model_step)
+__device__ __forceinline__ void model_lag_hess(const Bike& p, int integ, const double* x,
+                                               const double* u, const double* lam, double* H) {
+  if (integ == 1) {
+    bike_rk4_lag_hess(p, x, u, lam, H);
+  } else {
+    const BikePt q = bike_pt(p, x, u);
+    bike_lag_hess(p, q, x, lam, H);
+  }
 }
 
 // the prediction model of the OCP: 0 = forward Euler (main.py:132-135),

@@ -166,7 +166,8 @@ __device__ __forceinline__ void project_stage(double* Hl, const double* Qw, cons
     }
 }
 
-__global__ __launch_bounds__(256) void bike_hess_kernel(int batch, int N, Bike p, const double* X, const double* U,
+__global__ __launch_bounds__(256) void bike_hess_kernel(int batch, int N, Bike p, int integ,
+                                 const double* X, const double* U,
                                  const double* pi, const int32_t* flags, const double* mu,
                                  const int32_t* fix, double fix_rho, const double* Qw,
                                  const double* Rw, double eps, double* H2, double* q2) {
@@ -186,9 +187,8 @@ __global__ __launch_bounds__(256) void bike_hess_kernel(int batch, int N, Bike p
   const double* x = X + (b * (N + 1) + k) * 4;
   const double* u = U + (b * N + k) * 2;
   const double* lam = pi + (b * N + k) * 4;  // costate of x_{k+1} = fe(x_k, u_k)
-  const BikePt pt = bike_pt(p, x, u);
   double Hl[36];
-  bike_lag_hess(p, pt, x, lam, Hl);
+  model_lag_hess(p, integ, x, u, lam, Hl);
   if (proj) project_stage(Hl, Qw, Rw, eps);
   if (mu)
     for (int i = 0; i < 6; ++i) Hl[i * 6 + i] += mu[b];
@@ -632,7 +632,7 @@ static double fix_rho() {
 }
 
 static int bicycle_hessian_impl(const char* fn, int dtype, int batch, int N, double ts,
-                                const double* params, const void* X, const void* U,
+                                const double* params, int integrator, const void* X, const void* U,
                                 const void* pi, const int32_t* flags, const double* mu,
                                 const int32_t* fix, const void* Q, const void* R, double eps,
                                 void* H2, void* q2, void* stream) {
@@ -641,10 +641,12 @@ static int bicycle_hessian_impl(const char* fn, int dtype, int batch, int N, dou
   MPCQP_CHECK_ARG(batch >= 0 && N >= 1, "%s: bad sizes", fn);
   MPCQP_CHECK_ARG(params && X && U && pi && H2 && q2, "%s: null pointer", fn);
   MPCQP_CHECK_ARG(params[1] > 0 && params[0] + params[1] > 0, "%s: bad axle lengths", fn);
+  MPCQP_CHECK_ARG(integrator == MPCQP_MODEL_FE || integrator == MPCQP_MODEL_RK4,
+                  "%s: integrator %d", fn, integrator);
   if (batch == 0) return MPCQP_OK;
   const int64_t total = (int64_t)batch * N;
   hipLaunchKernelGGL(bike_hess_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, batch, N, bike_of(ts, params), (const double*)X,
+                     (hipStream_t)stream, batch, N, bike_of(ts, params), integrator, (const double*)X,
                      (const double*)U, (const double*)pi, flags, mu, fix, fix_rho(), (const double*)Q,
                      (const double*)R, eps, (double*)H2, (double*)q2);
   MPCQP_CHECK_LAUNCH("bike_hess_kernel");
@@ -652,21 +654,24 @@ static int bicycle_hessian_impl(const char* fn, int dtype, int batch, int N, dou
 }
 
 extern "C" int mpcqp_bicycle_hessian(int dtype, int batch, int N, double ts, const double* params,
-                                     const void* X, const void* U, const void* pi,
+                                     int integrator, const void* X, const void* U, const void* pi,
                                      const int32_t* flags, const double* mu, const int32_t* fix,
                                      void* H2, void* q2, void* stream) {
-  return bicycle_hessian_impl("mpcqp_bicycle_hessian", dtype, batch, N, ts, params, X, U, pi,
+  return bicycle_hessian_impl("mpcqp_bicycle_hessian", dtype, batch, N, ts, params, integrator,
+                              X, U, pi,
                               flags, mu, fix, nullptr, nullptr, 0.0, H2, q2, stream);
 }
 
 extern "C" int mpcqp_bicycle_hessian_convex(int dtype, int batch, int N, double ts,
-                                            const double* params, const void* X, const void* U,
+                                            const double* params, int integrator, const void* X,
+                                            const void* U,
                                             const void* pi, const int32_t* flags,
                                             const double* mu, const int32_t* fix, const void* Q,
                                             const void* R, double eps, void* H2, void* q2,
                                             void* stream) {
   MPCQP_CHECK_ARG(Q && R && eps > 0.0, "mpcqp_bicycle_hessian_convex: Q, R and eps > 0 required");
-  return bicycle_hessian_impl("mpcqp_bicycle_hessian_convex", dtype, batch, N, ts, params, X, U,
+  return bicycle_hessian_impl("mpcqp_bicycle_hessian_convex", dtype, batch, N, ts, params,
+                              integrator, X, U,
                               pi, flags, mu, fix, Q, R, eps, H2, q2, stream);
 }
 

@@ -82,11 +82,9 @@ class MPCController:
             raise ValueError(f"integrator must be 'fe' or 'rk4', got {integrator!r}")
         # the prediction model: fwd_euler (main.py:132-135, the model of
         # main.py:76 and session4_sol.py:192) or runge_kutta4 (main.py:138-147,
-        # template.py:141); the exact Hessian is the FE model's, so an RK4
-        # controller iterates with Gauss-Newton
+        # template.py:141); the exact Hessian follows the model (RK4: the
+        # second-order adjoint through its four stages)
         self.integrator = integrator
-        if integrator == "rk4":
-            hessian = "gauss-newton"
         self.mode, self.hessian = mode, hessian
         self.max_iter, self.tol = int(max_iter), float(tol)
         self.nx, self.nu = 4, 2
@@ -346,7 +344,9 @@ class SqpSolver:
             # damping mu handles indefiniteness
             cw = dict(Q=ctl.Q, R=ctl.R) if ctl.hessian == "exact" else {}
             H2, q2 = batched.bicycle_hessian(Xr, self.U, self.pi, ctl.params, ctl.ts,
-                                             flags=self.flags, mu=self.mu, fix=self.fix, **cw)
+                                             flags=self.flags, mu=self.mu, fix=self.fix,
+                                             integrator=nat.MODEL_RK4 if ctl.integrator == "rk4"
+                                             else nat.MODEL_FE, **cw)
         self.qp = batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, N, X0, lb=ctl.lbz, ub=ctl.ubz,
                                   c=c, tv=True, H2=H2, q2=q2, strict=self.STRICT, skip=self.flags,
                                   skip_mask=SQP_DONE, max_iter=self.QP_MAX_ITER, out=self.qp,
