@@ -46,6 +46,7 @@ Prints ONE JSON line on rank 0 ("Measurement").
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -99,24 +100,30 @@ def sweep_flops_per_instance(n, m=0):
     return n ** 3 + 2 * m * n * n + m * m * n
 
 
-def sweep_time(H, G, n, m, reps, dev):
-    """Device time (ms) of mpcqp_sweep alone (dense output + status)."""
-    from model_predictive_control_amd import _native as nat
-    bsz = H.shape[0]
-    nt = n + m
-    M = torch.empty((bsz, nt, nt), dtype=H.dtype, device=dev)
-    st = torch.empty((bsz,), dtype=torch.int32, device=dev)
-    lib = nat.load()
-    sG = 0 if G is None else G[0].numel()
+STAGES = ("condense", "sweep", "solve", "fallback", "states")
 
-    def run():
-        rc = lib.mpcqp_sweep(nat.F32, bsz, n, m, H.data_ptr(), H[0].numel(),
-                             None if G is None else G.data_ptr(), sG, M.data_ptr(), 1,
-                             st.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        nat.check(rc, "mpcqp_sweep")
-    t = time_kernel(run, reps, dev)
-    del M
-    return t
+
+def mpc_qp_stage_ms(fn, reps: int) -> dict:
+    """Per-stage device time (ms) of one mpcqp_mpc_qp call, averaged over
+    `reps` calls of fn(): HIP events the library records on the call's own
+    stream around each stage (mpcqp_mpc_qp_profile / mpcqp_mpc_qp_stage_ms).
+    Stages the call did not run are absent."""
+    from model_predictive_control_amd import _native as nat
+    lib = nat.load()
+    nat.check(lib.mpcqp_mpc_qp_profile(1), "mpcqp_mpc_qp_profile")
+    acc, cnt = np.zeros(len(STAGES)), np.zeros(len(STAGES))
+    ms = (ctypes.c_float * len(STAGES))()
+    try:
+        fn()
+        for _ in range(reps):
+            fn()
+            nat.check(lib.mpcqp_mpc_qp_stage_ms(ms), "mpcqp_mpc_qp_stage_ms")
+            v = np.frombuffer(ms, dtype=np.float32).astype(float)
+            acc += np.where(v >= 0, v, 0.0)
+            cnt += v >= 0
+    finally:
+        nat.check(lib.mpcqp_mpc_qp_profile(0), "mpcqp_mpc_qp_profile")
+    return {k: acc[i] / cnt[i] for i, k in enumerate(STAGES) if cnt[i] > 0}
 
 
 def roof(kernel, bound, amount, ms, es_peak, unit, traffic=None, extra=None):
@@ -452,38 +459,29 @@ class Config3:
         return self.ST
 
     def kernels(self, traffic):
+        """Per-kernel rooflines of the z-space path, every stage timed by the
+        library's HIP events on the call's stream (mpc_qp_stage_ms)."""
         R = self.args.reps
         bsz, nx, nu, N, n, m = self.args.batch, self.nx, self.nu, self.N, self.n, self.m
-        out = {"H": torch.empty((bsz, n * (n + 1) // 2), dtype=self.dtype, device=self.dev),
-               "f": torch.empty((bsz, n), dtype=self.dtype, device=self.dev),
-               "Gam": torch.empty((bsz, m, n), dtype=self.dtype, device=self.dev),
-               "xbar": torch.empty((bsz, m), dtype=self.dtype, device=self.dev)}
-
-        def cond():
-            batched.condense(self.A[0], self.B[0], self.Q_t, self.R_t, self.QN_t, self.N,
-                             x0=self.X0_t[0], c=self.c[0], tv=True,
-                             outputs=("H", "f", "Gam", "xbar"), out=out)
-        cond()
-        t_c = time_kernel(cond, R, self.dev)
         t_s = time_kernel(lambda: self.step(0), R, self.dev)
-        t_w = sweep_time(out["H"], out["Gam"], n, m, R, self.dev)
-        del out
-        t_p = max(t_s - t_c - t_w, 1e-6)
-        cb = condense_bytes_per_instance(nx, nu, N, 4, tv=True, gam=True, xbar=True) * bsz
-        # pf reads M0, s0 and the dynamics (A_k, B_k, c_k, x0) for the refinement
-        pb = ((n + m) ** 2 + (n + m) + N * (nx * nx + nx * nu + nx) + nx + n + 2 * m) * 4 * bsz
-        wf = sweep_flops_per_instance(n, m) * bsz
+        st = mpc_qp_stage_ms(lambda: self.step(0), R)
+        t_c, t_w, t_z = st["condense"], st["sweep"], st["solve"]
+        # condense writes packed H, f and Gamma (the row normals); no xbar
+        cb = condense_bytes_per_instance(nx, nu, N, 4, tv=True, gam=True, xbar=False) * bsz
+        wf = sweep_flops_per_instance(n, 0) * bsz
+        # the z-space kernel reads H^-1 (n x n), s0, f, Gamma (m x n: every
+        # row is checked once at the end), the dynamics (A_k, B_k, c_k, x0)
+        # of the refinement, the shared bounds once; writes z, y, status
+        zb = (n * n + 2 * n + m * n + N * (nx * nx + nx * nu + nx) + nx + n + m + 1) * 4 * bsz
         r_c = roof("condense_kernel<float,4>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
                    traffic.get("condense"), {"bytes_per_launch": cb})
-        r_w = roof("sweep_rows_kernel<4>", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
+        r_w = roof("sweep_mfma_kernel<4> (H^-1)", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
                    traffic.get("sweep"), {"flops_per_launch": wf})
-        r_p = roof("qp_pf_kernel<3,4> (DYN refinement)", "hbm", pb, t_p, HBM_PEAK_GBS, "GB/s",
-                   traffic.get("solve_pf"), {"bytes_per_launch": pb,
-                                             "note": "time = mpc_qp - condense - sweep "
-                                                     "(includes the rows kernel)"})
-        extra = {"kernel_us": {"condense": round(t_c * 1e3, 2), "sweep": round(t_w * 1e3, 2),
-                               "solve_pf": round(t_p * 1e3, 2), "mpc_qp": round(t_s * 1e3, 2)}}
-        rs = sorted([(t_c, r_c), (t_w, r_w), (t_p, r_p)], key=lambda x: -x[0])
+        r_z = roof("qp_zf_kernel<4> (DYN refinement)", "hbm", zb, t_z, HBM_PEAK_GBS, "GB/s",
+                   traffic.get("solve_zf"), {"bytes_per_launch": zb})
+        extra = {"kernel_us": {k: round(v * 1e3, 2) for k, v in st.items()},
+                 "mpc_qp_us": round(t_s * 1e3, 2)}
+        rs = sorted([(t_c, r_c), (t_w, r_w), (t_z, r_z)], key=lambda x: -x[0])
         return rs[0][1], {"roofline_other": [r for _, r in rs[1:]]}, extra
 
     def check(self):
@@ -679,18 +677,9 @@ class Config5:
     def kernels(self, traffic):
         R = self.args.reps
         bsz, nx, nu, N, n = self.args.batch, self.nx, self.nu, self.N, self.n
-        out = {"H": torch.empty((bsz, n * (n + 1) // 2), dtype=self.dtype, device=self.dev),
-               "f": torch.empty((bsz, n), dtype=self.dtype, device=self.dev)}
-
-        def cond():
-            batched.condense(self.A[0], self.B[0], self.Q_t, self.R_t, self.Q_t, self.N,
-                             x0=self.X0_t[0], tv=True, outputs=("H", "f"), out=out)
-        cond()
-        t_c = time_kernel(cond, R, self.dev)
         t_s = time_kernel(lambda: self.step(0), R, self.dev)
-        t_w = sweep_time(out["H"], None, n, 0, R, self.dev)
-        del out
-        t_p = max(t_s - t_c - t_w, 1e-6)
+        st = mpc_qp_stage_ms(lambda: self.step(0), R)
+        t_c, t_w, t_p = st["condense"], st["sweep"], st["solve"]
         fl = condense_flops_per_instance(nx, nu, N) * bsz
         cb = condense_bytes_per_instance(nx, nu, N, 4, tv=True) * bsz
         # the survey's condensing flop formula counts the explicit Gam'QGam
@@ -705,10 +694,9 @@ class Config5:
         # pf reads M0, s0 and the dynamics (A_k, B_k, x0) for the refinement
         pb = (n * n + n + N * (nx * nx + nx * nu) + nx + n) * 4 * bsz
         r_p = roof("qp_pf_kernel<3,12> (DYN refinement)", "hbm", pb, t_p, HBM_PEAK_GBS, "GB/s",
-                   traffic.get("solve_pf"), {"bytes_per_launch": pb,
-                                             "note": "time = mpc_qp - condense - sweep"})
-        extra = {"kernel_us": {"condense": round(t_c * 1e3, 2), "sweep": round(t_w * 1e3, 2),
-                               "solve_pf": round(t_p * 1e3, 2), "mpc_qp": round(t_s * 1e3, 2)}}
+                   traffic.get("solve_pf"), {"bytes_per_launch": pb})
+        extra = {"kernel_us": {k: round(v * 1e3, 2) for k, v in st.items()},
+                 "mpc_qp_us": round(t_s * 1e3, 2)}
         rs = sorted([(t_c, r_c), (t_w, r_w), (t_p, r_p)], key=lambda x: -x[0])
         return rs[0][1], {"roofline_other": [r for _, r in rs[1:]]}, extra
 

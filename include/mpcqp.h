@@ -303,6 +303,17 @@ int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
                  const void* lb, int64_t strideLb, const void* ub, int64_t strideUb,
                  void* z, void* y, void* X, int32_t* status, int max_iter, double tol,
                  void* ws, size_t ws_bytes, void* stream);
+/*
+ * Stage timing of mpcqp_mpc_qp (profiling, one host thread): after
+ * mpcqp_mpc_qp_profile(1) every mpcqp_mpc_qp call records HIP events on its
+ * stream around its stages; mpcqp_mpc_qp_stage_ms(ms) waits for the last
+ * call's events and writes 5 floats, the milliseconds of condense, sweep,
+ * solve, fp64 fallback and states (-1 for a stage the call did not run).
+ * An enabled call cannot be captured in a graph; mpcqp_mpc_qp_profile(0)
+ * turns it off.
+ */
+int mpcqp_mpc_qp_profile(int enable);
+int mpcqp_mpc_qp_stage_ms(float* ms);
 
 /*
  * The same MPC step (same problem, arguments and outputs as mpcqp_mpc_qp) on

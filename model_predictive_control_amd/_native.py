@@ -86,6 +86,8 @@ SIGNATURES = {
                            _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int32, _i, _d, _vp,
                            ctypes.c_size_t, _vp]),
     "mpcqp_mpc_box_loop": (_i, [_i] * 6 + [_vp, _i64] * 7 + [_vp] * 3 + [_vp, _i, _d, _vp]),
+    "mpcqp_mpc_qp_profile": (_i, [_i]),
+    "mpcqp_mpc_qp_stage_ms": (_i, [ctypes.POINTER(ctypes.c_float)]),
     "mpcqp_bicycle_hessian": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp, _vp,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "mpcqp_bicycle_hessian_convex": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp,

@@ -148,7 +148,56 @@ static int launch_states(int batch, int nx, int nu, int N, int tv, const void* A
   return MPCQP_OK;
 }
 
+// Stage timing of mpcqp_mpc_qp (bench.py's per-kernel rooflines): while
+// enabled, every call records a HIP event on its stream before its first
+// launch and after each stage (condense, sweep, solve, fp64 fallback,
+// states); mpcqp_mpc_qp_stage_ms reads the last call's stage times.  A
+// profiling facility for one host thread, off by default (an enabled call
+// cannot be captured in a graph).
+struct StageProf {
+  int on = 0;
+  bool done[kProfN] = {};
+  hipEvent_t ev[kProfN] = {};
+};
+static StageProf g_prof;
+
+void prof_mark(int stage, hipStream_t st) {
+  if (!g_prof.on) return;
+  if (hipEventRecord(g_prof.ev[stage], st) == hipSuccess) g_prof.done[stage] = true;
+}
+
 }  // namespace mpcqp
+
+extern "C" int mpcqp_mpc_qp_profile(int enable) {
+  using namespace mpcqp;
+  if (enable && !g_prof.ev[0])
+    for (int i = 0; i < kProfN; ++i) {
+      const hipError_t e = hipEventCreate(&g_prof.ev[i]);
+      if (e != hipSuccess) return hip_fail(e, "mpcqp_mpc_qp_profile: hipEventCreate");
+    }
+  g_prof.on = enable ? 1 : 0;
+  return MPCQP_OK;
+}
+
+extern "C" int mpcqp_mpc_qp_stage_ms(float* ms) {
+  using namespace mpcqp;
+  MPCQP_CHECK_ARG(ms, "mpcqp_mpc_qp_stage_ms: null pointer");
+  for (int i = 0; i + 1 < kProfN; ++i) ms[i] = -1.0f;
+  if (!g_prof.done[kProfStart]) return MPCQP_OK;
+  hipError_t e;
+  int prev = kProfStart;
+  for (int i = 1; i < kProfN; ++i) {
+    if (!g_prof.done[i]) continue;
+    e = hipEventSynchronize(g_prof.ev[i]);
+    if (e != hipSuccess) return hip_fail(e, "mpcqp_mpc_qp_stage_ms: hipEventSynchronize");
+    float t = 0.0f;
+    e = hipEventElapsedTime(&t, g_prof.ev[prev], g_prof.ev[i]);
+    if (e != hipSuccess) return hip_fail(e, "mpcqp_mpc_qp_stage_ms: hipEventElapsedTime");
+    ms[i - 1] = t;
+    prev = i;
+  }
+  return MPCQP_OK;
+}
 
 // the stage-wise interior point takes the step when the caller asks for it
 // (MPCQP_IPM) or when the condensed QP exceeds the dense kernels' size
@@ -208,6 +257,8 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
   MPCQP_CHECK_ARG(ws && ws_bytes >= L.total, "mpcqp_mpc_qp: workspace %zu bytes < %zu", ws_bytes,
                   L.total);
   hipStream_t st = (hipStream_t)stream;
+  for (int i = 0; i < kProfN; ++i) g_prof.done[i] = false;
+  prof_mark(kProfStart, st);
   char* w = (char*)ws;
   const int tv = (flags & MPCQP_TV) ? 1 : 0;
   void* Hw = w + L.H;
@@ -257,6 +308,7 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
                           strideR, Qf, strideQf, c, strideC, x0, strideX0, Hw, nullptr, fw, Gw,
                           nullptr, xbw, stream);
   if (rc != MPCQP_OK) return rc;
+  prof_mark(kProfCondense, st);
   if (zf) {
     hipError_t e = hipMemsetAsync(P.cnt, 0, sizeof(int), st);
     if (e != hipSuccess) return hip_fail(e, "mpcqp_mpc_qp: hipMemsetAsync");
@@ -264,14 +316,18 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
     const float tl = tol > 0 ? (float)tol : 1e-6f;
     rc = sweep_hinv(batch, n, Hw, sH, fw, n, P.m0, P.s0, status, st);
     if (rc != MPCQP_OK) return rc;
+    prof_mark(kProfSweep, st);
     rc = launch_zf(batch, n, m, (const float*)P.m0, (const float*)P.s0, (const float*)Gw,
                    (const float*)fw, n, (const float*)lb, strideLb, (const float*)ub, strideUb,
                    (float*)z, (float*)y, status, P.cnt, P.list, mi, mpc_refine(), tl, d, st);
+    prof_mark(kProfSolve, st);
     if (rc == MPCQP_OK) rc = fallback_f64();
     if (rc != MPCQP_OK) return rc;
+    prof_mark(kProfFallback, st);
     if (X)
       rc = launch_states<float>(batch, nx, nu, N, tv, A, strideA, Bm, strideB, c, strideC, x0,
                                 strideX0, z, X, st);
+    prof_mark(kProfStates, st);
     return rc;
   }
   void* hl = sbox ? w + L.hl : nullptr;
@@ -294,7 +350,9 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
     rc = solve_two_kernel(batch, n, m, Hw, sH, fw, n, Gw, sG, hl, hu, m, lb, strideLb, ub,
                           strideUb, z, y, status, max_iter, tol, w + L.qp, st,
                           dyn_ok ? &d : nullptr, dyn_ok ? mpc_refine() : -1, f64_fb ? 0 : 1);
+    prof_mark(kProfSolve, st);
     if (rc == MPCQP_OK && f64_fb) rc = fallback_f64();
+    if (rc == MPCQP_OK && f64_fb) prof_mark(kProfFallback, st);
   } else if (m == 0) {  // input box only: the wavefront box kernels
     rc = mpcqp_solve_box(dtype, batch, n, Hw, sH, fw, n, lb, strideLb, ub, strideUb, z, status,
                          max_iter, tol, stream);
@@ -303,12 +361,14 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
                         strideUb, z, y, status, max_iter, tol, stream);
   }
   if (rc != MPCQP_OK) return rc;
+  if (!(qpb > 0)) prof_mark(kProfSolve, st);
   if (X) {
     rc = dtype == MPCQP_F64
              ? launch_states<double>(batch, nx, nu, N, tv, A, strideA, Bm, strideB, c, strideC,
                                      x0, strideX0, z, X, st)
              : launch_states<float>(batch, nx, nu, N, tv, A, strideA, Bm, strideB, c, strideC,
                                     x0, strideX0, z, X, st);
+    prof_mark(kProfStates, st);
   }
   return rc;
 }

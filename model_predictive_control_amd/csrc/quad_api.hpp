@@ -78,6 +78,10 @@ size_t qp_ws_bytes(int dtype, int batch, int n, int m);
 struct PfDyn;
 // dyn != NULL: refine from the dynamics (pf.hpp); refine < 0: default steps;
 // wg_fallback = 0: the hand-off list is left to the caller (see qp_ws_parts)
+// stage marks of mpcqp_mpc_qp's profiler (mpc_qp.hip; no-ops unless enabled)
+enum { kProfStart, kProfCondense, kProfSweep, kProfSolve, kProfFallback, kProfStates, kProfN };
+void prof_mark(int stage, hipStream_t st);
+
 int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const void* f,
                      int64_t sf, const void* G, int64_t sG, const void* hl, const void* hu,
                      int64_t sh, const void* lb, int64_t sLb, const void* ub, int64_t sUb,

@@ -356,6 +356,7 @@ int solve_two_kernel(int batch, int n, int m, const void* H, int64_t sH, const v
   if (e != hipSuccess) return hip_fail(e, "mpcqp_solve_qp_ws: hipMemsetAsync");
   int rc = sweep_launch(batch, n, m, H, sH, G, sG, M0, 1, status, st, f, sf, s0);
   if (rc != MPCQP_OK) return rc;
+  prof_mark(kProfSweep, st);
   const int mi = max_iter > 0 ? max_iter : 3 * (n + m) + 30;
   const float tl = tol > 0 ? (float)tol : 1e-6f;
   rc = launch_pf(batch, n, m, (const float*)H, sH, (const float*)f, sf, (const float*)G, sG,
