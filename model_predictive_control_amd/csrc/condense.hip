@@ -48,6 +48,7 @@ struct CondenseArgs {
   const T* x0; int64_t sX0;
   T* H; T* F; T* f; T* Gam; T* Phi; T* xbar;
   int rh, rg;  // output rings (elements, powers of two) of the streamed sweep; rh = 0: direct stores
+  const int* count = nullptr;  // device count: instances b >= *count are skipped (list mode)
 };
 
 struct CLayout {
@@ -107,6 +108,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   T* sm = reinterpret_cast<T*>(smem_raw);
   const int b = blockIdx.x;
+  if (a.count && b >= *a.count) return;  // uniform per workgroup
   const int lane = threadIdx.x;
   const int nx = a.nx, nu = a.nu, N = a.N, n = N * nu;
   const int tv = a.tv;
@@ -986,8 +988,9 @@ static int condense_t(int batch, int nx, int nu, int N, int flags, const void* A
                       const void* Bm, int64_t sB, const void* Q, int64_t sQ, const void* R,
                       int64_t sR, const void* Qf, int64_t sQf, const void* c, int64_t sC,
                       const void* x0, int64_t sX0, void* H, void* F, void* f, void* Gam,
-                      void* Phi, void* xbar, hipStream_t st) {
+                      void* Phi, void* xbar, hipStream_t st, const int* count = nullptr) {
   CondenseArgs<T> a;
+  a.count = count;
   a.batch = batch; a.nx = nx; a.nu = nu; a.N = N; a.tv = (flags & MPCQP_TV) ? 1 : 0;
   a.A = (const T*)A; a.sA = sA; a.B = (const T*)Bm; a.sB = sB;
   a.Q = (const T*)Q; a.sQ = sQ; a.R = (const T*)R; a.sR = sR;
@@ -1003,6 +1006,18 @@ static int condense_t(int batch, int nx, int nu, int N, int flags, const void* A
   if (nx <= 8) return launch_condense<T, 8>(a, st);
   if (nx <= 12) return launch_condense<T, 12>(a, st);
   return launch_condense<T, 16>(a, st);
+}
+
+// fp64 condensing of the first min(*count, batch) instances (the fp64
+// hand-off of mpcqp_mpc_qp, fallback64.hip): the per-instance kernel, the
+// workgroups past the device count return at once
+int condense_f64_count(int batch, int nx, int nu, int N, int flags, const double* A, int64_t sA,
+                       const double* Bm, int64_t sB, const double* Q, int64_t sQ, const double* R,
+                       int64_t sR, const double* Qf, int64_t sQf, const double* c, int64_t sC,
+                       const double* x0, int64_t sX0, double* H, double* f, double* Gam,
+                       double* xbar, const int* count, hipStream_t st) {
+  return condense_t<double>(batch, nx, nu, N, flags, A, sA, Bm, sB, Q, sQ, R, sR, Qf, sQf, c, sC,
+                            x0, sX0, H, nullptr, f, Gam, nullptr, xbar, st, count);
 }
 
 }  // namespace mpcqp

@@ -30,7 +30,7 @@ template <typename T, int NX, int NU>
 __global__ __launch_bounds__(64) void ipm_kernel(ipm::Args<T> a) {
   if (a.list) {
     const int cnt = *a.list_count;
-    for (int k = blockIdx.x * 64 + threadIdx.x; k < cnt; k += gridDim.x * 64)
+    for (int k = a.list_begin + blockIdx.x * 64 + threadIdx.x; k < cnt; k += gridDim.x * 64)
       ipm::solve_lane<T, NX, NU>(a, a.list[k]);
     return;
   }
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(64) void ipm_lds_kernel(ipm::Args<T> a) {
   if (lane >= G) return;
   if (a.list) {
     const int cnt = *a.list_count;
-    for (int k = blockIdx.x * G + lane; k < cnt; k += gridDim.x * G)
+    for (int k = a.list_begin + blockIdx.x * G + lane; k < cnt; k += gridDim.x * G)
       ipm::solve_lane<T, NX, NU, G>(a, a.list[k], ipm_lds + lane);
     return;
   }
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(64, 1) void ipm_quad_kernel(ipm::Args<T> a) {
   if (a.list) {
     // the group's four lanes take the same entries (uniform trip count)
     const int cnt = *a.list_count;
-    for (int k = blockIdx.x * G + g; k < cnt; k += gridDim.x * G)
+    for (int k = a.list_begin + blockIdx.x * G + g; k < cnt; k += gridDim.x * G)
       ipmq::solve_quad<T, G>(a, a.list[k], ipm_lds + g);
     return;
   }
@@ -213,7 +213,8 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
                  int64_t sU0, const void* H2, int64_t sH2, const void* q2, int64_t sq2, void* z,
                  void* y, void* X, void* lam_u, void* pi, int32_t* status,
                  const int32_t* skip, int32_t skip_mask, int max_iter, double tol, void* ws,
-                 size_t ws_bytes, hipStream_t st, const int* list, const int* list_count) {
+                 size_t ws_bytes, hipStream_t st, const int* list, const int* list_count,
+                 int list_begin) {
   const size_t need = ipm_ws_bytes(batch, nx, nu, N);
   MPCQP_CHECK_ARG(ws && ws_bytes >= need, "mpcqp_mpc_ipm: workspace %zu bytes < %zu", ws_bytes,
                   need);
@@ -236,7 +237,7 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
     a.z = (T*)z; a.y = (T*)y; a.X = (T*)X; a.lam_u = (T*)lam_u; a.pi = (T*)pi; a.status = status;
     a.skip = skip; a.skip_mask = skip_mask;
     a.ws = (double*)ws;
-    a.list = list; a.list_count = list_count;
+    a.list = list; a.list_count = list_count; a.list_begin = list_begin;
   };
   if (dtype == MPCQP_F64) {
     ipm::Args<double> a;
@@ -285,5 +286,5 @@ extern "C" int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int fl
                       strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi, strideXb, lb,
                       strideLb, ub, strideUb, U0, strideU0, H2, strideH2, q2, strideq2, z, y, X,
                       lam_u, pi, status, skip, skip_mask, max_iter, tol, ws, ws_bytes,
-                      (hipStream_t)stream, nullptr, nullptr);
+                      (hipStream_t)stream, nullptr, nullptr, 0);
 }

@@ -120,6 +120,7 @@ struct Args {
   // memory; the fp64 fallback of mpcqp_mpc_qp), on a grid sized for a few
   // of them -- an empty list costs one short launch, not one per instance
   const int* list; const int* list_count;
+  int list_begin;  // list mode: entries list_begin .. *list_count
 };
 
 constexpr double kInf = __builtin_huge_val();

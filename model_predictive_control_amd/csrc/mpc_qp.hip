@@ -81,7 +81,11 @@ static size_t al256(size_t v) { return (v + 255) / 256 * 256; }
 
 // workspace of the dense path with its fp64 fallback: the dense layout (the
 // hand-off list is in it), then the interior point's workspace
-static size_t mpc_fallback_bytes(size_t dense, size_t ipm) { return al256(dense) + ipm; }
+// the fp64 hand-off's workspace (the interior point's or fallback64.hip's
+// slots, which run one after the other) after the dense path's data
+static size_t mpc_fallback_bytes(size_t dense, size_t ipm, size_t fb64) {
+  return al256(dense) + (ipm > fb64 ? ipm : fb64);
+}
 
 struct MpcWs {
   size_t H, f, Gam, xbar, hl, hu, qp, total;
@@ -124,10 +128,15 @@ static bool mpc_zf() {
 }
 
 // MPCQP_MPC_FALLBACK=wg sends uncertified instances to the fp32 workgroup
-// kernel (flagged MPCQP_STATUS_UNREFINED) instead of the fp64 interior point
+// kernel (flagged MPCQP_STATUS_UNREFINED) instead of the fp64 hand-off;
+// =ipm keeps the whole hand-off on the fp64 interior point (A/B)
 static bool mpc_fallback_f64() {
   const char* v = getenv("MPCQP_MPC_FALLBACK");
   return !(v && v[0] == 'w');
+}
+static bool mpc_fallback_ipm_only() {
+  const char* v = getenv("MPCQP_MPC_FALLBACK");
+  return v && v[0] == 'i';
 }
 
 template <typename T>
@@ -215,9 +224,10 @@ extern "C" size_t mpcqp_mpc_qp_workspace(int dtype, int batch, int nx, int nu, i
   // room for either path (the flags are not known here)
   const size_t ipm = mpcqp::ipm_supported(nx, nu) ? mpcqp::ipm_ws_bytes(batch, nx, nu, N) : 0;
   if (mpc_use_ipm(dtype, nx, nu, N, state_box ? 1 : 0, 0)) return ipm;
-  // the dense path's fp64 fallback: the interior point's workspace over the
-  // dead condensed data, then one skip word per instance
-  return mpcqp::mpc_fallback_bytes(dense, ipm);
+  // the dense path's fp64 hand-off after the condensed data
+  const size_t fb64 =
+      dtype == MPCQP_F32 ? mpcqp::fallback64_bytes(batch, nx, nu, N, state_box ? 1 : 0) : 0;
+  return mpcqp::mpc_fallback_bytes(dense, ipm, fb64);
 }
 
 extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int flags,
@@ -288,16 +298,34 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
   // instance skipped, its workspace over the (then dead) condensed data.
   const QpWsParts P = qp_ws_parts(w + L.qp, batch, n, m);
   const size_t ipmb = ipm_supported(nx, nu) ? ipm_ws_bytes(batch, nx, nu, N) : 0;
+  const size_t fb64b = fallback64_bytes(batch, nx, nu, N, sbox);
   const bool f64_fb = dyn_ok && mpc_fallback_f64() && ipmb > 0 &&
-                      ws_bytes >= mpc_fallback_bytes(L.total, ipmb);
-  // the interior point in list mode: only the handed-back instances, read
-  // from the device list (an empty list costs one short launch)
+                      ws_bytes >= mpc_fallback_bytes(L.total, ipmb, fb64b);
+  const bool use_fb64 = f64_fb && !mpc_fallback_ipm_only() && n + m <= max_qp_size_dtype(MPCQP_F64);
+  // the first fallback64_cap(batch) listed instances: fp64 re-condensing +
+  // the fp64 workgroup active set (fallback64.hip); the rest of the list on
+  // the interior point in list mode (an empty remainder costs one short
+  // launch)
   auto fallback_f64 = [&]() -> int {
+    if (use_fb64) {
+      Fallback64In in;
+      in.batch = batch; in.nx = nx; in.nu = nu; in.N = N; in.tv = tv;
+      in.A = (const float*)A; in.sA = strideA; in.B = (const float*)Bm; in.sB = strideB;
+      in.c = (const float*)c; in.sC = strideC; in.x0 = (const float*)x0; in.sX0 = strideX0;
+      in.Q = (const float*)Q; in.sQ = strideQ; in.R = (const float*)R; in.sR = strideR;
+      in.Qf = (const float*)Qf; in.sQf = strideQf;
+      in.xlo = (const float*)xlo; in.xhi = (const float*)xhi; in.sXb = strideXb;
+      in.lb = (const float*)lb; in.sLb = strideLb; in.ub = (const float*)ub; in.sUb = strideUb;
+      const int rc = fallback64(in, P.list, P.cnt, (float*)z, (float*)y, status,
+                                w + al256(L.total), fb64b, st);
+      if (rc != MPCQP_OK) return rc;
+    }
     return mpc_ipm_impl(MPCQP_F32, batch, nx, nu, N, flags & MPCQP_TV, A, strideA, Bm, strideB, Q,
                         strideQ, R, strideR, Qf, strideQf, c, strideC, x0, strideX0, xlo, xhi,
                         strideXb, lb, strideLb, ub, strideUb, nullptr, 0, nullptr, 0, nullptr, 0, z,
                         y, nullptr, nullptr, nullptr, status, nullptr, 0, 0, 0.0,
-                        w + al256(L.total), ipmb, st, P.list, P.cnt);
+                        w + al256(L.total), ipmb, st, P.list, P.cnt,
+                        use_fb64 ? fallback64_cap(batch) : 0);
   };
   // fp32 with 48 < n <= 64 (config 3): the z-space product form -- H and f
   // (and Gamma for the row normals) are condensed, H^-1 by the MFMA sweep

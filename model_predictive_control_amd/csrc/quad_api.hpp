@@ -73,11 +73,38 @@ int mpc_ipm_impl(int dtype, int batch, int nx, int nu, int N, int flags, const v
                  void* y, void* X, void* lam_u, void* pi, int32_t* status,
                  const int32_t* skip, int32_t skip_mask, int max_iter, double tol, void* ws,
                  size_t ws_bytes, hipStream_t st, const int* list = nullptr,
-                 const int* list_count = nullptr);
+                 const int* list_count = nullptr, int list_begin = 0);
 size_t qp_ws_bytes(int dtype, int batch, int n, int m);
 struct PfDyn;
 // dyn != NULL: refine from the dynamics (pf.hpp); refine < 0: default steps;
 // wg_fallback = 0: the hand-off list is left to the caller (see qp_ws_parts)
+// condense.hip / solve_qp.hip: the fp64 kernels over the first
+// min(*count, batch) instances (compact slots of fallback64.hip)
+int condense_f64_count(int batch, int nx, int nu, int N, int flags, const double* A, int64_t sA,
+                       const double* Bm, int64_t sB, const double* Q, int64_t sQ, const double* R,
+                       int64_t sR, const double* Qf, int64_t sQf, const double* c, int64_t sC,
+                       const double* x0, int64_t sX0, double* H, double* f, double* Gam,
+                       double* xbar, const int* count, hipStream_t st);
+int solve_qp_f64_count(int batch, int n, int m, const double* H, int64_t sH, const double* f,
+                       int64_t sf, const double* G, int64_t sG, const double* hl,
+                       const double* hu, int64_t sh, const double* lb, int64_t sLb,
+                       const double* ub, int64_t sUb, double* z, double* y, int32_t* status,
+                       const int* count, hipStream_t st);
+
+// fallback64.hip: the fp64 hand-off of mpcqp_mpc_qp's fp32 paths -- the
+// first min(*count, cap) listed instances re-condensed in fp64 and solved by
+// the fp64 workgroup active set, results scattered back (status bit
+// MPCQP_STATUS_POLISHED); the rest of the list is left to the caller
+struct Fallback64In {
+  int batch, nx, nu, N, tv;
+  const float *A, *B, *c, *x0, *Q, *R, *Qf, *xlo, *xhi, *lb, *ub;
+  int64_t sA, sB, sC, sX0, sQ, sR, sQf, sXb, sLb, sUb;
+};
+int fallback64_cap(int batch);
+size_t fallback64_bytes(int batch, int nx, int nu, int N, int sbox);
+int fallback64(const Fallback64In& in, const int* list, const int* count, float* z, float* y,
+               int32_t* status, void* ws, size_t ws_bytes, hipStream_t st);
+
 // stage marks of mpcqp_mpc_qp's profiler (mpc_qp.hip; no-ops unless enabled)
 enum { kProfStart, kProfCondense, kProfSweep, kProfSolve, kProfFallback, kProfStates, kProfN };
 void prof_mark(int stage, hipStream_t st);

@@ -214,10 +214,26 @@ void qp_wg_retry_kernel(QpArgs<T> a) {
   }
 }
 
+// the first min(*retry_count, batch) instances, in place (the fp64 hand-off
+// of mpcqp_mpc_qp: compact slots): persistent workgroups walk them
+template <typename T, class S>
+__global__ __launch_bounds__(S::threads) __attribute__((amdgpu_waves_per_eu(2)))
+void qp_wg_count_kernel(QpArgs<T> a) {
+  const int c = *a.retry_count;
+  const int cnt = c < a.batch ? c : a.batch;
+  for (int t = blockIdx.x; t < cnt; t += gridDim.x) {
+    qp_wg_body<T, S>(a, t);
+    __syncthreads();
+  }
+}
+
 template <typename T, class S>
 static int launch_qp_bs(const QpArgs<T>& a, hipStream_t st) {
   const size_t bytes = (size_t)WLds<T, S>::total * sizeof(T);
-  if (a.retry_list)  // one persistent workgroup per CU walks the hand-off list
+  if (a.retry_count && !a.retry_list)  // count mode
+    hipLaunchKernelGGL((qp_wg_count_kernel<T, S>), dim3(a.batch < 512 ? a.batch : 512),
+                       dim3(S::threads), bytes, st, a);
+  else if (a.retry_list)  // one persistent workgroup per CU walks the hand-off list
     hipLaunchKernelGGL((qp_wg_retry_kernel<T, S>), dim3(a.batch < 256 ? a.batch : 256),
                        dim3(S::threads), bytes, st, a);
   else
@@ -273,6 +289,16 @@ static int solve_qp_t(int batch, int n, int m, const void* H, int64_t sH, const 
   a.retry_count = retry_count;
   a.retry_list = retry_list;
   return launch_qp<T>(a, st);
+}
+
+// fp64 solve of the first min(*count, batch) instances in place (fallback64.hip)
+int solve_qp_f64_count(int batch, int n, int m, const double* H, int64_t sH, const double* f,
+                       int64_t sf, const double* G, int64_t sG, const double* hl,
+                       const double* hu, int64_t sh, const double* lb, int64_t sLb,
+                       const double* ub, int64_t sUb, double* z, double* y, int32_t* status,
+                       const int* count, hipStream_t st) {
+  return solve_qp_t<double>(batch, n, m, H, sH, f, sf, G, sG, hl, hu, sh, lb, sLb, ub, sUb, z, y,
+                            status, 0, 0.0, st, nullptr, count, nullptr);
 }
 
 // used by mpcqp_solve_box for n > 64

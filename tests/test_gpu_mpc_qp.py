@@ -263,12 +263,14 @@ def test_mpc_qp_f32_near_active_bound_stays_optimal(dev):
     assert err < TOL_F32, err
 
 
-@pytest.mark.parametrize("fallback", ["f64", "wg"])
+@pytest.mark.parametrize("fallback", ["f64", "ipm", "wg"])
 def test_mpc_qp_handoff(dev, monkeypatch, fallback):
     """More than 64 active constraints send an fp32 instance of the refined
-    path back from the product-form kernel.  By default it is solved again by
-    the stage-wise fp64 interior point with its exact polish (status bit
-    STATUS_POLISHED, code OPTIMAL, fp64 accuracy); with MPCQP_MPC_FALLBACK=wg
+    path back from the product-form kernel.  By default it is solved again in
+    fp64 (fallback64.hip: fp64 re-condensing + the fp64 workgroup active set,
+    exact vertex solution; status bit STATUS_POLISHED, code OPTIMAL, fp64
+    accuracy); with MPCQP_MPC_FALLBACK=ipm by the stage-wise fp64 interior
+    point with its exact polish (same flag); with MPCQP_MPC_FALLBACK=wg
      by the fp32 workgroup kernel on the condensed QP, without the
     refinement against the dynamics: status STATUS_UNREFINED.  An instance
     with few active bounds in the same batch keeps the refined path and no
@@ -276,8 +278,8 @@ def test_mpc_qp_handoff(dev, monkeypatch, fallback):
     |u| <= 1e-3."""
     from model_predictive_control_amd import _native as nat
 
-    if fallback == "wg":
-        monkeypatch.setenv("MPCQP_MPC_FALLBACK", "wg")
+    if fallback != "f64":
+        monkeypatch.setenv("MPCQP_MPC_FALLBACK", fallback)
     N = 60
     t = lambda a: torch.as_tensor(np.asarray(a, float), dtype=torch.float32, device=dev)  # noqa: E731
     A, B = t([[0.9]]), t([[1.0, 1.0]])
@@ -288,7 +290,7 @@ def test_mpc_qp_handoff(dev, monkeypatch, fallback):
     torch.cuda.synchronize()
     st = st.cpu().numpy()
     assert (st & 0xFF == 0).all(), st
-    flag = nat.STATUS_POLISHED if fallback == "f64" else nat.STATUS_UNREFINED
+    flag = nat.STATUS_UNREFINED if fallback == "wg" else nat.STATUS_POLISHED
     assert st[0] & flag and not st[1] & (nat.STATUS_UNREFINED | nat.STATUS_POLISHED), st
     zn = z.cpu().numpy()
     # the oracle on the values the device sees (0.9 rounded to fp32)
@@ -299,7 +301,7 @@ def test_mpc_qp_handoff(dev, monkeypatch, fallback):
     # fp64 fallback: the fp64 solution (to the fp32 output rounding); the
     # workgroup kernel: the fp32 condensed QP's accuracy (the state box is
     # not active)
-    assert np.abs(zn[0] - zr).max() < (1e-9 if fallback == "f64" else 1e-4)
+    assert np.abs(zn[0] - zr).max() < (1e-4 if fallback == "wg" else 1e-9)
     assert np.abs(zn[1]).max() < 1e-9                   # x0 = 0: z = 0
 
 
