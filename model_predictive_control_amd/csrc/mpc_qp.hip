@@ -134,6 +134,12 @@ static bool mpc_fallback_f64() {
   const char* v = getenv("MPCQP_MPC_FALLBACK");
   return !(v && v[0] == 'w');
 }
+// MPCQP_MPC_FALLBACK=none (diagnostics): no hand-off, the fp32 kernels'
+// hand-off status (0x7f, reason in bits 24..27) is left in place
+static bool mpc_fallback_none() {
+  const char* v = getenv("MPCQP_MPC_FALLBACK");
+  return v && v[0] == 'n';
+}
 static bool mpc_fallback_ipm_only() {
   const char* v = getenv("MPCQP_MPC_FALLBACK");
   return v && v[0] == 'i';
@@ -307,6 +313,7 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
   // the interior point in list mode (an empty remainder costs one short
   // launch)
   auto fallback_f64 = [&]() -> int {
+    if (mpc_fallback_none()) return MPCQP_OK;
     if (use_fb64) {
       Fallback64In in;
       in.batch = batch; in.nx = nx; in.nu = nu; in.N = N; in.tv = tv;

@@ -59,7 +59,13 @@ struct ZfArgs {
   PfDyn d;
 };
 
-constexpr int kZfRowBufs = 16;  // normals of active state rows held in LDS
+// Normals of active state rows: the first kZfRowBufs - 1 in LDS buffers, the
+// last buffer the entering row's (transient) once those are taken; a row slot
+// past them reads its normal from the condensed Gamma (sbuf = kZfGlobal) --
+// an instance with more than 15 active state rows (1 % of config 3) stays on
+// the fp32 path instead of going to the fp64 hand-off
+constexpr int kZfRowBufs = 16;
+constexpr int kZfGlobal = 31;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -120,7 +126,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
     }
   }
   zmu[l] = 0.f;
-  int code = MPCQP_STATUS_OPTIMAL, iters = 0;
+  int code = MPCQP_STATUS_OPTIMAL, iters = 0, why = 0;  // why: hand-off reason (status bits 24..27)
   {
     const int pre = a.status[b];  // the sweep's (non-finite data, non-PD pivot)
     if (pre) code = pre;
@@ -247,7 +253,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
       float bs = 0.f;
       if (stype == 0) {
         bs = ssgn * pubB[sidx];
-      } else if (stype == 1) {
+      } else if (stype == 1 && sbuf != kZfGlobal) {
         const float* nv = nrm[sbuf];
         float acc = 0.f;
 #pragma unroll
@@ -257,6 +263,20 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
           acc = fmaf(a4.x, v4.x, fmaf(a4.y, v4.y, fmaf(a4.z, v4.z, fmaf(a4.w, v4.w, acc))));
         }
         bs = ssgn * acc;
+      }
+      // row slots past the LDS buffers: one coalesced Gamma row and a wave
+      // sum each (uniform loop)
+      uint64_t gs = __builtin_amdgcn_ballot_w64(stype == 1 && sbuf == kZfGlobal);
+      if (gs) {
+        const float pv = pubB[l];
+        while (gs) {
+          const int sl = __builtin_ctzll(gs);
+          gs &= gs - 1;
+          int e = (b * m + readlane(sidx, sl)) * n + l;
+          asm volatile("" : "+v"(e));
+          const float dsum = wave_sum(l < n ? a.Gam[e] * pv : 0.f);
+          if (l == sl) bs = ssgn * dsum;
+        }
       }
       return bs;
     };
@@ -273,7 +293,15 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
         rows &= rows - 1;
         const float coef = readlane(ssgn * cs, s);
         const int bb = readlane(sbuf, s);
-        acc = fmaf(coef, nrm[bb][l], acc);
+        float nv;
+        if (bb != kZfGlobal) {
+          nv = nrm[bb][l];
+        } else {
+          int e = (b * m + readlane(sidx, s)) * n + l;
+          asm volatile("" : "+v"(e));
+          nv = l < n ? a.Gam[e] : 0.f;
+        }
+        acc = fmaf(coef, nv, acc);
       }
       wave_lds_sync();
       pubA[l] += acc;
@@ -414,11 +442,8 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
           const float psgn = side == 1 ? 1.f : -1.f;
           int pb = 0;
           if (isrow) {
-            if (bufs == (1u << kZfRowBufs) - 1) {
-              code = kStatusRetry;
-              goto out;
-            }
-            pb = __builtin_ctz(~bufs);
+            constexpr unsigned keep = (1u << (kZfRowBufs - 1)) - 1;
+            pb = (bufs & keep) == keep ? kZfRowBufs - 1 : __builtin_ctz(~bufs);
             row_normal(pj, pb);
           }
           // a = H^-1 n_p
@@ -484,7 +509,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
               if (kt == 0 && l == ki) zst = 0;
               if (kt == 1) {
                 if (l == 0) rst[ki] = 0;
-                bufs &= ~(1u << kb);
+                if (kb < kZfRowBufs - 1) bufs &= ~(1u << kb);
               }
               if (l == k) {
                 stype = -1;
@@ -497,7 +522,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
                 goto out;
               }
               if (~used == 0) {
-                code = kStatusRetry;
+                code = kStatusRetry; why = 2;  // working set full
                 goto out;
               }
               const int snew = __builtin_ctzll(~used);
@@ -506,7 +531,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
               if (l == snew) {
                 stype = isrow ? 1 : 0;
                 sidx = isrow ? pj : p;
-                sbuf = pb;
+                sbuf = pb == kZfRowBufs - 1 ? kZfGlobal : pb;
                 ssgn = psgn;
                 su = tau;
                 sul = 0.f;
@@ -517,7 +542,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
               }
               if (isrow) {
                 if (l == 0) rst[pj] = side;
-                bufs |= 1u << pb;
+                if (pb < kZfRowBufs - 1) bufs |= 1u << pb;
               }
               added = true;
             }
@@ -695,7 +720,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
       if (code != MPCQP_STATUS_OPTIMAL) break;
       if (decided && !(pv > kDynTol) && !(dv > 0.f)) break;  // certified
       if (!decided || round + 1 >= kDynRounds) {
-        code = kStatusRetry;
+        code = kStatusRetry; why = decided ? 4 : 3;  // rounds spent / undecided
         break;
       }
       if (dv > 0.f) {
@@ -705,19 +730,19 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
         const int want = isz ? 0 : 1;
         const int q = uniform(__builtin_ctzll(__builtin_amdgcn_ballot_w64(stype == want && sidx == key) | (1ull << 63)));
         if (q == 63 && !(readlane(stype, 63) == want && readlane(sidx, 63) == key)) {
-          code = kStatusRetry;
+          code = kStatusRetry; why = 5;
           break;
         }
         const int qb = readlane(sbuf, q);
         if (!s_drop(q)) {
-          code = kStatusRetry;
+          code = kStatusRetry; why = 5;
           break;
         }
         used &= ~(1ull << q);
         if (isz && l == key) zst = 0;
         if (!isz) {
           if (l == 0) rst[key] = 0;
-          bufs &= ~(1u << qb);
+          if (qb < kZfRowBufs - 1) bufs &= ~(1u << qb);
         }
         if (l == q) {
           stype = -1;
@@ -733,7 +758,7 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
     // a non-finite final state: the fp64 fallback
     if (code == MPCQP_STATUS_OPTIMAL || code == MPCQP_STATUS_MAXITER) {
       const bool nf = !finite(z) || !finite(su);
-      if (__builtin_amdgcn_ballot_w64(nf)) code = kStatusRetry;
+      if (__builtin_amdgcn_ballot_w64(nf)) { code = kStatusRetry; why = 6; }
     }
   }
 out:
@@ -753,7 +778,7 @@ out:
       }
     }
     if (l == 0) {
-      a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8);
+      a.status[b] = (code & 0xff) | ((iters & 0xffff) << 8) | (code == kStatusRetry ? why << 24 : 0);
       if (code == kStatusRetry) a.retry_list[atomicAdd(a.retry_count, 1)] = b;
     }
   }
