@@ -133,6 +133,8 @@ def solve_map(worker, make_args, total: int, cores: int | None = None) -> list:
     """``worker`` over chunks [lo, hi) of ``total`` instances on ``cores``
     spawned processes (one BLAS thread each); the per-instance results in
     order."""
+    if total <= 0:
+        return []
     cores = min(cores or host_cores(), max(1, total))
     ctx = mp.get_context("spawn")
     saved = {k: os.environ.get(k) for k in _BLAS_ENV}
