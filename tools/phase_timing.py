@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CS = os.environ.get("PT_CS", os.path.join(ROOT, "model_predictive_control_amd", "csrc"))
 LIB = os.path.join(ROOT, "model_predictive_control_amd", "lib", "libmpcqp_timing.so")
 SRCS = ["api.cpp", "condense.hip", "solve_box.hip", "solve_poly.hip", "mpc_box.hip", "quad_box.hip",
-        "solve_qp.hip", "sweep.hip", "solve_pf.hip", "solve_zf.hip", "mpc_qp.hip", "bicycle.hip", "misc.hip",
+        "solve_qp.hip", "sweep.hip", "solve_pf.hip", "solve_zf.hip", "fallback64.hip", "mpc_qp.hip", "bicycle.hip", "misc.hip",
         "ipm.hip", "sqp.hip", "loop_box.hip"]
 PHASES = ["stage-in", "Riccati", "xbar/adjoint", "-H^-1 columns", "GI: refresh/recheck", "GI: scan+argmax", "GI: pivot col+ratio", "GI: sweep"]
 
