@@ -603,7 +603,7 @@ class Config4:
         nchk = min(self.args.check, self.args.batch)
         sols = parallel.solve_map(parallel.cfg4_solve, lambda lo, hi: (
             d["H"], d["F"], self.G, self.h, self.X0[0, lo:hi]), nchk)
-        return float(max(np.abs(Z[i] - zr).max() for i, zr in enumerate(sols)))
+        return float(max(np.abs(Z[i] - zr).max() for i, zr in enumerate(sols))) if sols else None
 
     def cpu_baseline(self, seconds):
         from oracle import condense as oc
@@ -711,7 +711,7 @@ class Config5:
         nchk = min(self.args.check, self.args.batch)
         sols = parallel.solve_map(parallel.cfg5_solve, lambda lo, hi: (
             A[lo:hi], B[lo:hi], X0[lo:hi], Q, Rm, N, self.lb, self.ub), nchk)
-        return float(max(np.abs(Z[i] - zr).max() for i, zr in enumerate(sols)))
+        return float(max(np.abs(Z[i] - zr).max() for i, zr in enumerate(sols))) if sols else None
 
     def cpu_baseline(self, seconds):
         from oracle import parallel
