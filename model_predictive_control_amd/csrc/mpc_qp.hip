@@ -359,10 +359,11 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
     if (rc == MPCQP_OK) rc = fallback_f64();
     if (rc != MPCQP_OK) return rc;
     prof_mark(kProfFallback, st);
-    if (X)
+    if (X) {
       rc = launch_states<float>(batch, nx, nu, N, tv, A, strideA, Bm, strideB, c, strideC, x0,
                                 strideX0, z, X, st);
-    prof_mark(kProfStates, st);
+      prof_mark(kProfStates, st);
+    }
     return rc;
   }
   void* hl = sbox ? w + L.hl : nullptr;

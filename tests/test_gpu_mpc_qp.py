@@ -331,3 +331,27 @@ def test_mpc_qp_cfg3_parity_tail(dev, golden):
         assert (code == 0).all(), np.unique(code, return_counts=True)
         err = np.abs(z.double().cpu().numpy() - np.repeat(g["z"], reps, 0)).max(1)
         assert err.max() < TOL_F32, (reps, err.reshape(k, reps).max(1))
+
+
+def test_mpc_qp_stage_profiler(dev):
+    """mpcqp_mpc_qp_profile / mpcqp_mpc_qp_stage_ms: HIP events around the
+    stages of one call -- positive times for the stages the config-3 path
+    runs (condense, sweep, solve, hand-off), -1 for states when not asked,
+    nothing recorded once profiling is off; the solution is unchanged."""
+    import ctypes
+
+    from model_predictive_control_amd import _native as nat
+
+    lib = nat.load()
+    ms = (ctypes.c_float * 5)()
+    pb0, (z0, _, _) = _run_cfg3(dev, torch.float32, b=64)
+    nat.check(lib.mpcqp_mpc_qp_profile(1), "mpcqp_mpc_qp_profile")
+    try:
+        _, (z1, _, st) = _run_cfg3(dev, torch.float32, b=64)
+        nat.check(lib.mpcqp_mpc_qp_stage_ms(ms), "mpcqp_mpc_qp_stage_ms")
+    finally:
+        nat.check(lib.mpcqp_mpc_qp_profile(0), "mpcqp_mpc_qp_profile")
+    v = list(ms)
+    assert all(t > 0.0 for t in v[:4]), v
+    assert v[4] == -1.0, v
+    assert torch.equal(z0, z1)
