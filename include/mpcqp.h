@@ -379,7 +379,9 @@ int mpcqp_mpc_ipm(int dtype, int batch, int nx, int nu, int N, int flags,
  *   (MPCQP_SQP_PROJ) and, if that QP fails too, its damping mu grows x4; in Gauss-Newton mode
  *   three failures in a row stop it with flags DONE | MPCQP_SQP_FAIL and the
  *   QP's status code in bits 28..30), L1 merit 1/2 J + rho |state-box violation|_1 with
- *   rho >= 2 max|yq|, Armijo backtracking by quadratic interpolation; then
+ *   rho >= 2 max|yq|, Armijo backtracking by quadratic interpolation (after
+ *   five shortened exact-Hessian steps in a row, one full step without the
+ *   test; flags bits 4..7 count them); then
  *   U += alpha d, y += alpha (yq - y), pi += alpha (piq - pi), the rollout X
  *   ((N+1) x 4) at the new U and the first-order optimality residual of the
  *   NLP there (projected gradient of the Lagrangian on the input box,
