@@ -32,6 +32,7 @@ non-convex and out of scope.
 from __future__ import annotations
 
 import inspect
+import os
 import warnings
 
 import numpy as np
@@ -288,8 +289,11 @@ class SqpSolver:
     MU0 = 1e-3  # initial Levenberg-Marquardt damping of the exact-Hessian QPs
     # interior-point budget of one QP: a convex one takes 6-10 iterations; one
     # that stalls is abandoned and the step kernel switches to the projected
-    # curvature or raises the damping instead
-    QP_MAX_ITER = 40
+    # curvature or raises the damping instead.  Every launch lasts as long as
+    # its slowest QP, so the cap is also the batch's per-iteration time: 25
+    # against 40 is +18 % converged NLP solves/s at 0.992 instead of 0.994
+    # converged in 60 iterations (MPCQP_SQP_QP_MAX_ITER overrides)
+    QP_MAX_ITER = int(os.environ.get("MPCQP_SQP_QP_MAX_ITER", "25"))
     # the QP takes as many inertia corrections as it needs (not strict): the
     # exact-Hessian QP is often non-convex away from its active face while
     # the barrier terms of the active bounds are still small; the inputs the
