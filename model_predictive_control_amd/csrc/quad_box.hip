@@ -9,12 +9,6 @@
 #include "quad.hpp"
 #include "quad_api.hpp"
 
-// QPs per wave of the fused MPC kernel (A/B: fewer than the layout's groups
-// leaves the others idle and puts more waves on each SIMD)
-#ifndef MPCQP_QPW
-#define MPCQP_QPW 0
-#endif
-
 namespace mpcqp {
 
 template <typename T, int BS>
@@ -170,11 +164,10 @@ __global__ __launch_bounds__(64, OCC) void mpc_group_kernel(MpcArgsQ<T> a) {
   constexpr int NV = BL::NV;
   constexpr int RPL = Mat::RPL;
   constexpr int GPW = kWave / GL;
-  constexpr int QPW = (MPCQP_QPW > 0 && MPCQP_QPW < GPW) ? MPCQP_QPW : GPW;  // live groups
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int lane = threadIdx.x, g = lane / GL, q = lane % GL;
-  const int b = blockIdx.x * QPW + g;
-  const bool live = g < QPW && b < a.batch;
+  const int b = blockIdx.x * GPW + g;
+  const bool live = b < a.batch;
   const int bl = live ? b : 0;
   const int nx = a.nx, nu = a.nu, N = a.N, n = N * nu, tv = a.tv;
   const int S = tv ? N : 1;
@@ -599,7 +592,6 @@ int solve_box_quad(const BoxArgsQ<T>& a, hipStream_t st) {
 template <typename T, int NX, int NU, class Mat, int GL, int OCC>
 int launch_mpc_group(const MpcArgsQ<T>& a, hipStream_t st) {
   constexpr int GPW = kWave / GL;
-  constexpr int QPW = (MPCQP_QPW > 0 && MPCQP_QPW < GPW) ? MPCQP_QPW : GPW;
   const int n = a.N * a.nu;
   const QMpcLds<T, NX, NU, Mat> L(a.N, n, a.tv);
   const size_t bytes = (size_t)GPW * L.total * sizeof(T);
@@ -613,7 +605,7 @@ int launch_mpc_group(const MpcArgsQ<T>& a, hipStream_t st) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(mpc_group)");
   }
-  hipLaunchKernelGGL(kern, dim3((a.batch + QPW - 1) / QPW), dim3(kWave), bytes, st, a);
+  hipLaunchKernelGGL(kern, dim3((a.batch + GPW - 1) / GPW), dim3(kWave), bytes, st, a);
   MPCQP_CHECK_LAUNCH("mpc_group_kernel");
   return MPCQP_OK;
 }
