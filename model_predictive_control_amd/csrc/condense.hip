@@ -661,6 +661,17 @@ static int launch_condense(CondenseArgs<T> a, hipStream_t st) {
 // column c in lane (g, c), so each H row segment is one 64-lane store.
 // NT: Gamma tiles (n <= 16 NT); NU4: What rows held per lane (nu <= NU4);
 // DRIFT: per-stage c_k present (its loads get their own queue)
+//
+// State slots: tile position pos = 4g + s holds state cm_state(pos) -- states
+// 0..11 in registers s = 0..2, states 12..14 and the affine slot in register
+// s = 3 of the four lane groups.  For nx <= 12 the K chunk s = 3 of Gamma~
+// (states 12..14 and the affine row, all zero in Gamma~) is then empty, and
+// the forward product A~ Gamma~ -- three quarters of the kernel's MFMA work --
+// runs three of the four 16x16x4 instructions.
+__device__ __forceinline__ int cm_state(int pos) {
+  const int g = pos >> 2, s = pos & 3;
+  return s < 3 ? 3 * g + s : (g < 3 ? 12 + g : 15);
+}
 template <int NT, int NU4, bool DRIFT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 void condense_mfma_kernel(CondenseArgs<float> a) {
@@ -692,12 +703,13 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int p = 4 * g + s;  // C layout: register s of lane (g, cl) is row 4g+s, column cl
-    oAb[s] = (p < nx && cl < nx) ? 4 * (p * nx + cl) : kOOB;
-    oCb[s] = (p < nx && cl == 15) ? 4 * p : kOOB;
-    oBb[s] = (p < nx && cl < nu) ? 4 * (p * nu + cl) : kOOB;
+    const int sp = cm_state(p), sc = cm_state(cl);
+    oAb[s] = (sp < nx && sc < nx) ? 4 * (sp * nx + sc) : kOOB;
+    oCb[s] = (sp < nx && cl == 15) ? 4 * sp : kOOB;
+    oBb[s] = (sp < nx && cl < nu) ? 4 * (sp * nu + cl) : kOOB;
     one_b[s] = (p == 15 && cl == 15) ? 1.f : 0.f;
-    oAf[s] = (cl < nx && p < nx) ? 4 * (cl * nx + p) : kOOB;  // forward: row cl, column p
-    oCf[s] = (cl < nx && p == 15) ? 4 * cl : kOOB;
+    oAf[s] = (sc < nx && sp < nx) ? 4 * (sc * nx + sp) : kOOB;  // forward: row cl, column p
+    oCf[s] = (sc < nx && p == 15) ? 4 * sc : kOOB;
     one_f[s] = (cl == 15 && p == 15) ? 1.f : 0.f;
   }
   auto stage_rsrc = [&](int k, rsrc_t& ra, rsrc_t& rb, rsrc_t& rc) {
@@ -710,10 +722,9 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
   float wB[4], qC[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int p = 4 * g + s;
-    wB[s] = (p < nx && cl < nx) ? a.Qf[(int64_t)b * a.sQf + p * nx + cl] : 0.f;
-    const int pc = 4 * g + s;
-    qC[s] = (pc < nx && cl < nx) ? a.Q[(int64_t)b * a.sQ + pc * nx + cl] : 0.f;
+    const int sp = cm_state(4 * g + s), sc = cm_state(cl);
+    wB[s] = (sp < nx && sc < nx) ? a.Qf[(int64_t)b * a.sQf + sp * nx + sc] : 0.f;
+    qC[s] = (sp < nx && sc < nx) ? a.Q[(int64_t)b * a.sQ + sp * nx + sc] : 0.f;
   }
   auto load_bw = [&](int k, float (&ao)[4], float (&co)[4], float (&bo)[4]) {
     (void)co;
@@ -790,10 +801,10 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
     const float* X0b = a.x0 ? a.x0 + (int64_t)b * a.sX0 : nullptr;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int p = 4 * g + s;
+      const int p = 4 * g + s, sp = cm_state(p), sc = cm_state(cl);
       float v = 0.f;
-      if (p < nx && cl < nx) v = (p == cl) ? 1.f : 0.f;
-      else if (cl == 15) v = (p < nx) ? (X0b ? X0b[p] : 0.f) : (p == 15 ? 1.f : 0.f);
+      if (sp < nx && sc < nx) v = (p == cl) ? 1.f : 0.f;
+      else if (cl == 15) v = (sp < nx) ? (X0b ? X0b[sp] : 0.f) : (p == 15 ? 1.f : 0.f);
       eB[s] = v;
     }
   }
@@ -811,8 +822,8 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
     const int q = (cl - r * nu) & 15;  // this lane's column offset in block r (mod 16)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int p = 4 * g + j;
-      bo[j] = bld(rb, (p < nx && q < nu) ? 4 * (p * nu + q) : kOOB);
+      const int sp = cm_state(4 * g + j);
+      bo[j] = bld(rb, (sp < nx && q < nu) ? 4 * (sp * nu + q) : kOOB);
     }
   };
   constexpr int PFF = 2;  // forward prefetch depth (the stage body is large)
@@ -836,12 +847,25 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
     MPCQP_PHASE(1);
     // all MFMA chains first (independent tiles overlap in the matrix pipe),
     // then the VALU epilogue per tile
+    if (nx <= 12) {  // K chunk 3 of Gamma~ is empty (cm_state)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      if (t < ntact) {
-        const mf4 dd = mfma4(aA, gB[t], mf4{0.f, 0.f, 0.f, 0.f});
+      for (int t = 0; t < NT; ++t) {
+        if (t < ntact) {
+          mf4 dd = mf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) gB[t][s] = dd[s];
+          for (int s = 0; s < 3; ++s) dd = __builtin_amdgcn_mfma_f32_16x16x4f32(aA[s], gB[t][s], dd, 0, 0, 0);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) gB[t][s] = dd[s];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (t < ntact) {
+          const mf4 dd = mfma4(aA, gB[t], mf4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+          for (int s = 0; s < 4; ++s) gB[t][s] = dd[s];
+        }
       }
     }
     float eC[4];
@@ -866,8 +890,8 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
         if (a.Gam) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int p = 4 * g + j;
-            bst(d[j], rG, (p < nx && col < n) ? 4 * ((r * nx + p) * n + col) : kOOB);
+            const int sp = cm_state(4 * g + j);
+            bst(d[j], rG, (sp < nx && col < n) ? 4 * ((r * nx + sp) * n + col) : kOOB);
           }
         }
 #pragma unroll
@@ -891,8 +915,8 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
       } else if (a.Gam && 16 * t < n) {  // structural zeros of the block row
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int p = 4 * g + j;
-          bst(0.f, rG, (p < nx && col < n) ? 4 * ((r * nx + p) * n + col) : kOOB);
+          const int sp = cm_state(4 * g + j);
+          bst(0.f, rG, (sp < nx && col < n) ? 4 * ((r * nx + sp) * n + col) : kOOB);
         }
       }
     }
@@ -901,9 +925,9 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
       float(&d)[4] = eC;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int p = 4 * g + j;
-        if (a.xbar) bst(d[j], rX, (p < nx && cl == 15) ? 4 * (r * nx + p) : kOOB);
-        if (a.Phi) bst(d[j], rP, (p < nx && cl < nx) ? 4 * ((r * nx + p) * nx + cl) : kOOB);
+        const int sp = cm_state(4 * g + j), sc = cm_state(cl);
+        if (a.xbar) bst(d[j], rX, (sp < nx && cl == 15) ? 4 * (r * nx + sp) : kOOB);
+        if (a.Phi) bst(d[j], rP, (sp < nx && sc < nx) ? 4 * ((r * nx + sp) * nx + sc) : kOOB);
       }
       if (wantFf) {
 #pragma unroll
@@ -920,7 +944,7 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
           const float h = (P[0] + P[1]) + (P[2] + P[3]);
           const int i = 4 * ic + g;
           const int R = blk0 + i;
-          if (a.F) bst(h, rF, (i < nu && cl < nx) ? 4 * (R * nx + cl) : kOOB);
+          if (a.F) bst(h, rF, (i < nu && cm_state(cl) < nx) ? 4 * (R * nx + cm_state(cl)) : kOOB);
           if (a.f) bst(h, rf, (i < nu && cl == 15) ? 4 * R : kOOB);
         }
       }
