@@ -672,7 +672,7 @@ __device__ __forceinline__ int cm_state(int pos) {
   const int g = pos >> 2, s = pos & 3;
   return s < 3 ? 3 * g + s : (g < 3 ? 12 + g : 15);
 }
-template <int NT, int NU4, bool DRIFT>
+template <int NT, int NU4, bool DRIFT, bool P12>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 void condense_mfma_kernel(CondenseArgs<float> a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -847,7 +847,7 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
     MPCQP_PHASE(1);
     // all MFMA chains first (independent tiles overlap in the matrix pipe),
     // then the VALU epilogue per tile
-    if (nx <= 12) {  // K chunk 3 of Gamma~ is empty (cm_state)
+    if constexpr (P12) {  // nx <= 12: K chunk 3 of Gamma~ is empty (cm_state)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         if (t < ntact) {
@@ -886,10 +886,10 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
         float(&d)[4] = gB[t];  // Gamma~_{r+1} tile, C layout
         const bool inblk = col >= blk0 && col < blk0 + nu;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) d[j] = inblk ? bI[j] : d[j];
+        for (int j = 0; j < (P12 ? 3 : 4); ++j) d[j] = inblk ? bI[j] : d[j];
         if (a.Gam) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < (P12 ? 3 : 4); ++j) {
             const int sp = cm_state(4 * g + j);
             bst(d[j], rG, (sp < nx && col < n) ? 4 * ((r * nx + sp) * n + col) : kOOB);
           }
@@ -901,7 +901,7 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
           for (int i = 0; i < 4; ++i) {
             float acc = 0.f;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc = fmaf(wv[4 * ic + i][j], d[j], acc);
+            for (int j = 0; j < (P12 ? 3 : 4); ++j) acc = fmaf(wv[4 * ic + i][j], d[j], acc);
             P[i] = acc;
           }
           xpose4(P);
@@ -964,17 +964,22 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
 #endif
 }
 
-template <int NT, int NU4, bool DRIFT>
-static int launch_condense_mfma3(const CondenseArgs<float>& a, hipStream_t st) {
+template <int NT, int NU4, bool DRIFT, bool P12>
+static int launch_condense_mfma4(const CondenseArgs<float>& a, hipStream_t st) {
   const size_t bytes = ((size_t)a.N * NU4 * 16 + (size_t)a.nu * a.nu) * sizeof(float);
   if (bytes > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)condense_mfma_kernel<NT, NU4, DRIFT>,
+    hipError_t e = hipFuncSetAttribute((const void*)condense_mfma_kernel<NT, NU4, DRIFT, P12>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(condense_mfma)");
   }
-  hipLaunchKernelGGL((condense_mfma_kernel<NT, NU4, DRIFT>), dim3(a.batch), dim3(kWave), bytes, st, a);
+  hipLaunchKernelGGL((condense_mfma_kernel<NT, NU4, DRIFT, P12>), dim3(a.batch), dim3(kWave), bytes, st, a);
   MPCQP_CHECK_LAUNCH("condense_mfma_kernel");
   return MPCQP_OK;
+}
+template <int NT, int NU4, bool DRIFT>
+static int launch_condense_mfma3(const CondenseArgs<float>& a, hipStream_t st) {
+  return a.nx <= 12 ? launch_condense_mfma4<NT, NU4, DRIFT, true>(a, st)
+                    : launch_condense_mfma4<NT, NU4, DRIFT, false>(a, st);
 }
 template <int NT, int NU4>
 static int launch_condense_mfma(const CondenseArgs<float>& a, hipStream_t st) {
