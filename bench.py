@@ -68,16 +68,31 @@ METRIC = "QP solves/sec (batch, horizon N=20) at 1/2/4/8 MI355X; max|u-u_ref|"
 
 
 # ------------------------------------------------------------- algorithmic counts
+def condense_bytes_survey(nx, nu, N, es, state_box):
+    """SURVEY.md 8(d) algorithmic bytes of condensing one instance, the count
+    roofline.achieved uses: in A_k, B_k per stage + x0; out the packed upper
+    triangle of H, F (n x nx), and -- only with state constraints -- Gamma's
+    lower block triangle (nx nu N(N+1)/2) and Phi (N nx x nx).  Config 3:
+    6,994 elements = 27,976 B; config 5: 22,492 = 89,968 B."""
+    n, m = N * nu, N * nx
+    inp = N * (nx * nx + nx * nu) + nx
+    out = n * (n + 1) // 2 + n * nx
+    if state_box:
+        out += nx * nu * N * (N + 1) // 2 + m * nx
+    return (inp + out) * es
+
+
 def condense_bytes_per_instance(nx, nu, N, es=8, tv=False, gam=False, xbar=False,
-                                F=False, f=True):
-    """HBM bytes of mpcqp_condense per instance (SURVEY.md 8(d) formula):
-    inputs A, B (per stage when TV), x0; outputs packed H, f and whatever
-    else the workload asks for (Gam, xbar, F)."""
+                                F=False, f=True, drift=False):
+    """HBM bytes mpcqp_condense actually moves per instance (reported beside
+    the 8(d) count): inputs A, B (per stage when TV), c (drift), x0; outputs
+    packed H, f and whatever else the workload asks for -- Gam as its lower
+    block triangle (MPCQP_GAM_PACKED), xbar, F."""
     n, m = N * nu, N * nx
     S = N if tv else 1
-    inp = S * (nx * nx + nx * nu) + nx + (S * nx if tv else 0)
-    out = n * (n + 1) // 2 + (n if f else 0) + (m * n if gam else 0) + (m if xbar else 0) \
-        + (n * nx if F else 0)
+    inp = S * (nx * nx + nx * nu) + nx + (N * nx if drift else 0)
+    out = n * (n + 1) // 2 + (n if f else 0) + (nx * nu * N * (N + 1) // 2 if gam else 0) \
+        + (m if xbar else 0) + (n * nx if F else 0)
     return (inp + out) * es
 
 
@@ -466,15 +481,19 @@ class Config3:
         t_s = time_kernel(lambda: self.step(0), R, self.dev)
         st = mpc_qp_stage_ms(lambda: self.step(0), R)
         t_c, t_w, t_z = st["condense"], st["sweep"], st["solve"]
-        # condense writes packed H, f and Gamma (the row normals); no xbar
-        cb = condense_bytes_per_instance(nx, nu, N, 4, tv=True, gam=True, xbar=False) * bsz
+        # achieved: SURVEY 8(d)'s bytes (H upper, F, Gamma's lower block
+        # triangle, Phi; A_k, B_k, x0 in).  The kernel itself reads c_k too and
+        # writes packed H, f and the packed Gamma (the row normals; no F, Phi)
+        cb = condense_bytes_survey(nx, nu, N, 4, True) * bsz
+        cm = condense_bytes_per_instance(nx, nu, N, 4, tv=True, gam=True, drift=True) * bsz
         wf = sweep_flops_per_instance(n, 0) * bsz
         # the z-space kernel reads H^-1 (n x n), s0, f, Gamma (m x n: every
         # row is checked once at the end), the dynamics (A_k, B_k, c_k, x0)
         # of the refinement, the shared bounds once; writes z, y, status
         zb = (n * n + 2 * n + m * n + N * (nx * nx + nx * nu + nx) + nx + n + m + 1) * 4 * bsz
         r_c = roof("condense_kernel<float,4>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
-                   traffic.get("condense"), {"bytes_per_launch": cb})
+                   traffic.get("condense"), {"bytes_per_launch": cb, "bytes_moved_per_launch": cm,
+                                             "bytes": "SURVEY 8(d)"})
         r_w = roof("sweep_mfma_kernel<4> (H^-1)", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
                    traffic.get("sweep"), {"flops_per_launch": wf})
         r_z = roof("qp_zf_kernel<4> (DYN refinement)", "hbm", zb, t_z, HBM_PEAK_GBS, "GB/s",
@@ -680,14 +699,15 @@ class Config5:
         t_s = time_kernel(lambda: self.step(0), R, self.dev)
         st = mpc_qp_stage_ms(lambda: self.step(0), R)
         t_c, t_w, t_p = st["condense"], st["sweep"], st["solve"]
-        fl = condense_flops_per_instance(nx, nu, N) * bsz
-        cb = condense_bytes_per_instance(nx, nu, N, 4, tv=True) * bsz
-        # the survey's condensing flop formula counts the explicit Gam'QGam
-        # product; the augmented-state recursion does ~1/3 of that work, so the
-        # formula rate exceeds the fp32 MFMA peak: report the byte roof instead
+        # achieved: SURVEY 8(d)'s bytes (A_k, B_k, x0 in; H upper + F out);
+        # the kernel writes f instead of F.  (8(d)'s flop formula counts the
+        # explicit Gam'QGam product, which the recursion never forms: it is
+        # not a rate of this kernel and is not reported as one)
+        cb = condense_bytes_survey(nx, nu, N, 4, False) * bsz
+        cm = condense_bytes_per_instance(nx, nu, N, 4, tv=True) * bsz
         r_c = roof("condense_mfma_kernel<10,4>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
-                   traffic.get("condense"), {"bytes_per_launch": cb, "formula_flops_per_launch": fl,
-                                             "formula_TFLOPs": round(fl / (t_c * 1e-3) / 1e12, 1)})
+                   traffic.get("condense"), {"bytes_per_launch": cb, "bytes_moved_per_launch": cm,
+                                             "bytes": "SURVEY 8(d)"})
         wf = sweep_flops_per_instance(n) * bsz
         r_w = roof("sweep_mfma_kernel<10>", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
                    traffic.get("sweep"), {"flops_per_launch": wf})

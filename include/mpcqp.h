@@ -84,6 +84,13 @@ extern "C" {
    Riccati pivots the solve ends with MPCQP_STATUS_NOT_CONVEX instead of
    regularising further (an SQP caller raises its own damping and retries) */
 #define MPCQP_STRICT 4
+/* mpcqp_condense: Gam is written as its lower block triangle only, block row
+   k (rows k*nx .. k*nx+nx-1, the state x_{k+1}) holding its (k+1)*nu leading
+   columns from element offset nx*nu*k*(k+1)/2, column by column: entry
+   (k*nx + q, col) at nx*nu*k*(k+1)/2 + col*nx + q -- nx*nu*N*(N+1)/2
+   elements per instance instead of N*nx*N*nu (the upper block triangle is
+   structurally zero; SURVEY 8(d) counts only this part) */
+#define MPCQP_GAM_PACKED 8
 
 /* status bit 24: the solution was polished to the exact active-set vertex */
 #define MPCQP_STATUS_POLISHED (1 << 24)
@@ -112,7 +119,8 @@ int mpcqp_max_box_n(int dtype);
  *   R nu*nu, Qf nx*nx, c (optional, N*nx), x0 (optional, nx).
  * Outputs (NULL to skip; per-instance, densely packed):
  *   H (required), F, f (uses x0 and c; x0 = NULL means x0 = 0),
- *   Gam (N*nx x n), Phi (N*nx x nx), xbar (N*nx).
+ *   Gam (N*nx x n; with MPCQP_GAM_PACKED its lower block triangle,
+ *   nx*nu*N*(N+1)/2), Phi (N*nx x nx), xbar (N*nx).
  * Limits: 1 <= nx <= 16, 1 <= nu <= 16, N >= 1.
  */
 int mpcqp_condense(int dtype, int batch, int nx, int nu, int N, int flags,

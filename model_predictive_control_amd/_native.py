@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("MPCQP_LIB", os.path.join(_HERE, "lib", "libmpcqp.so")
 F64 = 0
 F32 = 1
 TV = 1
+GAM_PACKED = 8  # mpcqp_condense: Gam as its lower block triangle
 IPM = 2
 STRICT = 4
 STATUS_POLISHED = 1 << 24

@@ -146,13 +146,15 @@ def unpack_lower(P: torch.Tensor, n: int) -> torch.Tensor:
 
 # ---------------------------------------------------------------- condense
 def condense(A, B, Q, R, Qf, N: int, x0=None, c=None, *, tv: bool = False,
-             outputs=("H", "f"), out: dict | None = None) -> dict:
+             outputs=("H", "f"), out: dict | None = None, gam_packed: bool = False) -> dict:
     """Batched condensing (include/mpcqp.h ``mpcqp_condense``).
 
     A: (nx,nx) | (b,nx,nx) | with ``tv``: (N,nx,nx) | (b,N,nx,nx); B likewise
     with nu columns; Q/Qf (nx,nx) | (b,nx,nx); R (nu,nu) | (b,nu,nu);
     x0 (nx,) | (b,nx); c (N,nx) | (b,N,nx).  Returns a dict with the requested
-    ``outputs`` among H (packed), F, f, Gam, Phi, xbar.
+    ``outputs`` among H (packed), F, f, Gam, Phi, xbar.  ``gam_packed``: Gam
+    as its lower block triangle, (b, nx*nu*N*(N+1)/2) (``MPCQP_GAM_PACKED``;
+    ``unpack_gam`` restores the dense (b, N*nx, N*nu) form).
     """
     dt = A.dtype if isinstance(A, torch.Tensor) else torch.float64
     dev = A.device if isinstance(A, torch.Tensor) else torch.device("cuda")
@@ -173,17 +175,29 @@ def condense(A, B, Q, R, Qf, N: int, x0=None, c=None, *, tv: bool = False,
     want = set(outputs) | {"H"}
     out = dict(out or {})
     shapes = {"H": (batch, n * (n + 1) // 2), "F": (batch, n, nx), "f": (batch, n),
-              "Gam": (batch, N * nx, n), "Phi": (batch, N * nx, nx), "xbar": (batch, N * nx)}
+              "Gam": (batch, nx * nu * N * (N + 1) // 2) if gam_packed else (batch, N * nx, n), "Phi": (batch, N * nx, nx), "xbar": (batch, N * nx)}
     for k in want:
         if k not in out:
             out[k] = torch.empty(shapes[k], dtype=dt, device=dev)
     rc = _lib().mpcqp_condense(
-        _code(dt), batch, nx, nu, N, nat.TV if tv else 0,
+        _code(dt), batch, nx, nu, N, (nat.TV if tv else 0) | (nat.GAM_PACKED if gam_packed else 0),
         _ptr(A), sA, _ptr(B), sB, _ptr(Q), sQ, _ptr(R), sR, _ptr(Qf), sQf, _ptr(c), sC,
         _ptr(x0), sX, _ptr(out.get("H")), _ptr(out.get("F")), _ptr(out.get("f")),
         _ptr(out.get("Gam")), _ptr(out.get("Phi")), _ptr(out.get("xbar")), _stream())
     nat.check(rc, "mpcqp_condense")
     return {k: out[k] for k in want}
+
+
+def unpack_gam(P, N: int, nx: int, nu: int):
+    """Dense (..., N*nx, N*nu) Gamma from its packed lower block triangle
+    (``condense(..., gam_packed=True)``): block row k holds its (k+1)*nu
+    leading columns from offset nx*nu*k*(k+1)/2, column by column (entry
+    (k*nx + q, col) at nx*nu*k*(k+1)/2 + col*nx + q)."""
+    out = P.new_zeros(P.shape[:-1] + (N * nx, N * nu))
+    for k in range(N):
+        o, w = nx * nu * k * (k + 1) // 2, (k + 1) * nu
+        out[..., k * nx:(k + 1) * nx, :w] = P[..., o:o + nx * w].reshape(P.shape[:-1] + (w, nx)).transpose(-1, -2)
+    return out
 
 
 # ---------------------------------------------------- fused condense + box
@@ -751,6 +765,22 @@ def bicycle_hessian(X, U, pi, params, ts: float, flags=None, mu=None,
     return H2, q2
 
 
+def _bound_pair(lo, hi, b: int, width: int, what: str):
+    """A lower/upper bound pair that the C call reads with ONE instance stride:
+    each side None, (width,) shared or (b, width).  A shared side next to a
+    per-instance one is broadcast to (b, width), so the shared stride is never
+    applied to a per-instance buffer or the reverse (which would read past
+    the shared side's end).  Returns (lo, hi, stride)."""
+    sides = [v for v in (lo, hi) if v is not None]
+    for v in sides:
+        if tuple(v.shape) not in ((width,), (b, width)):
+            raise ValueError(f"{what}: shape {tuple(v.shape)} is neither ({width},) nor ({b}, {width})")
+    if not any(v.ndim == 2 for v in sides):
+        return lo, hi, 0
+    ex = lambda v: None if v is None else v.expand(b, width).contiguous()  # noqa: E731
+    return ex(lo), ex(hi), width
+
+
 def bicycle_sqp_step(x0, U, Z, yq, piq, y, pi, X, state: dict, params, ts: float, Q, R, Qf,
                      xlo=None, xhi=None, lb=None, ub=None, tol: float = 1e-9, qp_status=None,
                      integrator: int = 0):
@@ -760,12 +790,8 @@ def bicycle_sqp_step(x0, U, Z, yq, piq, y, pi, X, state: dict, params, ts: float
     the inputs to hold at their bound in the next exact-Hessian QP).  Bounds: xlo/xhi (N*4,)
     shared or (b, N*4); lb/ub (N*2,) shared or (b, N*2)."""
     b, N = int(U.shape[0]), int(U.shape[1])
-    sxb = 0 if xlo is None or xlo.ndim == 1 else 4 * N
-    if xhi is not None and xhi.ndim == 2:
-        sxb = 4 * N
-    slb = 0 if lb is None or lb.ndim == 1 else 2 * N
-    if ub is not None and ub.ndim == 2:
-        slb = 2 * N
+    xlo, xhi, sxb = _bound_pair(xlo, xhi, b, 4 * N, "xlo/xhi")
+    lb, ub, slb = _bound_pair(lb, ub, b, 2 * N, "lb/ub")
     rc = _lib().mpcqp_bicycle_sqp_step(
         nat.F64, b, N, float(ts), _bike_params(params), int(integrator), _ptr(x0), 4, _ptr(Q),
         _ptr(R), _ptr(Qf),

@@ -143,8 +143,10 @@ class ClosedLoop:
             s["xs"][0].copy_(X0)
             for t in range(T):
                 self._step(s, t)
-        return {k: s[k] for k in ("xs", "us", "success", "iters", "state_prediction",
-                                  "input_prediction")}
+        keys = ("xs", "us", "success", "iters", "state_prediction", "input_prediction")
+        # graph mode replays into buffers cached per (b, T): hand out copies, so a
+        # later run() of the same shape cannot overwrite results the caller holds
+        return {k: s[k].clone() if self.graph else s[k] for k in keys}
 
     def _reset(self, s):
         s["sqp"].reset()

@@ -58,6 +58,26 @@ struct PhaseClock {
 
 constexpr int kWave = 64;  // CDNA wavefront width (hard-coded, never warpSize)
 
+// LDS exchange inside the single-wave workgroup: a wave's LDS operations
+// execute in issue order, so only the compiler must not move them (no
+// s_barrier, and no fence that would drain the outstanding global loads)
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Gamma as its lower block triangle (MPCQP_GAM_PACKED): block row k (the
+// state x_{k+1}, nx rows) keeps its (k+1) nu leading columns, column by
+// column, from element nx nu k (k+1) / 2 -- entry (k nx + q, col) at
+// gam_packed_off(k) + col nx + q, so the nx entries one lane of the
+// condensing sweep holds for its column are one contiguous vector
+__host__ __device__ __forceinline__ int gam_packed_off(int nx, int nu, int k) {
+  return nx * nu * (k * (k + 1) / 2);
+}
+__host__ __device__ __forceinline__ int64_t gam_packed_size(int nx, int nu, int N) {
+  return (int64_t)nx * nu * ((int64_t)N * (N + 1) / 2);
+}
+
 // ---------------------------------------------------------------- errors
 void set_error(const char* fmt, ...);
 int hip_fail(hipError_t e, const char* where);

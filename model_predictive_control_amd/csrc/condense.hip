@@ -48,6 +48,7 @@ struct CondenseArgs {
   const T* x0; int64_t sX0;
   T* H; T* F; T* f; T* Gam; T* Phi; T* xbar;
   int rh, rg;  // output rings (elements, powers of two) of the streamed sweep; rh = 0: direct stores
+  int gpk = 0;     // Gam as its lower block triangle (MPCQP_GAM_PACKED)
   const int* count = nullptr;  // device count: instances b >= *count are skipped (list mode)
 };
 
@@ -103,6 +104,111 @@ __device__ __forceinline__ int qdiv(int e, int d, float rd) {
   return s;
 }
 
+// Stage-in of one instance into LDS.  A, B, c of one instance are dense runs
+// in HBM.  All loads of a chunk (UA + UB + UC per lane, clamped addresses, no
+// branches) are issued before its LDS stores, so a chunk costs one HBM round
+// trip; config 3 (N = 30, nx = 4) is one chunk.  Padding (nx < NX) is zeroed
+// first and the data scattered over it (LDS ops of one wave complete in order).
+template <typename T, int NX>
+__device__ __forceinline__ void stage_in(const CondenseArgs<T>& a, int b, int lane, bool need_aff,
+                                         T* As, T* Bs, T* Cs, T* Qs, T* Qfs, T* Rs, T* X0s) {
+  const int nx = a.nx, nu = a.nu, N = a.N;
+  const int S = a.tv ? N : 1;
+  const T* Ab = a.A + (int64_t)b * a.sA;
+  const T* Bb = a.B + (int64_t)b * a.sB;
+  const T* Cb = (need_aff && a.c) ? a.c + (int64_t)b * a.sC : nullptr;
+  const T* Qb = a.Q + (int64_t)b * a.sQ;
+  const T* Qfb = a.Qf + (int64_t)b * a.sQf;
+  const T* Rb = a.R + (int64_t)b * a.sR;
+  const T* X0b = (need_aff && a.x0) ? a.x0 + (int64_t)b * a.sX0 : nullptr;
+  const int cA = S * nx * nx, cB = S * nx * nu, cC = Cb ? N * nx : 0, cR = nu * nu;
+  // small operands: Q, Qf (QK padded entries per lane), R (<= 4 per lane), x0
+  constexpr int QK = (NX * NX + kWave - 1) / kWave;
+  T qv[QK], qfv[QK];
+  bool qin[QK];
+#pragma unroll
+  for (int k = 0; k < QK; ++k) {
+    const int e = k * kWave + lane, qr = e / NX, qq = e % NX;
+    qin[k] = e < NX * NX && qr < nx && qq < nx;
+    const int qo = qin[k] ? qr * nx + qq : 0;
+    qv[k] = Qb[qo];
+    qfv[k] = Qfb[qo];
+  }
+  T rv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = k * kWave + lane;
+    rv[k] = Rb[e < cR ? e : 0];
+  }
+  const T x0v = X0b ? X0b[lane < nx ? lane : 0] : T(0);
+  const bool pad = nx < NX;
+  if (pad) {
+    for (int e = lane; e < S * NX * NX; e += kWave) As[e] = T(0);
+    for (int e = lane; e < S * NX * nu; e += kWave) Bs[e] = T(0);
+  }
+  if (need_aff && (pad || !Cb))
+    for (int e = lane; e < N * NX; e += kWave) Cs[e] = T(0);
+  const float rA = 1.f / (float)(nx * nx), rB = 1.f / (float)(nx * nu), rN = 1.f / (float)nx;
+  constexpr int UA = 8, UB = 4, UC = 2;
+  auto chunk = [&](int c) {
+    T va[UA], vb[UB], vc[UC];
+#pragma unroll
+    for (int k = 0; k < UA; ++k) {
+      const int e = (c * UA + k) * kWave + lane;
+      va[k] = Ab[e < cA ? e : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < UB; ++k) {
+      const int e = (c * UB + k) * kWave + lane;
+      vb[k] = Bb[e < cB ? e : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < UC; ++k) {
+      const int e = (c * UC + k) * kWave + lane;
+      vc[k] = (e < cC) ? Cb[e] : T(0);
+    }
+#pragma unroll
+    for (int k = 0; k < UA; ++k) {
+      const int e = (c * UA + k) * kWave + lane;
+      if (e < cA) {
+        int o = e;
+        if (pad) {
+          const int s = qdiv(e, nx * nx, rA), rem = e - s * nx * nx;
+          const int r = qdiv(rem, nx, rN);
+          o = s * NX * NX + r * NX + (rem - r * nx);
+        }
+        As[o] = va[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UB; ++k) {
+      const int e = (c * UB + k) * kWave + lane;
+      if (e < cB) Bs[pad ? e + qdiv(e, nx * nu, rB) * (NX - nx) * nu : e] = vb[k];
+    }
+#pragma unroll
+    for (int k = 0; k < UC; ++k) {
+      const int e = (c * UC + k) * kWave + lane;
+      if (e < cC) Cs[pad ? e + qdiv(e, nx, rN) * (NX - nx) : e] = vc[k];
+    }
+  };
+  // chunk 0 outside the loop: its loads share the round trip of the small
+  // operands above (a loop header would wait for those first)
+  chunk(0);
+  for (int c = 1; c * kWave * UA < cA || c * kWave * UB < cB || c * kWave * UC < cC; ++c) chunk(c);
+#pragma unroll
+  for (int k = 0; k < QK; ++k) {
+    const int e = k * kWave + lane;
+    if (e < NX * NX) {
+      Qs[e] = qin[k] ? qv[k] : T(0);
+      Qfs[e] = qin[k] ? qfv[k] : T(0);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (k * kWave + lane < cR) Rs[k * kWave + lane] = rv[k];
+  if (need_aff && lane < NX) X0s[lane] = lane < nx ? x0v : T(0);
+}
+
 template <typename T, int NX>
 __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -130,107 +236,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   PhaseClock mpcqp_clk;
 #endif
 
-  // ---------------------------------------------------------------- stage in
-  // A, B, c of one instance are dense runs in HBM.  All loads of a chunk
-  // (UA + UB + UC per lane, clamped addresses, no branches) are issued before
-  // its LDS stores, so a chunk costs one HBM round trip; config 3 (N = 30,
-  // nx = 4) is one chunk.  Padding (nx < NX) is zeroed first and the data
-  // scattered over it (LDS ops of one wave complete in order).
-  {
-    const T* Ab = a.A + (int64_t)b * a.sA;
-    const T* Bb = a.B + (int64_t)b * a.sB;
-    const T* Cb = (need_aff && a.c) ? a.c + (int64_t)b * a.sC : nullptr;
-    const T* Qb = a.Q + (int64_t)b * a.sQ;
-    const T* Qfb = a.Qf + (int64_t)b * a.sQf;
-    const T* Rb = a.R + (int64_t)b * a.sR;
-    const T* X0b = (need_aff && a.x0) ? a.x0 + (int64_t)b * a.sX0 : nullptr;
-    const int cA = S * nx * nx, cB = S * nx * nu, cC = Cb ? N * nx : 0, cR = nu * nu;
-    // small operands: Q, Qf (QK padded entries per lane), R (<= 4 per lane), x0
-    constexpr int QK = (NX * NX + kWave - 1) / kWave;
-    T qv[QK], qfv[QK];
-    bool qin[QK];
-#pragma unroll
-    for (int k = 0; k < QK; ++k) {
-      const int e = k * kWave + lane, qr = e / NX, qq = e % NX;
-      qin[k] = e < NX * NX && qr < nx && qq < nx;
-      const int qo = qin[k] ? qr * nx + qq : 0;
-      qv[k] = Qb[qo];
-      qfv[k] = Qfb[qo];
-    }
-    T rv[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = k * kWave + lane;
-      rv[k] = Rb[e < cR ? e : 0];
-    }
-    const T x0v = X0b ? X0b[lane < nx ? lane : 0] : T(0);
-    const bool pad = nx < NX;
-    if (pad) {
-      for (int e = lane; e < S * NX * NX; e += kWave) As[e] = T(0);
-      for (int e = lane; e < S * NX * nu; e += kWave) Bs[e] = T(0);
-    }
-    if (need_aff && (pad || !Cb))
-      for (int e = lane; e < N * NX; e += kWave) Cs[e] = T(0);
-    const float rA = 1.f / (float)(nx * nx), rB = 1.f / (float)(nx * nu), rN = 1.f / (float)nx;
-    constexpr int UA = 8, UB = 4, UC = 2;
-    auto chunk = [&](int c) {
-      T va[UA], vb[UB], vc[UC];
-#pragma unroll
-      for (int k = 0; k < UA; ++k) {
-        const int e = (c * UA + k) * kWave + lane;
-        va[k] = Ab[e < cA ? e : 0];
-      }
-#pragma unroll
-      for (int k = 0; k < UB; ++k) {
-        const int e = (c * UB + k) * kWave + lane;
-        vb[k] = Bb[e < cB ? e : 0];
-      }
-#pragma unroll
-      for (int k = 0; k < UC; ++k) {
-        const int e = (c * UC + k) * kWave + lane;
-        vc[k] = (e < cC) ? Cb[e] : T(0);
-      }
-#pragma unroll
-      for (int k = 0; k < UA; ++k) {
-        const int e = (c * UA + k) * kWave + lane;
-        if (e < cA) {
-          int o = e;
-          if (pad) {
-            const int s = qdiv(e, nx * nx, rA), rem = e - s * nx * nx;
-            const int r = qdiv(rem, nx, rN);
-            o = s * NX * NX + r * NX + (rem - r * nx);
-          }
-          As[o] = va[k];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < UB; ++k) {
-        const int e = (c * UB + k) * kWave + lane;
-        if (e < cB) Bs[pad ? e + qdiv(e, nx * nu, rB) * (NX - nx) * nu : e] = vb[k];
-      }
-#pragma unroll
-      for (int k = 0; k < UC; ++k) {
-        const int e = (c * UC + k) * kWave + lane;
-        if (e < cC) Cs[pad ? e + qdiv(e, nx, rN) * (NX - nx) : e] = vc[k];
-      }
-    };
-    // chunk 0 outside the loop: its loads share the round trip of the small
-    // operands above (a loop header would wait for those first)
-    chunk(0);
-    for (int c = 1; c * kWave * UA < cA || c * kWave * UB < cB || c * kWave * UC < cC; ++c) chunk(c);
-#pragma unroll
-    for (int k = 0; k < QK; ++k) {
-      const int e = k * kWave + lane;
-      if (e < NX * NX) {
-        Qs[e] = qin[k] ? qv[k] : T(0);
-        Qfs[e] = qin[k] ? qfv[k] : T(0);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (k * kWave + lane < cR) Rs[k * kWave + lane] = rv[k];
-    if (need_aff && lane < NX) X0s[lane] = lane < nx ? x0v : T(0);
-  }
+  stage_in<T, NX>(a, b, lane, need_aff, As, Bs, Cs, Qs, Qfs, Rs, X0s);
   __syncthreads();
   MPCQP_PHASE(0);
 
@@ -414,7 +420,11 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   const int ncol = n + ((a.F || a.Phi) ? nx : 0);
   T* Hb = a.H + (int64_t)b * ((int64_t)n * (n + 1) / 2);
   T* Fb = a.F ? a.F + (int64_t)b * n * nx : nullptr;
-  T* Gb = a.Gam ? a.Gam + (int64_t)b * ((int64_t)N * nx * n) : nullptr;
+  // packed Gam: block row i (x_{i+1}) holds its (i+1) nu leading columns,
+  // column by column (nx entries each), from nx nu i (i+1) / 2
+  // (gam_packed_size / gam_packed_off)
+  const int64_t gsz = a.gpk ? gam_packed_size(nx, nu, N) : (int64_t)N * nx * n;
+  T* Gb = a.Gam ? a.Gam + (int64_t)b * gsz : nullptr;
   T* Pb = a.Phi ? a.Phi + (int64_t)b * ((int64_t)N * nx * nx) : nullptr;
   if (a.rh) {
     // Streamed sweep (ncol <= 64, one column per lane).  H row block i is
@@ -459,7 +469,7 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
     const int dg = Gb ? (int)(((uintptr_t)Gb / sizeof(T)) % VEC) : 0;
     T* Hal = Hb - dh;
     T* Gal = Gb ? Gb - dg : nullptr;
-    const int hiH = dh + n * (n + 1) / 2, hiG = dg + N * nx * n;
+    const int hiH = dh + n * (n + 1) / 2, hiG = dg + (int)gsz;
     auto flush = [&](const T* ring, int rmask, T* gal, int w, int lo, int hi) {
       const int p0 = w + lane * VEC;
       if (p0 < hi && p0 + VEC > lo) {
@@ -492,9 +502,17 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
 #pragma unroll
       for (int q = 0; q < NX; ++q) s[q] = inj ? bcol[q] : t[q];
       if (Gb && isz) {
+        if (a.gpk) {
+          const int o = dg + gam_packed_off(nx, nu, i) + col * nx;
+          if (col < (i + 1) * nu)
 #pragma unroll
-        for (int q = 0; q < NX; ++q)
-          if (q < nx) RG[(dg + (i * nx + q) * n + col) & RGM] = s[q];
+            for (int q = 0; q < NX; ++q)
+              if (q < nx) RG[(o + q) & RGM] = s[q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < NX; ++q)
+            if (q < nx) RG[(dg + (i * nx + q) * n + col) & RGM] = s[q];
+        }
       }
       if (act && !isz && Pb) {
 #pragma unroll
@@ -513,7 +531,8 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
         }
       }
       const int rr = (i + 1) * nu;
-      const int ph = dh + rr * (rr + 1) / 2, pg = Gb ? dg + (i + 1) * nx * n : 0;
+      const int ph = dh + rr * (rr + 1) / 2,
+                pg = Gb ? dg + (a.gpk ? gam_packed_off(nx, nu, i + 1) : (i + 1) * nx * n) : 0;
       if (ph - fh >= CH || pg - fg >= CH) {
         __syncthreads();
         for (; ph - fh >= CH; fh += CH) flush(RH, RHM, Hal, fh, dh, hiH);
@@ -557,9 +576,16 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
       }
       if (act) {
         if (isz && Gb) {
+          if (a.gpk) {
+            if (col < (i + 1) * nu)
 #pragma unroll
-          for (int q = 0; q < NX; ++q)
-            if (q < nx) __builtin_nontemporal_store(s[q], &Gb[((int64_t)(i * nx + q)) * n + col]);
+              for (int q = 0; q < NX; ++q)
+                if (q < nx) __builtin_nontemporal_store(s[q], &Gb[gam_packed_off(nx, nu, i) + col * nx + q]);
+          } else {
+#pragma unroll
+            for (int q = 0; q < NX; ++q)
+              if (q < nx) __builtin_nontemporal_store(s[q], &Gb[((int64_t)(i * nx + q)) * n + col]);
+          }
         }
         if (!isz && Pb) {
 #pragma unroll
@@ -597,8 +623,352 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
 #endif
 }
 
+// ================================================================ streamed kernel
+// condense_stream_kernel<T, NX, NU>: the wavefront kernel's streamed sweep
+// (one column per lane, every column <= 64) with the affine part carried by
+// a spare lane instead of the free-response and adjoint chains, and ONE LDS
+// round trip per backward stage.  With the affine cost-to-go
+//     y_k = W_k xbar_k + eta_k,  eta_N = 0,
+//     eta_k = A_k' (W_{k+1} c_k + eta_{k+1})
+// (y_k = Q xbar_k + A_k' y_{k+1} by induction), the linear term is
+//     f_(i,a) = B_i[:,a]' y_{i+1} = What_i[a,:] xbar_{i+1} + ghat_i[a],
+//     ghat_i = B_i' eta_{i+1},
+// i.e. the H-row formula of one more column whose vector is xbar itself
+// (s = A_i s + c_i from s = x0): the lane after the last column computes f
+// and xbar inside the forward sweep.  Every backward quantity of stage k is a
+// function of stage k+1's only,
+//     out = base + sum_p L[p] (sum_s W_{k+1}[p][s] y[s] + e1 eta_{k+1}[p])
+//   W_k(r,q):   L = A_k[:,r], y = A_k[:,q], base = Q[r][q]
+//   eta_k(r):   L = A_k[:,r], y = c_k,      e1 = 1
+//   What_k(a,q): L = B_k[:,a], y = e_q
+//   ghat_k(a):  L = B_k[:,a], y = 0,        e1 = 1
+// so each stage is one phase: every lane evaluates the same expression for
+// its item (no divergence), W and eta double-buffered in LDS.
+// Gamma is written packed (MPCQP_GAM_PACKED, block column by column): a
+// lane's nx entries of its column are one contiguous vector, one 16-byte
+// store per lane and stage (no ring).  H keeps the ring of packed rows,
+// flushed in half-wave windows (a 256-element ring at config 3).
+struct SLayout {
+  int oA, oC, oWh, oGh, oR, oX0, oFo, oXo, oB, oQ, oQf, oW, oE, oI, oZ, oRH, total;
+};
+__host__ __device__ inline SLayout slayout(int NX, int nu, int N, int tv, int rh, int fo, int xo) {
+  SLayout L;
+  const int S = tv ? N : 1;
+  auto al4 = [](int o) { return (o + 3) & ~3; };
+  int o = 0;
+  L.oA = o; o = al4(o + S * NX * NX);
+  L.oC = o; o = al4(o + N * NX);
+  L.oWh = o; o = al4(o + N * nu * NX);
+  L.oGh = o; o = al4(o + N * nu);
+  L.oR = o; o = al4(o + nu * nu);
+  L.oX0 = o; o = al4(o + NX);
+  L.oFo = o; o = al4(o + (fo ? N * nu : 0));
+  L.oXo = o; o = al4(o + (xo ? N * NX : 0));
+  // dead once the backward pass is done: the H ring overlays them
+  int u = o;
+  L.oB = u; u = al4(u + S * NX * nu);
+  L.oQ = u; u = al4(u + NX * NX);
+  L.oQf = u; u = al4(u + NX * NX);
+  L.oW = u; u = al4(u + 2 * NX * NX);
+  L.oE = u; u = al4(u + 2 * NX);
+  L.oI = u; u = al4(u + NX * NX);
+  L.oZ = u; u = al4(u + NX);
+  L.oRH = o;
+  L.total = u > o + rh ? u : o + rh;
+  return L;
+}
+
+template <typename T, int NX, int NU>
+__global__ __launch_bounds__(64) void condense_stream_kernel(CondenseArgs<T> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  T* sm = reinterpret_cast<T*>(smem_raw);
+  const int b = blockIdx.x;
+  if (a.count && b >= *a.count) return;  // uniform per workgroup
+  const int lane = threadIdx.x;
+  const int nx = a.nx, N = a.N, n = N * NU;
+  const int tv = a.tv;
+  const bool want_x0 = a.F || a.Phi;
+  const bool want_aff = a.f || a.xbar;
+  const SLayout L = slayout(NX, NU, N, tv, a.rh, a.f ? 1 : 0, a.xbar ? 1 : 0);
+  T* As = sm + L.oA;
+  T* Cs = sm + L.oC;
+  T* Whs = sm + L.oWh;
+  T* Ghs = sm + L.oGh;
+  T* Rs = sm + L.oR;
+  T* X0s = sm + L.oX0;
+  T* Fo = sm + L.oFo;
+  T* Xo = sm + L.oXo;
+  T* Bs = sm + L.oB;
+  T* Qs = sm + L.oQ;
+  T* Qfs = sm + L.oQf;
+  T* Ws = sm + L.oW;
+  T* Es = sm + L.oE;
+  T* Is = sm + L.oI;
+  T* Zs = sm + L.oZ;
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
+  stage_in<T, NX>(a, b, lane, want_aff, As, Bs, Cs, Qs, Qfs, Rs, X0s);
+  const int pN = N & 1;
+  for (int e = lane; e < NX * NX; e += kWave) {
+    Ws[pN * NX * NX + e] = Qfs[e];
+    Is[e] = (e / NX == e % NX) ? T(1) : T(0);
+  }
+  if (lane < NX) {
+    Es[pN * NX + lane] = T(0);
+    Zs[lane] = T(0);
+  }
+  MPCQP_PHASE(0);
+
+  // ------------------------------------------------------------ backward
+  // per-lane item(s): L / y pointers (stage offsets added per stage), e1, base
+  constexpr int nW = NX * NX, nE = NX, nH = NU * NX, nG = NU;
+  constexpr int nItems = nW + nE + nH + nG;
+  constexpr int IPL = (nItems + kWave - 1) / kWave;
+  const int sAk = tv ? NX * NX : 0, sBk = tv ? NX * NU : 0;
+  int lo[IPL], ls[IPL], lk[IPL], yo[IPL], ys[IPL], yk[IPL], dst[IPL], dpar[IPL], dk[IPL];
+  T base[IPL];
+  bool act[IPL], e1[IPL];  // e1: the item adds eta_{k+1} (a select, not a product: an
+                           // unused eta may hold anything, e.g. without the drift)
+#pragma unroll
+  for (int it = 0; it < IPL; ++it) {
+    const int e = it * kWave + lane;
+    act[it] = e < nItems;
+    e1[it] = false;
+    base[it] = T(0);
+    if (e < nW) {  // W_k(r,q)
+      const int r = e / NX, q = e % NX;
+      lo[it] = L.oA + r; ls[it] = NX; lk[it] = sAk;
+      yo[it] = L.oA + q; ys[it] = NX; yk[it] = sAk;
+      base[it] = Qs[e];
+      dst[it] = L.oW + e; dpar[it] = NX * NX; dk[it] = 0;
+    } else if (e < nW + nE) {  // eta_k(r)
+      const int r = e - nW;
+      lo[it] = L.oA + r; ls[it] = NX; lk[it] = sAk;
+      yo[it] = L.oC; ys[it] = 1; yk[it] = NX;
+      e1[it] = true;
+      dst[it] = L.oE + r; dpar[it] = NX; dk[it] = 0;
+    } else if (e < nW + nE + nH) {  // What_k(a,q)
+      const int h = e - nW - nE, aa = h / NX, q = h % NX;
+      lo[it] = L.oB + aa; ls[it] = NU; lk[it] = sBk;
+      yo[it] = L.oI + q * NX; ys[it] = 1; yk[it] = 0;
+      dst[it] = L.oWh + h; dpar[it] = 0; dk[it] = NU * NX;
+    } else {  // ghat_k(a) (and idle lanes: harmless reads of B, the zeros)
+      const int aa = act[it] ? e - nW - nE - nH : 0;
+      lo[it] = L.oB + aa; ls[it] = NU; lk[it] = sBk;
+      yo[it] = L.oZ; ys[it] = 1; yk[it] = 0;
+      e1[it] = true;
+      dst[it] = L.oGh + aa; dpar[it] = 0; dk[it] = NU;
+    }
+  }
+  wave_lds_sync();
+  for (int k = N - 1; k >= 0; --k) {
+    const int p1 = (k + 1) & 1, p0 = k & 1;
+    const T* W1 = Ws + p1 * NX * NX;
+    const T* E1 = Es + p1 * NX;
+#pragma unroll
+    for (int it = 0; it < IPL; ++it) {
+      const T* Lp = sm + lo[it] + k * lk[it];
+      const T* Yp = sm + yo[it] + k * yk[it];
+      T y[NX], x[NX];
+#pragma unroll
+      for (int s2 = 0; s2 < NX; ++s2) y[s2] = Yp[s2 * ys[it]];
+#pragma unroll
+      for (int p = 0; p < NX; ++p) {
+        T acc = e1[it] ? E1[p] : T(0);
+#pragma unroll
+        for (int s2 = 0; s2 < NX; ++s2) acc = fma(W1[p * NX + s2], y[s2], acc);
+        x[p] = acc;
+      }
+      T out = base[it];
+#pragma unroll
+      for (int p = 0; p < NX; ++p) out = fma(Lp[p * ls[it]], x[p], out);
+      if (act[it]) sm[dst[it] + p0 * dpar[it] + k * dk[it]] = out;
+    }
+    wave_lds_sync();
+  }
+  MPCQP_PHASE(1);
+
+  // ------------------------------------------------------------ forward sweep
+  const int ncx = n + (want_x0 ? nx : 0);  // z columns, then the x0 columns
+  const int col = lane;
+  const bool isz = col < n;
+  const bool isx0 = !isz && col < ncx;
+  const bool isxl = want_aff && col == ncx;  // the affine lane: s = xbar
+  const int j = isz ? col / NU : -1;
+  const int bc = isz ? col - j * NU : (isx0 ? col - n : 0);
+  T bcol[NX];
+#pragma unroll
+  for (int q = 0; q < NX; ++q) bcol[q] = isz ? Bs[(tv ? j : 0) * NX * NU + q * NU + bc] : T(0);
+  T s[NX];
+#pragma unroll
+  for (int q = 0; q < NX; ++q) s[q] = isx0 ? (q == bc ? T(1) : T(0)) : (isxl ? X0s[q] : T(0));
+  T rcol[NU];
+#pragma unroll
+  for (int aa = 0; aa < NU; ++aa) rcol[aa] = isz ? Rs[aa * NU + bc] : T(0);
+  wave_lds_sync();  // B, W, ... dead: the H ring takes over
+
+  T* Hb = a.H + (int64_t)b * ((int64_t)n * (n + 1) / 2);
+  T* Fb = a.F ? a.F + (int64_t)b * n * nx : nullptr;
+  T* Pb = a.Phi ? a.Phi + (int64_t)b * ((int64_t)N * nx * nx) : nullptr;
+  T* Gb = a.Gam ? a.Gam + (int64_t)b * gam_packed_size(nx, NU, N) : nullptr;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int FW = (kWave / 2) * VEC;  // flush window: half a wave of 16-byte stores
+  typedef T VT __attribute__((ext_vector_type(VEC)));
+  T* RH = sm + L.oRH;
+  const int RHM = a.rh - 1;
+  const int dh = (int)(((uintptr_t)Hb / sizeof(T)) % VEC);
+  T* Hal = Hb - dh;
+  const int hiH = dh + n * (n + 1) / 2;
+  auto flush = [&](int w) {
+    const int p0 = w + lane * VEC;
+    if (lane < kWave / 2 && p0 < hiH && p0 + VEC > dh) {
+      const VT v = *reinterpret_cast<const VT*>(RH + (p0 & RHM));
+      if (p0 >= dh && p0 + VEC <= hiH) {
+        __builtin_nontemporal_store(v, reinterpret_cast<VT*>(Hal + p0));
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e)
+          if (p0 + e >= dh && p0 + e < hiH) Hal[p0 + e] = v[e];
+      }
+    }
+  };
+  // Gamma column vectors: one or more 16-byte stores when nx == NX and the
+  // instance's packed block is 16-byte aligned, element stores otherwise
+  constexpr int GV = NX * (int)sizeof(T) / 16;
+  const bool gvec = Gb && nx == NX && GV >= 1 && (NX * (int)sizeof(T)) % 16 == 0 &&
+                    ((uintptr_t)Gb % 16) == 0;
+  int fh = 0;
+  for (int i = 0; i < N; ++i) {
+    const T* Ai = As + (tv ? i : 0) * NX * NX;
+    const T* Wh = Whs + i * NU * NX;
+    const bool inj = isz && (i == j);
+    T t[NX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+      T acc = isxl ? Cs[i * NX + r] : T(0);
+#pragma unroll
+      for (int q = 0; q < NX; ++q) acc = fma(Ai[r * NX + q], s[q], acc);
+      t[r] = acc;
+    }
+#pragma unroll
+    for (int q = 0; q < NX; ++q) s[q] = inj ? bcol[q] : t[q];
+    if (Gb && isz && col < (i + 1) * NU) {
+      T* g = Gb + gam_packed_off(nx, NU, i) + col * nx;
+      if (gvec) {
+        typedef T GT __attribute__((ext_vector_type(VEC)));
+#pragma unroll
+        for (int v = 0; v < GV; ++v) {
+          GT gv;
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) gv[e] = s[v * VEC + e];
+          __builtin_nontemporal_store(gv, reinterpret_cast<GT*>(g) + v);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < NX; ++q)
+          if (q < nx) __builtin_nontemporal_store(s[q], g + q);
+      }
+    }
+    if (Pb && isx0) {
+#pragma unroll
+      for (int q = 0; q < NX; ++q)
+        if (q < nx) Pb[(i * nx + q) * nx + bc] = s[q];
+    }
+    if (a.xbar && isxl) {
+#pragma unroll
+      for (int q = 0; q < NX; ++q) Xo[i * NX + q] = s[q];
+    }
+#pragma unroll
+    for (int aa = 0; aa < NU; ++aa) {
+      T o = inj ? rcol[aa] : (isxl ? Ghs[i * NU + aa] : T(0));
+#pragma unroll
+      for (int q = 0; q < NX; ++q) o = fma(Wh[aa * NX + q], s[q], o);
+      const int r = i * NU + aa;
+      if (isz) {
+        if (col <= r) RH[(dh + r * (r + 1) / 2 + col) & RHM] = o;
+      } else if (isx0) {
+        if (Fb) Fb[r * nx + bc] = o;
+      } else if (isxl && a.f) {
+        Fo[r] = o;
+      }
+    }
+    const int rr = (i + 1) * NU;
+    const int ph = dh + rr * (rr + 1) / 2;
+    if (ph - fh >= FW) {
+      wave_lds_sync();
+      for (; ph - fh >= FW; fh += FW) flush(fh);
+      wave_lds_sync();
+    }
+  }
+  wave_lds_sync();
+  for (; fh < hiH; fh += FW) flush(fh);
+  if (a.f) {
+    T* fb = a.f + (int64_t)b * n;
+    if (lane < n) fb[lane] = Fo[lane];
+  }
+  if (a.xbar) {
+    T* xb = a.xbar + (int64_t)b * N * nx;
+    const float rN = 1.f / (float)nx;
+    for (int e = lane; e < N * nx; e += kWave) {
+      const int k = qdiv(e, nx, rN), q = e - k * nx;
+      xb[e] = Xo[k * NX + q];
+    }
+  }
+  MPCQP_PHASE(2);
+#ifdef MPCQP_PHASE_TIMING
+  mpcqp_clk.flush();
+#endif
+}
+
+template <typename T, int NX, int NU>
+static int launch_condense_stream(CondenseArgs<T> a, hipStream_t st) {
+  constexpr int VEC = 16 / (int)sizeof(T), FW = (kWave / 2) * VEC;
+  const int n = a.N * NU;
+  int rh = 1;
+  while (rh < FW + NU * n + VEC) rh <<= 1;
+  a.rh = rh;
+  a.rg = 0;
+  const size_t bytes =
+      (size_t)slayout(NX, NU, a.N, a.tv, rh, a.f ? 1 : 0, a.xbar ? 1 : 0).total * sizeof(T);
+  if (bytes > 160 * 1024) return 1;
+  if (bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)condense_stream_kernel<T, NX, NU>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(condense_stream)");
+  }
+  hipLaunchKernelGGL((condense_stream_kernel<T, NX, NU>), dim3(a.batch), dim3(kWave), bytes, st, a);
+  MPCQP_CHECK_LAUNCH("condense_stream_kernel");
+  return MPCQP_OK;
+}
+
+// The streamed kernel takes every shape whose columns (z, the x0 columns,
+// and the affine lane when f or xbar is requested) fit one wavefront, for
+// nu in {1, 2, 4} and nx <= 8, Gamma packed or not requested; 1 = not
+// applicable (MPCQP_CONDENSE_STREAM=0
+// keeps everything on condense_kernel, for A/B checks)
+template <typename T, int NX>
+static int condense_stream(const CondenseArgs<T>& a, hipStream_t st) {
+  static const int enabled = [] {
+    const char* e = getenv("MPCQP_CONDENSE_STREAM");
+    return e ? atoi(e) : 1;
+  }();
+  const int n = a.N * a.nu;
+  const int lanes = n + ((a.F || a.Phi) ? a.nx : 0) + ((a.f || a.xbar) ? 1 : 0);
+  // (a dense Gamma, structural zeros included, stays on condense_kernel's ring)
+  if (!enabled || NX > 8 || lanes > kWave || (a.Gam && !a.gpk)) return 1;
+  if (a.nu == 1) return launch_condense_stream<T, NX, 1>(a, st);
+  if (a.nu == 2) return launch_condense_stream<T, NX, 2>(a, st);
+  if (a.nu == 4) return launch_condense_stream<T, NX, 4>(a, st);
+  return 1;
+}
+
 template <typename T, int NX>
 static int launch_condense(CondenseArgs<T> a, hipStream_t st) {
+  if constexpr (NX <= 8) {
+    const int rc = condense_stream<T, NX>(a, st);
+    if (rc != 1) return rc;
+  }
   // streamed sweep when every column fits one wavefront (MPCQP_CONDENSE_RING=0: direct stores)
   static const int ring_on = [] {
     const char* e = getenv("MPCQP_CONDENSE_RING");
@@ -994,7 +1364,9 @@ static int condense_mfma(const CondenseArgs<float>& a, hipStream_t st) {
     return e ? atoi(e) : 1;
   }();
   const int n = a.N * a.nu;
-  if (!enabled || a.nx < 5 || a.nx > 15 || a.nu > 16 || n > 256 ||
+  // (packed Gamma only on the wavefront kernel: its one consumer, the
+  // z-space QP, has nx <= 4)
+  if (!enabled || a.gpk || a.nx < 5 || a.nx > 15 || a.nu > 16 || n > 256 ||
       (size_t)a.N * 16 * 16 * sizeof(float) > 160 * 1024)
     return 1;
   const int nt = (n + 15) / 16;
@@ -1026,6 +1398,7 @@ static int condense_t(int batch, int nx, int nu, int N, int flags, const void* A
   a.Qf = (const T*)Qf; a.sQf = sQf; a.c = (const T*)c; a.sC = sC;
   a.x0 = (const T*)x0; a.sX0 = sX0;
   a.H = (T*)H; a.F = (T*)F; a.f = (T*)f; a.Gam = (T*)Gam; a.Phi = (T*)Phi; a.xbar = (T*)xbar;
+  a.gpk = (flags & MPCQP_GAM_PACKED) ? 1 : 0;
   if constexpr (sizeof(T) == 4) {
     const int rc = condense_mfma(a, st);
     if (rc != 1) return rc;

@@ -257,6 +257,11 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
                   "mpcqp_mpc_qp: negative stride");
   const int sbox = (xlo || xhi) ? 1 : 0;
   const int n = N * nu, m = sbox ? N * nx : 0;
+  // stage timing: only a profiled call touches the (process-global) record,
+  // and it clears it first, so a call routed to the interior point reports
+  // -1 for every stage instead of the previous call's times
+  if (g_prof.on)
+    for (int i = 0; i < kProfN; ++i) g_prof.done[i] = false;
   if (mpc_use_ipm(dtype, nx, nu, N, sbox, flags)) {
     if (batch == 0) return MPCQP_OK;
     return mpc_ipm_impl(dtype, batch, nx, nu, N, flags, A, strideA, Bm, strideB, Q, strideQ, R,
@@ -273,7 +278,6 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
   MPCQP_CHECK_ARG(ws && ws_bytes >= L.total, "mpcqp_mpc_qp: workspace %zu bytes < %zu", ws_bytes,
                   L.total);
   hipStream_t st = (hipStream_t)stream;
-  for (int i = 0; i < kProfN; ++i) g_prof.done[i] = false;
   prof_mark(kProfStart, st);
   char* w = (char*)ws;
   const int tv = (flags & MPCQP_TV) ? 1 : 0;
@@ -339,7 +343,10 @@ extern "C" int mpcqp_mpc_qp(int dtype, int batch, int nx, int nu, int N, int fla
   const bool zf = dyn_ok && f64_fb && mpc_zf() && zf_supported(n, m, nx, nu, N);
   void* Gw = sbox ? w + L.Gam : nullptr;
   void* xbw = (sbox && !zf) ? w + L.xbar : nullptr;
-  int rc = mpcqp_condense(dtype, batch, nx, nu, N, flags, A, strideA, Bm, strideB, Q, strideQ, R,
+  // the z-space kernel reads Gamma rows as normals: its lower block triangle
+  // is all it needs (the upper one is structurally zero)
+  const int cflags = (flags & MPCQP_TV) | (zf ? MPCQP_GAM_PACKED : 0);
+  int rc = mpcqp_condense(dtype, batch, nx, nu, N, cflags, A, strideA, Bm, strideB, Q, strideQ, R,
                           strideR, Qf, strideQf, c, strideC, x0, strideX0, Hw, nullptr, fw, Gw,
                           nullptr, xbw, stream);
   if (rc != MPCQP_OK) return rc;

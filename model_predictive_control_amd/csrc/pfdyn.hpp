@@ -46,13 +46,6 @@ __device__ __forceinline__ float bperm(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(lane << 2, __float_as_int(v)));
 }
 
-// LDS exchange inside the single-wave workgroup: a wave's LDS operations
-// execute in issue order, so only the compiler must not move them (no
-// s_barrier, and no fence that would drain the outstanding global loads)
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
 
 template <int NR, typename V>
 __device__ __forceinline__ V pick(const V (&x)[NR], int i) {

@@ -48,7 +48,7 @@ struct ZfArgs {
   int batch, n, m;
   const float* M;               // -H^-1, n x n row-major per instance (sweep_hinv)
   const float* s0;              // -H^-1 f (n per instance)
-  const float* Gam;             // condensed Gamma, m x n row-major (row normals)
+  const float* Gam;             // condensed Gamma, lower block triangle (MPCQP_GAM_PACKED; row normals)
   const float* f; int64_t sf;
   const float* lb; int64_t sLb;
   const float* ub; int64_t sUb;
@@ -103,6 +103,15 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
   float* ext = reinterpret_cast<float*>(pool + kPool);
   const float* xlo = d.xlo ? d.xlo + (int64_t)b * d.sXb : nullptr;
   const float* xhi = d.xhi ? d.xhi + (int64_t)b * d.sXb : nullptr;
+  // Gamma row j (state x_{k+1}, k = j / nx, component q): its (k+1) nu
+  // leading columns, entry col at gr[col * nx] (the packed block stores
+  // columns); the rest of the row is structurally zero
+  const float* Gb = a.Gam + (int64_t)b * gam_packed_size(nx, d.nu, d.N);
+  auto gam_row = [&](int j, int& len) __attribute__((always_inline)) -> const float* {
+    const int k = j / nx;
+    len = (k + 1) * d.nu;
+    return Gb + gam_packed_off(nx, d.nu, k) + (j - k * nx);
+  };
 
   // ------------------------------------------------------------ per z index
   const bool zl_ok = l < n;
@@ -272,9 +281,11 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
         while (gs) {
           const int sl = __builtin_ctzll(gs);
           gs &= gs - 1;
-          int e = (b * m + readlane(sidx, sl)) * n + l;
+          int len;
+          const float* gr = gam_row(readlane(sidx, sl), len);
+          int e = l;
           asm volatile("" : "+v"(e));
-          const float dsum = wave_sum(l < n ? a.Gam[e] * pv : 0.f);
+          const float dsum = wave_sum(e < len ? gr[e * nx] * pv : 0.f);
           if (l == sl) bs = ssgn * dsum;
         }
       }
@@ -297,9 +308,11 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
         if (bb != kZfGlobal) {
           nv = nrm[bb][l];
         } else {
-          int e = (b * m + readlane(sidx, s)) * n + l;
+          int len;
+          const float* gr = gam_row(readlane(sidx, s), len);
+          int e = l;
           asm volatile("" : "+v"(e));
-          nv = l < n ? a.Gam[e] : 0.f;
+          nv = e < len ? gr[e * nx] : 0.f;
         }
         acc = fmaf(coef, nv, acc);
       }
@@ -309,7 +322,9 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
     };
     // row normal Gamma_j (row j of the condensed Gamma) into buffer bb
     auto row_normal = [&](int j, int bb) __attribute__((always_inline)) {
-      const float v = l < n ? a.Gam[((int64_t)b * m + j) * n + l] : 0.f;
+      int len;
+      const float* gr = gam_row(j, len);
+      const float v = l < len ? gr[l * nx] : 0.f;
       wave_lds_sync();
       nrm[bb][l] = v;
       wave_lds_sync();

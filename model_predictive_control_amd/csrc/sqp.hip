@@ -265,6 +265,14 @@ __device__ double box_viol(const SqpArgs& a, int64_t b, int k, const double* x) 
 // Search direction component i of instance b: Z - U, except for an input
 // the QP held at its bound (fix bit set when the QP was built), which stays
 // put -- the interior-point QP leaves such an input a barrier gap inside.
+// An exact-Hessian QP holds it by the proximal term of bike_hess_kernel; in
+// the Gauss-Newton phase before the switch the zeroed components make the
+// step a projected one (an input on its bound whose gradient pushes outward
+// stays there), checked by the merit line search like any other step.
+// Measured on the saturated-tail fixtures (tests/golden/nlp_tail.npz):
+// holding only in exact mode, or giving the Gauss-Newton QP the proximal
+// term as well, sends 1-2 of the 10 to another local minimum.  A controller
+// that never builds H2 (hessian="gauss-newton") passes no fix array.
 __device__ __forceinline__ double sqp_dir(const SqpArgs& a, int64_t b, int i) {
   const int64_t o = b * a.N * 2 + i;
   if (a.fix && ((a.fix[b * a.N + (i >> 1)] >> (i & 1)) & 1)) return 0.0;

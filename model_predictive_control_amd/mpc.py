@@ -163,13 +163,43 @@ class MPCController:
                                                **self._box())
             self.last_lam_g = lam
             U = z.view(b, N, nu)
-        # predicted states x_1..x_N of the last linearisation (IPOPT's "g" rows)
-        self.last_prediction = X
-        self.last_lam_u = None  # (the condensed step reports no input multipliers)
-        self.last_cost = self._cost(X0, X, U)
+        # IPOPT's "g" rows and "f" are those of the NLP at the returned inputs:
+        # the states of the prediction model's own rollout of U (not of the
+        # last linearisation), and the objective along it; the multipliers
+        # lam_x / lam_p follow from the adjoint along that rollout
+        Xn, lam_u, lam_0 = self._adjoint(X0, U, self.last_lam_g)
+        self.last_prediction = Xn[:, 1:].to(self.dtype)
+        self.last_lam_u = lam_u
+        self.last_lam_p = lam_0
+        self.last_cost = self._cost(X0, Xn[:, 1:], U)
         self._warm = torch.cat([U[:, 1:], U[:, -1:]], 1).contiguous()
         self.last_status = status
         return z, status
+
+    def _adjoint(self, X0, U, y):
+        """The NLP's adjoint at inputs U (fp64, prediction model's rollout):
+        lambda_N = Q_N x_N + y_N, lambda_k = Q x_k + y_k + A_k' lambda_{k+1},
+        with y the state-row multipliers of the halved objective (> 0 at
+        xhi; None = 0).  Returns the rollout X (b, N+1, 4), the input gradient
+        of J/2 + y'g, R u_k + B_k' lambda_{k+1} (b, N, 2), and
+        lambda_0 = Q x0 + A_0' lambda_1 (b, 4) -- the halved Lagrangian's
+        derivative in x0 (oracle/nlp.py grad / lam_p)."""
+        b, N = X0.shape[0], self.N
+        X0d, Ud = X0.double().contiguous(), U.double().reshape(b, N, self.nu).contiguous()
+        if self.integrator == "rk4":
+            A, B, _, X = batched.bicycle_linearise(X0d, Ud, self.params, self.ts, nat.MODEL_RK4)
+        else:
+            A, B, _, X = batched.bicycle_rti(X0d, Ud, self.params, self.ts, states=True)
+        Q, QN, R = self.Q.double(), self.QN.double(), self.R.double()
+        Y = torch.zeros((b, N, 4), dtype=torch.float64, device=X.device) if y is None \
+            else y.double().reshape(b, N, 4)
+        g = torch.empty((b, N, self.nu), dtype=torch.float64, device=X.device)
+        lam = X[:, N] @ QN.T + Y[:, N - 1]
+        for k in range(N - 1, -1, -1):
+            g[:, k] = Ud[:, k] @ R.T + torch.einsum("bij,bi->bj", B[:, k], lam)
+            q = Y[:, k - 1] if k > 0 else 0.0
+            lam = X[:, k] @ Q.T + q + torch.einsum("bij,bi->bj", A[:, k], lam)
+        return X, g, lam
 
     def _solve_sqp(self, X0):
         """SQP to a first-order point of the NLP (module docstring)."""
@@ -185,6 +215,7 @@ class MPCController:
         self.last_prediction = sqp.X[:, 1:]
         self.last_lam_g = sqp.y
         self.last_lam_u = sqp.qp["lam_u"] if sqp.qp is not None else None
+        self.last_lam_p = self._adjoint(X0, sqp.U, sqp.y)[2]
         self.last_cost = self._cost(X0, sqp.X[:, 1:], sqp.U)
         self.last_costates = sqp.pi
         self.last_kkt = sqp.kkt
@@ -212,11 +243,17 @@ class MPCController:
           "g"      the constraint rows: the predicted states x_1..x_N,
           "lam_g"  their multipliers in IPOPT's convention for that cost
                    (> 0 at the upper bound xhi),
-          "lam_x"  the input-bound multipliers (> 0 at ubx; SQP mode -- the
-                   condensed RTI step does not form them),
+          "lam_x"  the input-bound multipliers (> 0 at ubx): the QP's in SQP
+                   mode; in RTI mode -2 x the input gradient of the
+                   Lagrangian by the adjoint along the rollout,
+          "lam_p"  the multipliers of the parameter p = x0 (CasADi's
+                   convention, lam_p = -d(f + lam_g'g)/dp = -2 lambda_0:
+                   dJ*/dx0 = -lam_p at the optimum),
         plus "status", "success" and, in SQP mode, "kkt" (the NLP optimality
         residual) and "iterations".  The device solvers work with the halved
-        cost J/2, so their multipliers are doubled here."""
+        cost J/2, so their multipliers are doubled here.  In RTI mode "g" and
+        "f" are the prediction model's rollout of x and the objective along it
+        (IPOPT's values at that x), not the last linearisation's."""
         xa = np.asarray(x, dtype=float)
         single = xa.ndim == 1
         X0 = torch.as_tensor(xa.reshape(-1, self.nx), dtype=self.dtype, device=self.device)
@@ -227,8 +264,12 @@ class MPCController:
         g = self.last_prediction.reshape(b, -1).cpu().numpy()
         lam = (2.0 * self.last_lam_g.reshape(b, -1).double()).cpu().numpy() \
             if self.last_lam_g is not None else None
-        lam_u = (2.0 * self.last_lam_u.reshape(b, -1).double()).cpu().numpy() \
-            if self.last_lam_u is not None else None
+        if self.mode == "rti":  # -2 x the Lagrangian's input gradient (zero where free at a KKT point)
+            lam_u = (-2.0 * self.last_lam_u.reshape(b, -1)).cpu().numpy()
+        else:
+            lam_u = (2.0 * self.last_lam_u.reshape(b, -1).double()).cpu().numpy() \
+                if self.last_lam_u is not None else None
+        lam_p = (-2.0 * self.last_lam_p).cpu().numpy()
         f = self.last_cost.double().cpu().numpy()
         one = (lambda a: a[0].reshape(-1, 1)) if single else (lambda a: a)  # noqa: E731
         out = {"x": one(zn), "f": float(f[0]) if single else f, "g": one(g),
@@ -238,6 +279,7 @@ class MPCController:
             out["lam_g"] = one(lam)
         if lam_u is not None:
             out["lam_x"] = one(lam_u)
+        out["lam_p"] = one(lam_p)
         if self.mode == "sqp":
             kkt = self.last_kkt.cpu().numpy()
             it = self.last_iters.cpu().numpy()
@@ -318,7 +360,10 @@ class SqpSolver:
         self.box = ctl._box()
 
     def state(self) -> dict:
-        return dict(rho=self.rho, kkt=self.kkt, mu=self.mu, flags=self.flags, fix=self.fix)
+        # held inputs exist only for exact-Hessian QPs (the proximal term of
+        # bicycle_hessian); a Gauss-Newton controller never builds H2
+        fix = None if self.ctl.hessian == "gauss-newton" else self.fix
+        return dict(rho=self.rho, kkt=self.kkt, mu=self.mu, flags=self.flags, fix=fix)
 
     def reset(self, U0=None):
         """Cold (U0 None: zeros) or warm start; multipliers and state cleared."""

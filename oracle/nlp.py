@@ -137,6 +137,19 @@ class OCP:
                 lam = self.Q @ X[k] + y[k - 1] + A[k].T @ lam
         return g.reshape(-1), X
 
+    def lam_p(self, x0, U, y=None):
+        """CasADi's lam_p for p = x0 in IPOPT's convention for the unhalved
+        objective: lam_p = -d/dx0 (J + lam_g'g) along the single-shooting
+        rollout = -2 lambda_0, lambda_0 = Q x0 + A_0' lambda_1 (the adjoint
+        of grad() carried one stage further).  By the envelope theorem
+        dJ*/dx0 = -lam_p at a KKT point."""
+        X, A, _, _ = self.linearise(x0, U)
+        y = np.zeros((self.N, 4)) if y is None else np.asarray(y, float).reshape(self.N, 4)
+        lam = self.QN @ X[self.N] + y[self.N - 1]
+        for k in range(self.N - 1, 0, -1):
+            lam = self.Q @ X[k] + y[k - 1] + A[k].T @ lam
+        return -2.0 * (self.Q @ X[0] + A[0].T @ lam)
+
     def kkt(self, x0, U, y):
         """First-order optimality residual of (U, y): projected gradient of the
         Lagrangian on the input box, state-box violation, wrong-sign and

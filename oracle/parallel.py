@@ -148,10 +148,20 @@ def solve_map(worker, make_args, total: int, cores: int | None = None) -> list:
             else:
                 os.environ[k] = v
     per = -(-total // cores)
-    with pool:
+    try:
         parts = pool.map(worker, [make_args(k * per, min(total, (k + 1) * per))
                                   for k in range(cores) if k * per < total])
+    finally:
+        _shutdown(pool)
     return [x for part in parts for x in part]
+
+
+def _shutdown(pool) -> None:
+    """Let the workers exit on their own (close + join).  Leaving ``with pool:``
+    calls Pool.terminate(), which SIGTERMs every worker -- under rocprofv3 its
+    preloaded signal handler reports each one as an abort in the run's log."""
+    pool.close()
+    pool.join()
 
 
 def rate(worker, make_args, total: int, seconds: float, cores: int | None = None) -> dict:
@@ -172,7 +182,7 @@ def rate(worker, make_args, total: int, seconds: float, cores: int | None = None
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    with pool:
+    try:
         pool.map(_noop, range(cores))          # every worker up before the clock
         t0 = time.time()
         deadline = t0 + seconds
@@ -181,5 +191,7 @@ def rate(worker, make_args, total: int, seconds: float, cores: int | None = None
                 if k * per < total]
         counts = pool.map(worker, args)
         dt = time.time() - t0
+    finally:
+        _shutdown(pool)
     done = int(sum(counts))
     return {"value": done / dt, "done": done, "seconds": dt, "cores": cores}

@@ -190,3 +190,48 @@ def test_condense_streamed_outputs_misaligned(dev, dt, off):
     Hd = batched.unpack_lower(got["H"].double(), n).cpu().numpy()[0]
     tol = 1e-10 if dt == torch.float64 else 2e-5
     assert np.abs(Hd - o["H"]).max() <= tol * max(1.0, np.abs(o["H"]).max())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("nx,nu,N,off", [(4, 2, 30, 0), (4, 2, 30, 3), (2, 1, 20, 1), (3, 2, 7, 2),
+                                         (6, 2, 10, 0), (4, 3, 40, 1)])
+def test_condense_gam_packed(dev, dt, nx, nu, N, off):
+    """MPCQP_GAM_PACKED: Gamma's lower block triangle only (SURVEY 8(d)'s output list).
+    Streamed (n <= 64) and direct sweeps, misaligned starts, an nx that would take the
+    MFMA kernel in fp32 (it runs on the wavefront kernel): the packed stream equals the
+    dense call's lower block triangle bit for bit, matches the explicit oracle, and
+    nothing outside it is written."""
+    rng = np.random.default_rng(700 + 10 * nx + N + off)
+    batch = 5
+    A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, True, batch)
+    x0 = rng.normal(size=(batch, nx))
+    c = rng.normal(size=(batch, N, nx))
+    args = (_t(A, dev, dt), _t(B, dev, dt), _t(Q, dev, dt), _t(R, dev, dt), _t(Qf, dev, dt), N)
+    kw = dict(x0=_t(x0, dev, dt), c=_t(c, dev, dt), tv=True, outputs=("H", "f", "Gam"))
+    dense = batched.condense(*args, **kw)
+    numel = batch * nx * nu * N * (N + 1) // 2
+    buf = torch.full((numel + off + 8,), 7.0, dtype=dt, device=dev)
+    pk = buf[off:off + numel].view(batch, -1)
+    got = batched.condense(*args, **kw, out={"Gam": pk}, gam_packed=True)
+    torch.cuda.synchronize()
+    assert bool((buf[:off] == 7.0).all()) and bool((buf[off + numel:] == 7.0).all())
+    G = batched.unpack_gam(got["Gam"], N, nx, nu)
+    tol = 1e-10 if dt == torch.float64 else 2e-5
+    if dt == torch.float32 and 5 <= nx <= 15:
+        # the dense fp32 call ran on the MFMA kernel: same values up to rounding
+        for k, v in (("H", got["H"]), ("f", got["f"]), ("Gam", G)):
+            s = max(1.0, float(dense[k].abs().max()))
+            assert float((v - dense[k]).abs().max()) <= tol * s, k
+    else:
+        # same recursion for H and Gamma; f comes from the affine lane (y = W xbar + eta)
+        # here and from the adjoint chain on the dense call's kernel: equal up to rounding
+        assert torch.equal(got["H"], dense["H"])
+        assert torch.equal(G, dense["Gam"])  # the upper block triangle of the dense call is 0
+        s = max(1.0, float(dense["f"].abs().max()))
+        assert float((got["f"] - dense["f"]).abs().max()) <= tol * s
+    for b in range(batch):
+        o = oc.condense(A[b], B[b], Q, R, Qf, N, x0=x0[b], c=c[b])
+        g = G[b].double().cpu().numpy()
+        assert np.abs(g - o["Gam"]).max() <= tol * max(1.0, np.abs(o["Gam"]).max())
+        f = got["f"][b].double().cpu().numpy()
+        assert np.abs(f - o["f"]).max() <= tol * max(1.0, np.abs(o["f"]).max())

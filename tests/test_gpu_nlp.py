@@ -318,3 +318,66 @@ def test_held_inputs_sit_on_their_bounds(golden):
             break
     assert bool(sqp.done().all())
     assert held_seen > 0
+
+
+def test_gauss_newton_on_saturated_tail(golden):
+    """A Gauss-Newton controller never builds the held-input proximal term, so
+    its step kernel gets no held inputs (fix stays clear) and moves every input
+    along the QP's own direction: on the saturated-tail fixtures
+    (tests/golden/nlp_tail.npz) it reaches the oracle's optimum."""
+    from model_predictive_control_amd.mpc import SqpSolver
+
+    g = golden("nlp_tail.npz")
+    ctl = MPCController(int(g["N"]), float(g["ts"]), VehicleParameters(),
+                        hessian="gauss-newton", max_iter=400, tol=1e-8)
+    X0 = torch.as_tensor(g["x0"], dtype=torch.float64, device=ctl.device)
+    sqp = SqpSolver(ctl, X0.shape[0])
+    sqp.reset()
+    for _ in range(ctl.max_iter):
+        sqp.iterate(X0)
+        if bool(sqp.done().all()):
+            break
+    assert int(sqp.fix.abs().sum()) == 0
+    assert bool(sqp.done().all()), sqp.kkt.cpu().numpy()
+    U = sqp.U.reshape(X0.shape[0], -1).cpu().numpy()
+    assert np.abs(U - g["U"]).max() < 1e-5
+
+
+@pytest.mark.parametrize("tag", ["main", "sol"])
+def test_solve_returns_lam_p(golden, tag):
+    """CasADi's nlpsol dict (main.py:115-116) also carries lam_p, the multiplier of
+    the parameter p = x0: -d(f + lam_g'g)/dx0 along the rollout, i.e. -2 lambda_0 of
+    the device adjoint at the returned optimum.  Against oracle/nlp.py lam_p at the
+    fixture optimum (which test_oracle pins to the optimal value's sensitivity)."""
+    g = golden("nlp_s4.npz")
+    ocp = _ocp(g, tag)
+    X0, Ustar, Ystar = g[f"{tag}_x0"], g[f"{tag}_U"], g[f"{tag}_y"]
+    sol = _controller(g, tag).solve(X0)
+    assert np.asarray(sol["success"]).all()
+    for i, x0 in enumerate(X0):
+        lp = ocp.lam_p(x0, Ustar[i], Ystar[i])
+        assert np.abs(sol["lam_p"][i] - lp).max() < 1e-6 * (1 + np.abs(lp).max()), (i, sol["lam_p"][i], lp)
+    one = _controller(g, tag).solve(X0[0])
+    assert one["lam_p"].shape == (4, 1)
+
+
+def test_rti_mode_result_mapping(golden):
+    """mode='rti' (fixed RTI steps on mpcqp_mpc_qp) reports IPOPT's keys at the inputs
+    it returns: "g" and "f" on the prediction model's own rollout of x (not the last
+    linearisation's states); lam_x and lam_p from the adjoint along that rollout with
+    the returned lam_g -- each against oracle/nlp.py evaluated at the same point."""
+    g = golden("nlp_s4.npz")
+    ocp = _ocp(g, "main")
+    x0 = g["main_x0"][0]
+    rti = MPCController(30, 0.08, VehicleParameters(), mode="rti", sqp_iters=3)
+    sol = rti.solve(x0)
+    U = np.asarray(sol["x"]).reshape(-1)
+    y = np.asarray(sol["lam_g"]).reshape(-1) / 2.0
+    X, _, _, _ = ocp.linearise(x0, U)
+    assert np.abs(np.asarray(sol["g"]).reshape(-1) - X[1:].reshape(-1)).max() < 1e-12
+    assert abs(sol["f"] - ocp.cost(x0, U)) < 1e-10 * (1 + abs(sol["f"]))
+    grad, _ = ocp.grad(x0, U, y)
+    lam_x = np.asarray(sol["lam_x"]).reshape(-1)
+    assert np.abs(lam_x + 2 * grad).max() < 1e-9 * (1 + np.abs(grad).max())
+    lp = ocp.lam_p(x0, U, y)
+    assert np.abs(np.asarray(sol["lam_p"]).reshape(-1) - lp).max() < 1e-9 * (1 + np.abs(lp).max())

@@ -181,3 +181,43 @@ def test_mpc_controller_model_params_and_x_obs():
     if not torch.cuda.is_available():
         with pytest.raises(RuntimeError):
             mpc.MPCController(10, 0.08, model=bicycle.KinematicBicycle(bad))
+
+
+def test_unpack_gam_layout():
+    """The MPCQP_GAM_PACKED layout (include/mpcqp.h): block row k holds its (k+1)*nu
+    leading columns from nx*nu*k*(k+1)/2, column by column; unpack_gam inverts it."""
+    import torch
+
+    from model_predictive_control_amd import batched
+    from oracle import condense as oc
+    rng = np.random.default_rng(5)
+    nx, nu, N = 3, 2, 6
+    A = rng.normal(size=(nx, nx)) * 0.5
+    B = rng.normal(size=(nx, nu))
+    G = oc.condense(A, B, np.eye(nx), np.eye(nu), np.eye(nx), N)["Gam"]
+    packed = np.concatenate([G[k * nx:(k + 1) * nx, :(k + 1) * nu].T.ravel() for k in range(N)])
+    assert packed.size == nx * nu * N * (N + 1) // 2
+    got = batched.unpack_gam(torch.as_tensor(packed)[None], N, nx, nu)[0].numpy()
+    assert np.array_equal(got, G)
+
+
+def test_bound_pair_strides():
+    """batched._bound_pair: one stride for a bound pair; a shared side next
+    to a per-instance one is broadcast, never read with the other side's stride."""
+    import pytest
+    import torch
+
+    from model_predictive_control_amd import batched
+    b, w = 3, 8
+    shared = torch.arange(w, dtype=torch.float64)
+    per = torch.randn(b, w, dtype=torch.float64)
+    lo, hi, s = batched._bound_pair(shared, None, b, w, "x")
+    assert s == 0 and lo is shared and hi is None
+    lo, hi, s = batched._bound_pair(shared, per, b, w, "x")
+    assert s == w and lo.shape == (b, w) and torch.equal(lo[2], shared) and torch.equal(hi, per)
+    lo, hi, s = batched._bound_pair(per, shared, b, w, "x")
+    assert s == w and hi.shape == (b, w) and hi.is_contiguous() and torch.equal(hi[1], shared)
+    lo, hi, s = batched._bound_pair(None, None, b, w, "x")
+    assert (lo, hi, s) == (None, None, 0)
+    with pytest.raises(ValueError):
+        batched._bound_pair(torch.zeros(b, w + 1), None, b, w, "x")

@@ -137,3 +137,30 @@ def test_bicycle_oracle_jacobian():
     A, B = ob.fe_jac_fd(x, u, 0.08)
     assert A.shape == (4, 4) and B.shape == (4, 2)
     assert abs(A[3, 3] - (1 - 0.08)) < 1e-7 and abs(B[3, 0] - 0.16) < 1e-7
+
+
+def test_oracle_lam_p_is_value_sensitivity(golden):
+    """oracle/nlp.py lam_p (CasADi's multiplier of the parameter x0): by the envelope
+    theorem the optimal value's derivative dJ*/dx0 equals -lam_p.  Checked by central
+    differences of the oracle's own optimum (warm-started re-solves) on a fixture of
+    tests/golden/nlp_s4.npz (session_4/main.py weights)."""
+    from oracle import nlp
+
+    g = golden("nlp_s4.npz")
+    xlo, lbu = g["xlo"], g["lbu"]
+    ocp = nlp.OCP(int(g["main_N"]), float(g["main_ts"]), g["main_Q"], g["main_QN"],
+                  g["main_R"], xlo, -xlo, lbu, -lbu)
+    x0, U, y = g["main_x0"][0], g["main_U"][0], g["main_y"][0]
+    lp = ocp.lam_p(x0, U, y)
+    h = 1e-5
+    fd = np.zeros(4)
+    for i in range(4):
+        J = []
+        for sgn in (1.0, -1.0):
+            xp = x0.copy()
+            xp[i] += sgn * h
+            Up, _, k = ocp.solve(xp, U0=U)
+            assert k < 1e-10
+            J.append(ocp.cost(xp, Up))
+        fd[i] = (J[0] - J[1]) / (2 * h)
+    assert np.abs(fd + lp).max() < 1e-5 * (1 + np.abs(lp).max()), (fd, -lp)

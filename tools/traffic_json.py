@@ -6,7 +6,10 @@ import csv
 import json
 import sys
 
-ROLES = [("mpc_group_kernel", "mpc_box"), ("mpc_quad_kernel", "mpc_box"), ("mpc_box_kernel", "mpc_box"), ("box_quad_kernel", "solve_box"),
+# first match wins: the fp64 hand-off's kernels (empty launches when no
+# instance is handed off) must not be averaged into the fp32 kernels' roles
+ROLES = [("condense_kernel<double", "fallback64"), ("qp_wg_count_kernel", "fallback64"),
+         ("condense_stream_kernel", "condense"), ("mpc_group_kernel", "mpc_box"), ("mpc_quad_kernel", "mpc_box"), ("mpc_box_kernel", "mpc_box"), ("box_quad_kernel", "solve_box"),
          ("box_gi_kernel", "solve_box"), ("condense_kernel", "condense"),
          ("condense_mfma_kernel", "condense"), ("sweep_mfma_kernel", "sweep"), ("sweep_rows_kernel", "sweep"), ("qp_pf_kernel", "solve_pf"), ("qp_zf_kernel", "solve_zf"), ("ipm_", "ipm"),
          ("qp_wg_kernel", "solve_qp"),
