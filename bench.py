@@ -491,7 +491,7 @@ class Config3:
         # row is checked once at the end), the dynamics (A_k, B_k, c_k, x0)
         # of the refinement, the shared bounds once; writes z, y, status
         zb = (n * n + 2 * n + m * n + N * (nx * nx + nx * nu + nx) + nx + n + m + 1) * 4 * bsz
-        r_c = roof("condense_kernel<float,4>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
+        r_c = roof("condense_stream_kernel<float,4,2>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
                    traffic.get("condense"), {"bytes_per_launch": cb, "bytes_moved_per_launch": cm,
                                              "bytes": "SURVEY 8(d)"})
         r_w = roof("sweep_mfma_kernel<4> (H^-1)", "mfma", wf, t_w, FP32_PEAK_TFS, "TFLOP/s",
@@ -705,7 +705,7 @@ class Config5:
         # not a rate of this kernel and is not reported as one)
         cb = condense_bytes_survey(nx, nu, N, 4, False) * bsz
         cm = condense_bytes_per_instance(nx, nu, N, 4, tv=True) * bsz
-        r_c = roof("condense_mfma_kernel<10,4>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
+        r_c = roof("condense_mfma_fh_kernel<10> (fused-H)", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
                    traffic.get("condense"), {"bytes_per_launch": cb, "bytes_moved_per_launch": cm,
                                              "bytes": "SURVEY 8(d)"})
         wf = sweep_flops_per_instance(n) * bsz

@@ -1334,6 +1334,317 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
 #endif
 }
 
+// ------------------------------------------------------- fused-H MFMA path
+// condense_mfma_fh_kernel<NT> (fp32, 5 <= nx <= 12, nu <= 4, no drift): the
+// H rows come out of the forward MFMA itself.  With nx <= 12 the state slots
+// 12..14 and the affine slot (tile positions 3, 7, 11, 15 = register 3 of
+// every lane group, cm_state) carry nothing in Gamma~ or Phi, so the four
+// output rows at those positions are free: the forward A operand gets
+// (What_r A_r)[a, :] in the lanes of output row 4a + 3, and
+//     D = [A_r; What_r A_r] Gamma~_r
+// gives Gamma~_{r+1} (registers 0..2, before the injection of B_r) AND the
+// H rows of block r (register 3: What_r A_r Gamma~_r = What_r Gamma~_{r+1}
+// off the diagonal block) in the same three 16x16x4 MFMAs; the E tile gives
+// [F | f] the same way.  No VALU epilogue, no What_k in LDS.
+// The backward pass gets What_k A_k and the diagonal block What_k B_k from
+// its own recursion: with Z_k = A~_k whose unused columns (positions 4b + 3)
+// hold B_k[:, b],
+//     X = W~_{k+1} Z_k,   Y = Q~ + Z_k' X,
+// Y's state block is W~_k, its row 4b + 3 is (B_k' W~_{k+1} A_k)[b, :] =
+// (What_k A_k)[b, :] and its entry (4b + 3, 4c + 3) is (What_k B_k)[b, c] --
+// six MFMAs per stage (three K chunks each: state slots only) for what took
+// twelve (X, W~, What).  LDS per instance: (What A)_k (4 x 12) and
+// What_k B_k + R (4 x 4) per stage, the footprint What had.
+#ifndef MPCQP_FH_PF
+#define MPCQP_FH_PF 8   // backward prefetch depth (stages)
+#endif
+#ifndef MPCQP_FH_PFF
+#define MPCQP_FH_PFF 4  // forward prefetch depth (stages)
+#endif
+__device__ __forceinline__ mf4 mfma3(const float* a, const float* b, mf4 acc) {
+#pragma unroll
+  for (int s = 0; s < 3; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+  return acc;
+}
+template <int NT, bool EXACT, bool X3>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void condense_mfma_fh_kernel(CondenseArgs<float> a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  float* whA = reinterpret_cast<float*>(smem_raw);  // (What_k A_k)[b][state]: N x 4 x 12
+  float* dgs = whA + a.N * 48;                      // What_k B_k + R: N x 4 x 4
+  // (exactly 256 floats per stage: 10 KB at N = 40, four waves per SIMD)
+#ifdef MPCQP_PHASE_TIMING
+  PhaseClock mpcqp_clk;
+#endif
+  const int b = blockIdx.x;
+  const int l = threadIdx.x, g = l >> 4, cl = l & 15;
+  const int nx = a.nx, nu = a.nu, N = a.N, n = N * nu;
+  const int64_t sa = a.tv ? (int64_t)nx * nx : 0, sbk = a.tv ? (int64_t)nx * nu : 0;
+  const float* Ab = a.A + (int64_t)b * a.sA;
+  const float* Bb = a.B + (int64_t)b * a.sB;
+  // position cl: a state column (zc false, state sc) or input column zb of
+  // Z (backward) / H row zb of the forward A operand (zc true)
+  const bool zc = (cl & 3) == 3;
+  const int zb = cl >> 2;
+  const int sc = cm_state(cl);
+  // R[g][zb]: what this lane adds to its entry of What_k B_k
+  const float rgz = (zc && g < nu && zb < nu) ? a.R[(int64_t)b * a.sR + g * nu + zb] : 0.f;
+  // backward prefetch depth (stages): a stage is a few hundred cycles of
+  // MFMA chain, an HBM miss under load several thousand
+  constexpr int PF = MPCQP_FH_PF;
+  // Memory instructions, not bytes, bound this kernel's loads (dword gathers
+  // of 64 lanes): one load per operand register and stage.  Backward: Z's
+  // column of this lane comes from A (state column sc, stride nx) or from B
+  // (input column zb, stride nu) through a per-lane pointer; a lane outside
+  // both reads A's first element and is masked to 0.
+  const bool zv = (zc ? (zb < nu) : (sc < nx)) && 3 * g < nx;  // (rows past nx: never read)
+  const float* zp = !zv ? Ab : (zc ? Bb + zb + 3 * g * nu : Ab + sc + 3 * g * nx);
+  const int zstep = !zv ? 0 : (zc ? nu : nx);
+  const int zstage = !zv ? 0 : (int)(zc ? sbk : sa);  // in-instance offsets: 32-bit
+  float zm[3];
+  int zo[3];  // element offsets (a row past nx re-reads row 3g: never out of bounds)
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    zm[s] = (zv && 3 * g + s < nx) ? 1.f : 0.f;
+    zo[s] = (zv && 3 * g + s < nx) ? s * zstep : 0;
+  }
+
+  // ------------------------------------------------ backward
+  float wB[3], qC[4];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int sp = 3 * g + s;
+    wB[s] = (sp < nx && sc < nx) ? a.Qf[(int64_t)b * a.sQf + sp * nx + sc] : 0.f;
+    qC[s] = (sp < nx && sc < nx) ? a.Q[(int64_t)b * a.sQ + sp * nx + sc] : 0.f;
+  }
+  qC[3] = 0.f;
+  auto load_bw = [&](int k, float (&za)[3]) {
+    const float* p = zp + k * zstage;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) za[s] = p[zo[s]];
+  };
+  auto bw_stage = [&](int k, float (&za)[3]) {
+    const float z[3] = {za[0] * zm[0], za[1] * zm[1], za[2] * zm[2]};
+    // the slot is consumed before its refill is issued: otherwise the
+    // scheduler hoists the refill above the consumption, the refill needs
+    // fresh registers and the loop's back edge copies them into the slot --
+    // a wait on every outstanding load once per PF stages
+    __builtin_amdgcn_sched_barrier(0);
+    load_bw(k - PF >= 0 ? (k - PF < N ? k - PF : N - 1) : 0, za);
+    // alignment padding (k >= N, the first stages when N % PF != 0) runs
+    // without effect instead of branching around: a branch here makes the
+    // queue slots loop-carried through copies again
+    const bool live = EXACT || k < N;
+    const mf4 X = mfma3(wB, z, mf4{0.f, 0.f, 0.f, 0.f});  // W~ Z (W~ symmetric)
+    const float xv[3] = {X[0], X[1], X[2]};
+    const mf4 Y = mfma3(z, xv, mf4{qC[0], qC[1], qC[2], qC[3]});  // Q~ + Z' W~ Z
+    if (live && g < nu) {
+      if (!zc) whA[(k * 4 + g) * 12 + sc] = Y[3];
+      else if (zb < nu) dgs[(k * 4 + g) * 4 + zb] = Y[3] + rgz;
+    }
+#pragma unroll
+    for (int s = 0; s < 3; ++s) wB[s] = live ? (zc ? 0.f : Y[s]) : wB[s];
+  };
+  float qz[PF][3];
+  const int ktop = N - 1 + (PF - N % PF) % PF;
+#pragma unroll
+  for (int d = 0; d < PF; ++d) {
+    const int k = ktop - d;
+    load_bw(k < N ? (k >= 0 ? k : 0) : N - 1, qz[d]);
+  }
+  for (int k0 = ktop; k0 >= 0; k0 -= PF) {
+#pragma unroll
+    for (int d = 0; d < PF; ++d) bw_stage(k0 - d, qz[d]);
+  }
+  wave_lds_sync();
+  MPCQP_PHASE(0);
+
+  // ------------------------------------------------ forward
+  const bool wantE = a.f || a.F || a.Phi || a.xbar;
+  const rsrc_t rH = mk_rsrc(a.H + (int64_t)b * ((int64_t)n * (n + 1) / 2), (int64_t)n * (n + 1) / 2 * 4);
+  const rsrc_t rG = mk_rsrc(a.Gam ? a.Gam + (int64_t)b * ((int64_t)N * nx * n) : a.H,
+                            a.Gam ? (int64_t)N * nx * n * 4 : 0);
+  const rsrc_t rF = mk_rsrc(a.F ? a.F + (int64_t)b * n * nx : a.H, a.F ? (int64_t)n * nx * 4 : 0);
+  const rsrc_t rf = mk_rsrc(a.f ? a.f + (int64_t)b * n : a.H, a.f ? (int64_t)n * 4 : 0);
+  const rsrc_t rP = mk_rsrc(a.Phi ? a.Phi + (int64_t)b * N * nx * nx : a.H, a.Phi ? (int64_t)N * nx * nx * 4 : 0);
+  const rsrc_t rX = mk_rsrc(a.xbar ? a.xbar + (int64_t)b * N * nx : a.H, a.xbar ? (int64_t)N * nx * 4 : 0);
+  float gB[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) gB[t][s] = 0.f;
+  float eB[3];
+  {
+    const float* X0b = a.x0 ? a.x0 + (int64_t)b * a.sX0 : nullptr;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int p = 4 * g + s, sp = 3 * g + s;
+      float v = 0.f;
+      if (sp < nx && sc < nx) v = (p == cl) ? 1.f : 0.f;
+      else if (cl == 15 && sp < nx) v = X0b ? X0b[sp] : 0.f;
+      eB[s] = v;
+    }
+  }
+  // Forward: the A operand of a state lane is row sc of A_r, columns 3g..3g+2
+  // -- contiguous, one 12-byte load when nx % 3 == 0 (X3) -- and, in K chunk
+  // 3 (the input selectors, below), B_r[sc][g]: two loads per stage.  The H
+  // lanes (zc) take (What A)_r and What_r B_r + R from LDS.  Invalid lanes
+  // read A's first element and are masked.
+  const bool av = !zc && sc < nx && 3 * g < nx;
+  const float* ap = av ? Ab + sc * nx + 3 * g : Ab;
+  const int astage = av ? (int)sa : 0;
+  float am[3];
+  int ao_[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    am[s] = (av && 3 * g + s < nx) ? 1.f : 0.f;
+    ao_[s] = (av && 3 * g + s < nx) ? s : 0;
+  }
+  const bool bv = !zc && sc < nx && g < nu;
+  const float* bp = bv ? Bb + sc * nu + g : Ab;
+  const int bstage = bv ? (int)sbk : 0;
+  const float bm = bv ? 1.f : 0.f;
+  const int zbr = zb < nu ? zb : 0, gr = g < nu ? g : 0;  // clamped LDS rows (written ones)
+  const float wm = (zc && zb < nu) ? 1.f : 0.f;
+  const float dm = (zc && zb < nu && g < nu) ? 1.f : 0.f;
+  auto load_fw = [&](int r, float (&ao)[3], float& bo) {
+    const float* p = ap + r * astage;
+    if constexpr (X3) {
+      typedef float f3 __attribute__((ext_vector_type(3)));
+      const f3 v = *reinterpret_cast<const f3*>(p);
+      ao[0] = v[0];
+      ao[1] = v[1];
+      ao[2] = v[2];
+    } else {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) ao[s] = p[ao_[s]];
+    }
+    bo = bp[r * bstage];
+  };
+  constexpr int PFF = MPCQP_FH_PFF;  // forward prefetch depth
+  auto fw_stage = [&](int r, float (&qa_)[3], float& qb_) {
+    float aA[4];
+    const int rr = r < N ? r : 0;
+    const float* wa = whA + (rr * 4 + zbr) * 12 + 3 * g;
+    const float dv = dgs[(rr * 4 + zbr) * 4 + gr];
+    // zc lanes: (What A)_r and What_r B_r + R from LDS; the others: A_r and
+    // B_r from their queue slot.  Masked arithmetic, not selects: a select on
+    // a load is turned into a masked load INTO the queue slot, whose refill
+    // then needs fresh registers (copies and a wait at the loop's back edge)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) aA[s] = fmaf(wa[s], wm, qa_[s] * am[s]);
+    aA[3] = fmaf(dv, dm, qb_ * bm);
+    // the slot is refilled at the END of the stage, once aA (its values) is
+    // dead: a refill issued while they are live needs fresh
+    // registers, which the loop's back edge copies back into the slot -- a
+    // wait on every outstanding load once per PFF stages
+    const int rnext = r + PFF < N ? r + PFF : N - 1;
+    if (!EXACT && r >= N) {  // alignment padding (EXACT: N % PFF == 0)
+      load_fw(rnext, qa_, qb_);
+      return;
+    }
+    const int blk0 = r * nu;
+    const int ntact = ((r + 1) * nu + 15) >> 4;
+    const int tlo = blk0 >> 4;  // tiles holding block r's columns: tlo..ntact-1
+    MPCQP_PHASE(1);
+    // K chunk 3 carries the input selectors on the tiles of block r: row
+    // 4b + 3 of Gamma~_r is 1 in block r's column b, and the A operand's
+    // chunk 3 is B_r (state rows) / What_r B_r + R (H rows), so the MFMA
+    // injects B_r into Gamma~_{r+1} and writes the diagonal block of H
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (t < ntact) {
+        mf4 dd;
+        if (t >= tlo) {
+          const int col = 16 * t + cl;
+          gB[t][3] = (g < nu && col == blk0 + g) ? 1.f : 0.f;
+          dd = mfma4(aA, gB[t], mf4{0.f, 0.f, 0.f, 0.f});
+        } else {
+          dd = mfma3(aA, gB[t], mf4{0.f, 0.f, 0.f, 0.f});
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) gB[t][s] = dd[s];
+      }
+    }
+    mf4 ee = mf4{0.f, 0.f, 0.f, 0.f};
+    if (wantE) ee = mfma3(aA, eB, ee);
+    MPCQP_PHASE(2);
+    const int R = blk0 + g;  // the H / F row of this lane's register 3
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = 16 * t + cl;
+      if (t < ntact) {
+        const float(&d)[4] = gB[t];
+        if (a.Gam) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {
+            const int sp = 3 * g + j;
+            bst(d[j], rG, (sp < nx && col < n) ? 4 * ((r * nx + sp) * n + col) : kOOB);
+          }
+        }
+#ifndef MPCQP_FH_NOSTORE
+        bst(d[3], rH, (g < nu && col <= R) ? 4 * (R * (R + 1) / 2 + col) : kOOB);
+#else
+        if (d[3] == 12345.f) bst(d[3], rH, 0);
+#endif
+      } else if (a.Gam && 16 * t < n) {  // structural zeros of the block row
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int sp = 3 * g + j;
+          bst(0.f, rG, (sp < nx && col < n) ? 4 * ((r * nx + sp) * n + col) : kOOB);
+        }
+      }
+    }
+    MPCQP_PHASE(3);
+    if (wantE) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int sp = 3 * g + j;
+        if (a.xbar) bst(ee[j], rX, (sp < nx && cl == 15) ? 4 * (r * nx + sp) : kOOB);
+        if (a.Phi) bst(ee[j], rP, (sp < nx && sc < nx) ? 4 * ((r * nx + sp) * nx + sc) : kOOB);
+        eB[j] = ee[j];
+      }
+      if (a.F) bst(ee[3], rF, (g < nu && sc < nx) ? 4 * (R * nx + sc) : kOOB);
+      if (a.f) bst(ee[3], rf, (g < nu && cl == 15) ? 4 * R : kOOB);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    load_fw(rnext, qa_, qb_);
+    MPCQP_PHASE(4);
+  };
+  float qa[PFF][3], qb[PFF];
+#pragma unroll
+  for (int d = 0; d < PFF; ++d) load_fw(d < N ? d : N - 1, qa[d], qb[d]);
+  for (int r0 = 0; r0 < N; r0 += PFF) {
+#pragma unroll
+    for (int d = 0; d < PFF; ++d) fw_stage(r0 + d, qa[d], qb[d]);
+  }
+#ifdef MPCQP_PHASE_TIMING
+  mpcqp_clk.flush();
+#endif
+}
+
+template <int NT, bool EXACT, bool X3>
+static int launch_condense_mfma_fh3(const CondenseArgs<float>& a, hipStream_t st) {
+  const size_t bytes = (size_t)a.N * 64 * sizeof(float);
+  if (bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)condense_mfma_fh_kernel<NT, EXACT, X3>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(condense_mfma_fh)");
+  }
+  hipLaunchKernelGGL((condense_mfma_fh_kernel<NT, EXACT, X3>), dim3(a.batch), dim3(kWave), bytes, st, a);
+  MPCQP_CHECK_LAUNCH("condense_mfma_fh_kernel");
+  return MPCQP_OK;
+}
+template <int NT, bool EXACT>
+static int launch_condense_mfma_fh2(const CondenseArgs<float>& a, hipStream_t st) {
+  return a.nx % 3 == 0 ? launch_condense_mfma_fh3<NT, EXACT, true>(a, st)
+                       : launch_condense_mfma_fh3<NT, EXACT, false>(a, st);
+}
+template <int NT>
+static int launch_condense_mfma_fh(const CondenseArgs<float>& a, hipStream_t st) {
+  return (a.N % MPCQP_FH_PF == 0 && a.N % MPCQP_FH_PFF == 0) ? launch_condense_mfma_fh2<NT, true>(a, st)
+                                                             : launch_condense_mfma_fh2<NT, false>(a, st);
+}
+
 template <int NT, int NU4, bool DRIFT, bool P12>
 static int launch_condense_mfma4(const CondenseArgs<float>& a, hipStream_t st) {
   const size_t bytes = ((size_t)a.N * NU4 * 16 + (size_t)a.nu * a.nu) * sizeof(float);
@@ -1370,6 +1681,19 @@ static int condense_mfma(const CondenseArgs<float>& a, hipStream_t st) {
       (size_t)a.N * 16 * 16 * sizeof(float) > 160 * 1024)
     return 1;
   const int nt = (n + 15) / 16;
+  // no drift, nx <= 12, nu <= 4: the fused-H kernel (MPCQP_CONDENSE_FH=0: the
+  // VALU-epilogue kernel, A/B)
+  static const int fh = [] {
+    const char* e = getenv("MPCQP_CONDENSE_FH");
+    return e ? atoi(e) : 1;
+  }();
+  if (fh && !a.c && a.nx <= 12 && (a.nu == 1 || a.nu == 2 || a.nu == 4)) {
+    if (nt <= 4) return launch_condense_mfma_fh<4>(a, st);
+    if (nt <= 8) return launch_condense_mfma_fh<8>(a, st);
+    if (nt <= 10) return launch_condense_mfma_fh<10>(a, st);
+    if (nt <= 12) return launch_condense_mfma_fh<12>(a, st);
+    return launch_condense_mfma_fh<16>(a, st);
+  }
   if (a.nu <= 4) {
     if (nt <= 4) return launch_condense_mfma<4, 4>(a, st);
     if (nt <= 8) return launch_condense_mfma<8, 4>(a, st);

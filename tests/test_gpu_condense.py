@@ -136,16 +136,20 @@ def test_condense_large_batch_pointwise(dev):
 
 @pytest.mark.parametrize("nx,nu,N,tv", [(5, 3, 6, True), (8, 2, 10, True), (12, 4, 40, True),
                                         (15, 1, 9, True), (12, 6, 20, True), (6, 12, 10, True),
-                                        (12, 4, 40, False), (7, 16, 16, True)])
-def test_condense_fp32_mfma_all_outputs(dev, nx, nu, N, tv):
+                                        (12, 4, 40, False), (7, 16, 16, True), (12, 4, 7, True),
+                                        (9, 1, 33, True)])
+@pytest.mark.parametrize("drift", [True, False])
+def test_condense_fp32_mfma_all_outputs(dev, nx, nu, N, tv, drift):
     """fp32 with 5 <= nx <= 15 runs condense_mfma_kernel (augmented-state
-    MFMA recursion): every output, per-stage drift c_k, vs the fp64 oracle."""
+    MFMA recursion; per-stage drift c_k) or, without drift for nx <= 12 and
+    nu <= 4, condense_mfma_fh_kernel (H rows from the forward MFMA's free
+    state slots): every output vs the fp64 oracle."""
     rng = np.random.default_rng(31 + 7 * nx + nu + N)
     batch = 3
     A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, tv, batch)
     A *= 0.8
     x0 = rng.normal(size=(batch, nx))
-    c = rng.normal(size=(batch, N, nx)) * 0.3 if tv else None
+    c = rng.normal(size=(batch, N, nx)) * 0.3 if (tv and drift) else None
     f32 = torch.float32
     out = batched.condense(_t(A, dev, f32), _t(B, dev, f32), _t(Q, dev, f32), _t(R, dev, f32),
                            _t(Qf, dev, f32), N, x0=_t(x0, dev, f32),

@@ -8,6 +8,7 @@ import torch
 from model_predictive_control_amd import batched, fhc, mpc, session1
 from model_predictive_control_amd.parameters import VehicleParameters
 from oracle import bicycle as ob
+from oracle import nlp as onlp
 
 pytestmark = pytest.mark.gpu
 
@@ -135,9 +136,16 @@ def test_mpc_controller_state_box_matches_oracle(dev):
         Ur, d = ob.rti_step(X0[i], np.zeros((N, 2)), ts, Q, 100 * Q, np.diag([1, 0.01]),
                             np.array([-1, -0.384]), np.array([1, 0.384]), N, xmin=xmin, xmax=xmax)
         assert np.abs(sol["x"][i].reshape(N, 2) - Ur).max() < 1e-6
+        # the QP's rows hold on the linearised prediction ...
         g = d["xbar"] + d["Gam"] @ Ur.reshape(-1)
-        assert np.abs(sol["g"][i] - g).max() < 1e-6
         assert (g <= np.tile(xmax, N) + 1e-8).all() and (g >= np.tile(xmin, N) - 1e-8).all()
+        # ... while "g" reports IPOPT's rows at the returned inputs: the model's own rollout
+        prm = (p.axis_front, p.axis_rear, p.acceleration, p.friction)
+        x, gn = X0[i], []
+        for k in range(N):
+            x = onlp.fe(x, Ur[k], ts, prm)
+            gn.append(x)
+        assert np.abs(sol["g"][i] - np.concatenate(gn)).max() < 1e-6
         active_rows += int((np.abs(g - np.tile(xmax, N)) < 1e-7).sum() + (np.abs(g - np.tile(xmin, N)) < 1e-7).sum())
     assert active_rows > 0  # the state box binds for these starts
     # ControllerLog output (session_2/log.py:8-12)

@@ -11,7 +11,7 @@ import sys
 ROLES = [("condense_kernel<double", "fallback64"), ("qp_wg_count_kernel", "fallback64"),
          ("condense_stream_kernel", "condense"), ("mpc_group_kernel", "mpc_box"), ("mpc_quad_kernel", "mpc_box"), ("mpc_box_kernel", "mpc_box"), ("box_quad_kernel", "solve_box"),
          ("box_gi_kernel", "solve_box"), ("condense_kernel", "condense"),
-         ("condense_mfma_kernel", "condense"), ("sweep_mfma_kernel", "sweep"), ("sweep_rows_kernel", "sweep"), ("qp_pf_kernel", "solve_pf"), ("qp_zf_kernel", "solve_zf"), ("ipm_", "ipm"),
+         ("condense_mfma_kernel", "condense"), ("condense_mfma_fh_kernel", "condense"), ("sweep_mfma_kernel", "sweep"), ("sweep_rows_kernel", "sweep"), ("qp_pf_kernel", "solve_pf"), ("qp_zf_kernel", "solve_zf"), ("ipm_", "ipm"),
          ("qp_wg_kernel", "solve_qp"),
          ("dual_range_kernel", "poly_solve"), ("bicycle_rti_kernel", "bicycle_rti")]
 
