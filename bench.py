@@ -988,7 +988,25 @@ class ConfigLoop:
         return err
 
     def cpu_baseline(self, seconds):
-        return None
+        """The host closed loop (oracle/parallel.py loop_chunk: per sample the
+        oracle's converged NLP solve warm-started from the shifted solution,
+        then the FE plant) over the host cores -- the reference's
+        simulate(..., policy=controller) of main.py:270-271 restated."""
+        from oracle import parallel
+
+        g = self.ctl
+        cores = parallel.host_cores()
+        total = min(self.args.batch, 8 * cores)
+        Q, QN, R = (v.cpu().numpy() for v in (g.Q, g.QN, g.R))
+        r = parallel.rate(parallel.loop_chunk, lambda lo, hi, dl: (
+            self.N, 0.08, Q, QN, R, g.lb_states, g.lb_inputs, self.X0[0, lo:hi], self.T, dl),
+            total, seconds, cores)
+        return {"value": round(r["value"], 3), "unit": "closed-loop MPC steps/s", "cores": r["cores"],
+                "kind": "port",
+                "sample": f"{r['done']} closed-loop steps of {self.T}-sample episodes "
+                          f"(oracle/nlp.py converged solve to KKT 1e-9 per sample, warm-started "
+                          f"from the shifted solution, FE plant), per-x0 episodes over "
+                          f"{r['cores']} spawned processes in {r['seconds']:.1f} s"}
 
 
 CONFIGS = {"2": Config2, "2loop": Config2Loop, "3": Config3, "4": Config4, "5": Config5,

@@ -19,6 +19,8 @@
 // rather than the stage-wise interior point's serial sweeps (1.3 ms for a
 // single instance there); the interior point keeps the list entries past
 // the slot capacity.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "quad_api.hpp"
 
@@ -157,11 +159,20 @@ __global__ __launch_bounds__(256) void fb64_scatter_kernel(Fb64Layout L, const c
 }  // namespace
 
 // slots of the fp64 hand-off: about 3 % of the batch (config 3 hands off
-// ~1 %), at least 64 (or the batch), at most 4096
+// ~1 %), at least 64 (or the batch), at most 4096.  MPCQP_FALLBACK64_CAP
+// (tests) lowers it, so that the list's remainder takes the interior point.
+// Which entries get the slots follows the list order (atomic appends): with
+// more hand-offs than slots, the solver an instance gets varies from run to
+// run, and so does its result at the level of the two fp64 solvers' rounding
+// (both return the exact active-set vertex)
 int fallback64_cap(int batch) {
   int c = batch / 32;
   if (c < 64) c = 64;
   if (c > 4096) c = 4096;
+  if (const char* e = getenv("MPCQP_FALLBACK64_CAP")) {
+    const int k = atoi(e);
+    if (k >= 1 && k < c) c = k;
+  }
   return c < batch ? c : batch;
 }
 

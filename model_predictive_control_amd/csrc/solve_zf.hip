@@ -57,6 +57,7 @@ struct ZfArgs {
   int max_iter, refine;
   float tol, dyn_stop;
   PfDyn d;
+  int force_retry;  // test knob (MPCQP_ZF_FORCE_RETRY=k): instances b % k == 0 are handed off
 };
 
 // Normals of active state rows: the first kZfRowBufs - 1 in LDS buffers, the
@@ -775,6 +776,12 @@ __global__ __launch_bounds__(64, 2) void qp_zf_kernel(ZfArgs a) {
       const bool nf = !finite(z) || !finite(su);
       if (__builtin_amdgcn_ballot_w64(nf)) { code = kStatusRetry; why = 6; }
     }
+    // the parity safety net under test: an uncertified instance is never
+    // returned OPTIMAL (tests force the hand-off of certified ones)
+    if (a.force_retry > 0 && b % a.force_retry == 0 && code == MPCQP_STATUS_OPTIMAL) {
+      code = kStatusRetry;
+      why = 15;
+    }
   }
 out:
   MPCQP_PHASE(6);
@@ -812,8 +819,9 @@ int launch_zf(int batch, int n, int m, const float* M, const float* s0, const fl
               int64_t sUb, float* z, float* y, int32_t* status, int* retry_count, int* retry_list,
               int max_iter, int refine, float tol, const PfDyn& dyn, hipStream_t st) {
   ZfArgs a{batch, n, m, M, s0, Gam, f, sf, lb, sLb, ub, sUb, z, y, status, retry_count,
-           retry_list, max_iter, refine, tol, kDynStop, dyn};
+           retry_list, max_iter, refine, tol, kDynStop, dyn, 0};
   if (const char* e = getenv("MPCQP_DYN_STOP")) a.dyn_stop = (float)atof(e);
+  if (const char* e = getenv("MPCQP_ZF_FORCE_RETRY")) a.force_retry = atoi(e);  // (read per call: tests)
   hipLaunchKernelGGL((qp_zf_kernel<4>), dim3(batch), dim3(kWave), 0, st, a);
   MPCQP_CHECK_LAUNCH("qp_zf_kernel");
   return MPCQP_OK;

@@ -90,6 +90,30 @@ def nlp_chunk(a):
     return done
 
 
+def loop_chunk(a):
+    """The reference's closed loop on the host (simulate(x0, dynamics, n, policy),
+    session_4/main.py:270-271): per sample one converged NLP solve (oracle/nlp.py,
+    warm-started from the shifted previous solution, as the device loop is), u_0
+    through the forward-Euler plant.  Returns the closed-loop steps done before
+    the deadline."""
+    from oracle import nlp
+
+    N, ts, Q, QN, R, xlo, lbu, X0, T, deadline = a
+    ocp = nlp.OCP(N, ts, Q, QN, R, xlo, -xlo, lbu, -lbu)
+    done = 0
+    for i in range(X0.shape[0]):
+        x, U = np.asarray(X0[i], float), None
+        for _ in range(T):
+            if time.time() >= deadline:
+                return done
+            U, _, _ = ocp.solve(x, U0=U, tol=1e-9)
+            U = np.asarray(U, float).reshape(N, 2)
+            x = nlp.fe(x, U[0], ts)
+            U = np.vstack([U[1:], U[-1:]])
+            done += 1
+    return done
+
+
 # -------------------------------------------- spot-check solves (bench check)
 def cfg3_solve(a):
     """Oracle solutions of config-3 instances (None where infeasible)."""

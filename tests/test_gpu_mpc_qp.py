@@ -355,3 +355,97 @@ def test_mpc_qp_stage_profiler(dev):
     assert all(t > 0.0 for t in v[:4]), v
     assert v[4] == -1.0, v
     assert torch.equal(z0, z1)
+
+
+def _cfg3_errors(pb, z, dt, N=30, xlo=None):
+    """Per-instance max|z - z_oracle| on the fp32-valued inputs the device saw."""
+    A, B, c = (pb[k].double().cpu().numpy() for k in ("A", "B", "c"))
+    X0 = pb["x0"].double().cpu().numpy()
+    r = lambda a: _rounded(a, dt)  # noqa: E731
+    Z = z.double().cpu().numpy()
+    errs, nact = [], []
+    for i in range(Z.shape[0]):
+        zr, d = _oracle_state_box(A[i], B[i], c[i], X0[i], r(pb["Q"]), r(pb["R"]), r(pb["QN"]), N,
+                                  r(pb["xlo"] if xlo is None else xlo), r(pb["xhi"]), r(pb["lb"]),
+                                  r(pb["ub"]))
+        errs.append(float(np.abs(Z[i] - zr).max()))
+        g = d["xbar"] + d["Gam"] @ zr
+        lo, hi = np.tile(r(pb["xlo"] if xlo is None else xlo), N), np.tile(r(pb["xhi"]), N)
+        nact.append(int((np.abs(g - lo) < 1e-7).sum() + (np.abs(g - hi) < 1e-7).sum()))
+    return np.array(errs), np.array(nact)
+
+
+@pytest.mark.parametrize("cap", [None, 8])
+def test_mpc_qp_zf_forced_handoff(dev, monkeypatch, cap):
+    """The z-space kernel's parity safety net (solve_zf.hip: an instance it cannot
+    certify goes to the fp64 hand-off, never OPTIMAL from the fp32 path).  The test
+    knob MPCQP_ZF_FORCE_RETRY=k hands off every k-th instance as if uncertified: they
+    come back from fallback64.hip (fp64 re-condensing + fp64 workgroup active set)
+    with STATUS_POLISHED at the fp64 solution (up to the fp32 output rounding of z),
+    the others stay certified fp32 results.  cap=8 (MPCQP_FALLBACK64_CAP) leaves the
+    list's remainder to the fp64 interior point in list mode (mpc_qp.hip): same flag,
+    same accuracy."""
+    from model_predictive_control_amd import _native as nat
+
+    k = 1 if cap else 3
+    monkeypatch.setenv("MPCQP_ZF_FORCE_RETRY", str(k))
+    if cap:
+        monkeypatch.setenv("MPCQP_FALLBACK64_CAP", str(cap))
+    dt = torch.float32
+    pb, (z, y, st) = _run_cfg3(dev, dt, b=32)
+    st = st.cpu().numpy()
+    assert ((st & 0xFF) == 0).all(), st & 0xFF
+    forced = np.arange(32) % k == 0
+    assert (st[forced] & nat.STATUS_POLISHED).all(), st
+    assert not (st[~forced] & nat.STATUS_POLISHED).any(), st
+    errs, _ = _cfg3_errors(pb, z, dt)
+    # fp64 solutions stored in fp32: |z| <= 1, so 2^-24-ish relative rounding
+    assert errs[forced].max() < 1e-7, errs[forced]
+    assert errs.max() < TOL_F32, errs
+
+
+def test_mpc_qp_zf_many_active_rows(dev):
+    """More than 15 active state rows (solve_zf.hip: normals past the 15 LDS buffers
+    are read from the packed Gamma, kZfGlobal): p_x >= 0.5 on every stage while the
+    cost pulls p_x to 0 from p_x0 in [0.52, 0.6] backing up at 0.2 -- the bound holds
+    over most of the horizon (18-27 active rows in the oracle's solution for most of
+    these starts).  Those instances stay on the fp32 path (no hand-off) and meet the
+    bar."""
+    from model_predictive_control_amd import _native as nat
+
+    dt, N = torch.float32, 30
+    pb = _bicycle_problem(dev, 32, N, seed=11, dt=dt)
+    x0 = pb["x0"].clone()
+    x0[:, 0] = torch.linspace(0.52, 0.6, 32, device=dev, dtype=dt)
+    x0[:, 3] = -0.2
+    p = VehicleParameters()
+    xa = torch.as_tensor(x0, dtype=torch.float64)
+    A, B, c = batched.bicycle_rti(xa, torch.zeros((32, N, 2), dtype=torch.float64, device=dev), p, 0.08)
+    pb.update(A=A.to(dt).contiguous(), B=B.to(dt).contiguous(), c=c.to(dt).contiguous(), x0=x0.contiguous())
+    xlo = pb["xlo"].copy()
+    xlo[0] = 0.5
+    t = lambda a: torch.as_tensor(np.asarray(a, float), dtype=dt, device=dev)  # noqa: E731
+    z, y, st = batched.mpc_qp(pb["A"], pb["B"], t(pb["Q"]), t(pb["R"]), t(pb["QN"]), N, pb["x0"],
+                              xlo=t(xlo), xhi=t(pb["xhi"]), lb=t(pb["lb"]), ub=t(pb["ub"]),
+                              c=pb["c"], tv=True)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert ((st & 0xFF) == 0).all(), st & 0xFF
+    errs, nact = _cfg3_errors(pb, z, dt, N, xlo=xlo)
+    many = nact > 15
+    assert many.sum() >= 8, nact
+    assert not (st[many] & nat.STATUS_POLISHED).any(), (st[many], nact[many])
+    assert errs.max() < TOL_F32, (errs, nact)
+
+
+def test_mpc_qp_cfg3_product_form_path(dev, monkeypatch):
+    """MPCQP_MPC_ZF=0 keeps the config-3 shape on the dense path (MFMA sweep of the
+    (n+m)^2 KKT matrix -> product-form active set with the dynamics refinement,
+    solve_pf.hip): still every instance optimal and within the bar of the oracle."""
+    monkeypatch.setenv("MPCQP_MPC_ZF", "0")
+    dt = torch.float32
+    pb, (z, y, st) = _run_cfg3(dev, dt, b=48)
+    code = batched.status_code(st).cpu().numpy()
+    assert (code == 0).all(), np.unique(code, return_counts=True)
+    errs, _ = _cfg3_errors(pb, z, dt)
+    assert errs.max() < TOL_F32, errs
