@@ -406,11 +406,40 @@ def test_mpc_qp_zf_forced_handoff(dev, monkeypatch, cap):
 
 def test_mpc_qp_zf_many_active_rows(dev):
     """More than 15 active state rows (solve_zf.hip: normals past the 15 LDS buffers
-    are read from the packed Gamma, kZfGlobal): p_x >= 0.5 on every stage while the
-    cost pulls p_x to 0 from p_x0 in [0.52, 0.6] backing up at 0.2 -- the bound holds
-    over most of the horizon (18-27 active rows in the oracle's solution for most of
-    these starts).  Those instances stay on the fp32 path (no hand-off) and meet the
-    bar."""
+    are read from the packed Gamma, kZfGlobal).  From the config-3 distribution (about
+    1 % of the instances): those the kernel certifies stay on the fp32 path (no
+    STATUS_POLISHED) and meet the bar against the oracle."""
+    from model_predictive_control_amd import _native as nat
+
+    dt, N, b = torch.float32, 30, 4096
+    pb = _bicycle_problem(dev, b, N, seed=3, dt=dt)
+    t = lambda a: torch.as_tensor(np.asarray(a, float), dtype=dt, device=dev)  # noqa: E731
+    z, y, st, X = batched.mpc_qp(pb["A"], pb["B"], t(pb["Q"]), t(pb["R"]), t(pb["QN"]), N, pb["x0"],
+                                 xlo=t(pb["xlo"]), xhi=t(pb["xhi"]), lb=t(pb["lb"]), ub=t(pb["ub"]),
+                                 c=pb["c"], tv=True, states=True)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert ((st & 0xFF) == 0).all(), np.unique(st & 0xFF)
+    Xn = X.double().cpu().numpy().reshape(b, -1)
+    lo, hi = np.tile(pb["xlo"], N), np.tile(pb["xhi"], N)
+    nact = ((np.abs(Xn - lo) < 1e-5) | (np.abs(Xn - hi) < 1e-5)).sum(1)
+    idx = np.flatnonzero(nact > 15)[:12]
+    assert idx.size >= 4, np.bincount(nact)
+    fp32 = idx[(st[idx] & nat.STATUS_POLISHED) == 0]
+    assert fp32.size >= 2, (st[idx], nact[idx])
+    sub = {k: (v[idx] if isinstance(v, torch.Tensor) else v) for k, v in pb.items()}
+    errs, nact_o = _cfg3_errors(sub, z[idx], dt, N)
+    assert (nact_o > 15).all(), nact_o
+    assert errs.max() < TOL_F32, errs
+
+
+def test_mpc_qp_dependent_rows_handoff(dev):
+    """An ill-conditioned working set: p_x >= 0.5 on consecutive stages while the
+    cost pulls p_x to 0 from p_x0 in [0.52, 0.6] backing up at 0.2 (18-27 nearly
+    dependent active rows in the oracle's solution).  The z-space kernel cannot
+    certify its fp32 refinement on most of these (it does not contract: hand-off
+    reason 3), so they are solved again by the fp64 hand-off: every instance OPTIMAL
+    at the oracle's solution, the handed-off ones to the fp32 rounding of z."""
     from model_predictive_control_amd import _native as nat
 
     dt, N = torch.float32, 30
@@ -419,8 +448,8 @@ def test_mpc_qp_zf_many_active_rows(dev):
     x0[:, 0] = torch.linspace(0.52, 0.6, 32, device=dev, dtype=dt)
     x0[:, 3] = -0.2
     p = VehicleParameters()
-    xa = torch.as_tensor(x0, dtype=torch.float64)
-    A, B, c = batched.bicycle_rti(xa, torch.zeros((32, N, 2), dtype=torch.float64, device=dev), p, 0.08)
+    A, B, c = batched.bicycle_rti(x0.double(), torch.zeros((32, N, 2), dtype=torch.float64, device=dev),
+                                  p, 0.08)
     pb.update(A=A.to(dt).contiguous(), B=B.to(dt).contiguous(), c=c.to(dt).contiguous(), x0=x0.contiguous())
     xlo = pb["xlo"].copy()
     xlo[0] = 0.5
@@ -434,8 +463,10 @@ def test_mpc_qp_zf_many_active_rows(dev):
     errs, nact = _cfg3_errors(pb, z, dt, N, xlo=xlo)
     many = nact > 15
     assert many.sum() >= 8, nact
-    assert not (st[many] & nat.STATUS_POLISHED).any(), (st[many], nact[many])
-    assert errs.max() < TOL_F32, (errs, nact)
+    pol = (st & nat.STATUS_POLISHED) != 0
+    assert pol[many].sum() >= many.sum() // 2, (st[many], nact[many])  # mostly handed off
+    assert errs[pol].max() < 1e-7, errs[pol]   # fp64 solutions, fp32 output rounding
+    assert errs.max() < TOL_F32, errs
 
 
 def test_mpc_qp_cfg3_product_form_path(dev, monkeypatch):
