@@ -218,7 +218,6 @@ __global__ __launch_bounds__(64) void condense_kernel(CondenseArgs<T> a) {
   const int lane = threadIdx.x;
   const int nx = a.nx, nu = a.nu, N = a.N, n = N * nu;
   const int tv = a.tv;
-  const int S = tv ? N : 1;
   const CLayout L = clayout(NX, nu, N, tv, a.rh, a.rg);
   T* As = sm + L.oA;
   T* Bs = sm + L.oB;
@@ -1335,7 +1334,8 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
 }
 
 // ------------------------------------------------------- fused-H MFMA path
-// condense_mfma_fh_kernel<NT> (fp32, 5 <= nx <= 12, nu <= 4, no drift): the
+// condense_mfma_fh_kernel<NT> (fp32, 5 <= nx <= 12, nu <= 4, no drift, no
+// F / Phi): the
 // H rows come out of the forward MFMA itself.  With nx <= 12 the state slots
 // 12..14 and the affine slot (tile positions 3, 7, 11, 15 = register 3 of
 // every lane group, cm_state) carry nothing in Gamma~ or Phi, so the four
@@ -1344,8 +1344,9 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
 //     D = [A_r; What_r A_r] Gamma~_r
 // gives Gamma~_{r+1} (registers 0..2, before the injection of B_r) AND the
 // H rows of block r (register 3: What_r A_r Gamma~_r = What_r Gamma~_{r+1}
-// off the diagonal block) in the same three 16x16x4 MFMAs; the E tile gives
-// [F | f] the same way.  No VALU epilogue, no What_k in LDS.
+// off the diagonal block) in the same three 16x16x4 MFMAs; f and xbar come
+// from a VALU mat-vec of the same A operand.  No VALU epilogue, no What_k in
+// LDS.
 // The backward pass gets What_k A_k and the diagonal block What_k B_k from
 // its own recursion: with Z_k = A~_k whose unused columns (positions 4b + 3)
 // hold B_k[:, b],
@@ -1366,7 +1367,7 @@ __device__ __forceinline__ mf4 mfma3(const float* a, const float* b, mf4 acc) {
   for (int s = 0; s < 3; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
   return acc;
 }
-template <int NT, bool EXACT, bool X3>
+template <int NT, bool EXACT, bool X3, bool GAM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void condense_mfma_fh_kernel(CondenseArgs<float> a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   float* whA = reinterpret_cast<float*>(smem_raw);  // (What_k A_k)[b][state]: N x 4 x 12
@@ -1457,32 +1458,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void co
   }
   wave_lds_sync();
   MPCQP_PHASE(0);
+#ifdef MPCQP_FH_NOFW  // (timing probe: the backward pass alone)
+  if (whA[0] == 12345.f) a.H[b] = whA[l];
+  return;
+#endif
 
   // ------------------------------------------------ forward
-  const bool wantE = a.f || a.F || a.Phi || a.xbar;
+  // f and xbar (no F, no Phi: those calls take condense_mfma_kernel) need
+  // one x0 column, not an E tile of three more MFMAs per stage:
+  // xbar_{r+1} = A_r xbar_r and f_r = (What A)_r xbar_r are the same mat-vec
+  // of this lane's A operand (state rows / H rows), done on the VALU (three
+  // FMAs, a sum over the four lane groups, a within-row gather for the next
+  // stage), off the MFMA chain.
+#ifndef MPCQP_FH_NOE
+  const bool wantX = a.f || a.xbar;
+#else  // (timing probe: no x0 column at all)
+  const bool wantX = false;
+#endif
   const rsrc_t rH = mk_rsrc(a.H + (int64_t)b * ((int64_t)n * (n + 1) / 2), (int64_t)n * (n + 1) / 2 * 4);
-  const rsrc_t rG = mk_rsrc(a.Gam ? a.Gam + (int64_t)b * ((int64_t)N * nx * n) : a.H,
-                            a.Gam ? (int64_t)N * nx * n * 4 : 0);
-  const rsrc_t rF = mk_rsrc(a.F ? a.F + (int64_t)b * n * nx : a.H, a.F ? (int64_t)n * nx * 4 : 0);
+  // dense Gamma (GAM: tests and callers that ask for it; mpcqp_mpc_qp does not)
+  auto rG = [&]() {
+    return mk_rsrc(a.Gam + (int64_t)b * ((int64_t)N * nx * n), (int64_t)N * nx * n * 4);
+  };
+  // (an output not asked for gets a zero-size descriptor: its stores drop)
   const rsrc_t rf = mk_rsrc(a.f ? a.f + (int64_t)b * n : a.H, a.f ? (int64_t)n * 4 : 0);
-  const rsrc_t rP = mk_rsrc(a.Phi ? a.Phi + (int64_t)b * N * nx * nx : a.H, a.Phi ? (int64_t)N * nx * nx * 4 : 0);
   const rsrc_t rX = mk_rsrc(a.xbar ? a.xbar + (int64_t)b * N * nx : a.H, a.xbar ? (int64_t)N * nx * 4 : 0);
   float gB[NT][4];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int s = 0; s < 4; ++s) gB[t][s] = 0.f;
-  float eB[3];
+  // xbar_r, states 3g..3g+2 (xbar_0 = x0), and the ds_bpermute address of
+  // tile position 4g (state 3g) in this lane's row (+4 s: state 3g + s)
+  float xv[3];
+  const int xsrc = 4 * (16 * g + 4 * g);
+  // f_r[zb] (H-row lanes of group 0) at blk0 + zb, xbar_{r+1}[sc] (state
+  // lanes of group 0) at r nx + sc: one per-lane byte base (kOOB elsewhere),
+  // the lane class picks the buffer
+  const int fxo = (g == 0 && (zc ? zb < nu : sc < nx)) ? 4 * (zc ? zb : sc) : kOOB;
   {
     const float* X0b = a.x0 ? a.x0 + (int64_t)b * a.sX0 : nullptr;
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int p = 4 * g + s, sp = 3 * g + s;
-      float v = 0.f;
-      if (sp < nx && sc < nx) v = (p == cl) ? 1.f : 0.f;
-      else if (cl == 15 && sp < nx) v = X0b ? X0b[sp] : 0.f;
-      eB[s] = v;
-    }
+    for (int s = 0; s < 3; ++s) xv[s] = (3 * g + s < nx && X0b) ? X0b[3 * g + s] : 0.f;
   }
   // Forward: the A operand of a state lane is row sc of A_r, columns 3g..3g+2
   // -- contiguous, one 12-byte load when nx % 3 == 0 (X3) -- and, in K chunk
@@ -1565,47 +1582,61 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void co
         for (int s = 0; s < 4; ++s) gB[t][s] = dd[s];
       }
     }
-    mf4 ee = mf4{0.f, 0.f, 0.f, 0.f};
-    if (wantE) ee = mfma3(aA, eB, ee);
+    if (wantX) {
+      // position cl of the sum: xbar_{r+1}[sc] (state lanes), f_r[zb] (H rows)
+      float px = fmaf(aA[2], xv[2], fmaf(aA[1], xv[1], aA[0] * xv[0]));
+      // sum over the four lane groups: permlane16_swap of (v, v) leaves rows
+      // (0, 1) and (2, 3) of the two results holding (v.r0, v.r1) and
+      // (v.r2, v.r3) in some order, so their sum is the pair sum in every
+      // lane without a select; permlane32_swap then pairs the row pairs
+      {
+        const auto s1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(px), __float_as_uint(px), false, false);
+        px = __uint_as_float(s1[0]) + __uint_as_float(s1[1]);
+        const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(px), __float_as_uint(px), false, false);
+        px = __uint_as_float(s2[0]) + __uint_as_float(s2[1]);
+      }
+      bst(px, rf, zc ? fxo + 4 * blk0 : kOOB);
+      bst(px, rX, zc ? kOOB : fxo + 4 * r * nx);
+      int xs = xsrc;
+      asm volatile("" : "+v"(xs));  // (the three addresses are formed here, not held)
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+        xv[s] = __int_as_float(__builtin_amdgcn_ds_bpermute(xs + 4 * s, __float_as_int(px)));
+    }
     MPCQP_PHASE(2);
-    const int R = blk0 + g;  // the H / F row of this lane's register 3
+    const int R = blk0 + g;  // the H row of this lane's register 3
+    // packed row R from column cl; tile t adds the immediate 64 t.  Tiles
+    // before tlo lie below the diagonal block (every column valid)
+    const int rowb = g < nu ? 4 * ((R * (R + 1) >> 1) + cl) : kOOB;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int col = 16 * t + cl;
       if (t < ntact) {
         const float(&d)[4] = gB[t];
-        if (a.Gam) {
+        if constexpr (GAM) {
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const int sp = 3 * g + j;
-            bst(d[j], rG, (sp < nx && col < n) ? 4 * ((r * nx + sp) * n + col) : kOOB);
+            bst(d[j], rG(), (sp < nx && col < n) ? 4 * ((r * nx + sp) * n + col) : kOOB);
           }
         }
 #ifndef MPCQP_FH_NOSTORE
-        bst(d[3], rH, (g < nu && col <= R) ? 4 * (R * (R + 1) / 2 + col) : kOOB);
+        if (t < tlo)  // (a uniform branch: no per-lane test below the diagonal)
+          bst(d[3], rH, rowb + 64 * t);
+        else
+          bst(d[3], rH, col <= R ? rowb + 64 * t : kOOB);
 #else
         if (d[3] == 12345.f) bst(d[3], rH, 0);
 #endif
-      } else if (a.Gam && 16 * t < n) {  // structural zeros of the block row
+      } else if (GAM && 16 * t < n) {  // structural zeros of the block row
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           const int sp = 3 * g + j;
-          bst(0.f, rG, (sp < nx && col < n) ? 4 * ((r * nx + sp) * n + col) : kOOB);
+          bst(0.f, rG(), (sp < nx && col < n) ? 4 * ((r * nx + sp) * n + col) : kOOB);
         }
       }
     }
     MPCQP_PHASE(3);
-    if (wantE) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int sp = 3 * g + j;
-        if (a.xbar) bst(ee[j], rX, (sp < nx && cl == 15) ? 4 * (r * nx + sp) : kOOB);
-        if (a.Phi) bst(ee[j], rP, (sp < nx && sc < nx) ? 4 * ((r * nx + sp) * nx + sc) : kOOB);
-        eB[j] = ee[j];
-      }
-      if (a.F) bst(ee[3], rF, (g < nu && sc < nx) ? 4 * (R * nx + sc) : kOOB);
-      if (a.f) bst(ee[3], rf, (g < nu && cl == 15) ? 4 * R : kOOB);
-    }
     __builtin_amdgcn_sched_barrier(0);
     load_fw(rnext, qa_, qb_);
     MPCQP_PHASE(4);
@@ -1622,15 +1653,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void co
 #endif
 }
 
-template <int NT, bool EXACT, bool X3>
+template <int NT, bool EXACT, bool X3, bool GAM = false>
 static int launch_condense_mfma_fh3(const CondenseArgs<float>& a, hipStream_t st) {
   const size_t bytes = (size_t)a.N * 64 * sizeof(float);
   if (bytes > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)condense_mfma_fh_kernel<NT, EXACT, X3>,
+    hipError_t e = hipFuncSetAttribute((const void*)condense_mfma_fh_kernel<NT, EXACT, X3, GAM>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(condense_mfma_fh)");
   }
-  hipLaunchKernelGGL((condense_mfma_fh_kernel<NT, EXACT, X3>), dim3(a.batch), dim3(kWave), bytes, st, a);
+  hipLaunchKernelGGL((condense_mfma_fh_kernel<NT, EXACT, X3, GAM>), dim3(a.batch), dim3(kWave), bytes, st, a);
   MPCQP_CHECK_LAUNCH("condense_mfma_fh_kernel");
   return MPCQP_OK;
 }
@@ -1641,6 +1672,7 @@ static int launch_condense_mfma_fh2(const CondenseArgs<float>& a, hipStream_t st
 }
 template <int NT>
 static int launch_condense_mfma_fh(const CondenseArgs<float>& a, hipStream_t st) {
+  if (a.Gam) return launch_condense_mfma_fh3<NT, false, false, true>(a, st);  // (generic)
   return (a.N % MPCQP_FH_PF == 0 && a.N % MPCQP_FH_PFF == 0) ? launch_condense_mfma_fh2<NT, true>(a, st)
                                                              : launch_condense_mfma_fh2<NT, false>(a, st);
 }
@@ -1687,7 +1719,7 @@ static int condense_mfma(const CondenseArgs<float>& a, hipStream_t st) {
     const char* e = getenv("MPCQP_CONDENSE_FH");
     return e ? atoi(e) : 1;
   }();
-  if (fh && !a.c && a.nx <= 12 && (a.nu == 1 || a.nu == 2 || a.nu == 4)) {
+  if (fh && !a.c && !a.F && !a.Phi && a.nx <= 12 && (a.nu == 1 || a.nu == 2 || a.nu == 4)) {
     if (nt <= 4) return launch_condense_mfma_fh<4>(a, st);
     if (nt <= 8) return launch_condense_mfma_fh<8>(a, st);
     if (nt <= 10) return launch_condense_mfma_fh<10>(a, st);

@@ -139,11 +139,14 @@ def test_condense_large_batch_pointwise(dev):
                                         (12, 4, 40, False), (7, 16, 16, True), (12, 4, 7, True),
                                         (9, 1, 33, True)])
 @pytest.mark.parametrize("drift", [True, False])
-def test_condense_fp32_mfma_all_outputs(dev, nx, nu, N, tv, drift):
+@pytest.mark.parametrize("outs", [("H", "F", "f", "Gam", "Phi", "xbar"), ("H", "f", "Gam", "xbar"),
+                                  ("H", "f")])
+def test_condense_fp32_mfma_all_outputs(dev, nx, nu, N, tv, drift, outs):
     """fp32 with 5 <= nx <= 15 runs condense_mfma_kernel (augmented-state
-    MFMA recursion; per-stage drift c_k) or, without drift for nx <= 12 and
-    nu <= 4, condense_mfma_fh_kernel (H rows from the forward MFMA's free
-    state slots): every output vs the fp64 oracle."""
+    MFMA recursion; per-stage drift c_k; the x0 columns F, Phi) or, without
+    drift, F and Phi for nx <= 12 and nu <= 4, condense_mfma_fh_kernel (H rows
+    from the forward MFMA's free state slots, f and xbar from a VALU mat-vec):
+    every requested output vs the fp64 oracle."""
     rng = np.random.default_rng(31 + 7 * nx + nu + N)
     batch = 3
     A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, tv, batch)
@@ -154,7 +157,7 @@ def test_condense_fp32_mfma_all_outputs(dev, nx, nu, N, tv, drift):
     out = batched.condense(_t(A, dev, f32), _t(B, dev, f32), _t(Q, dev, f32), _t(R, dev, f32),
                            _t(Qf, dev, f32), N, x0=_t(x0, dev, f32),
                            c=None if c is None else _t(c, dev, f32), tv=tv,
-                           outputs=("H", "F", "f", "Gam", "Phi", "xbar"))
+                           outputs=outs)
     torch.cuda.synchronize()
     A32, B32 = A.astype(np.float32).astype(np.float64), B.astype(np.float32).astype(np.float64)
     ref = [oc.condense(A32[b], B32[b], Q, R, Qf, N, x0=x0[b], c=None if c is None else c[b])

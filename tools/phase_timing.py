@@ -68,6 +68,9 @@ elif cfg == 55:
     reader = lib.mpcqp_debug_phase_cycles_condense
     reader.argtypes = [ctypes.c_void_p, ctypes.c_int]
     PHASES = ["backward W/What", "fw: loads+What", "fw: MFMA tiles", "fw: Gam/H epilogue", "fw: E tile", "", "", ""]
+    if os.environ.get("MPCQP_CONDENSE_FH", "1") != "0":  # condense_mfma_fh_kernel's phases
+        PHASES = ["backward", "fw: LDS What A, blend", "fw: MFMA tiles + xbar/f", "fw: H stores",
+                  "fw: next loads", "", "", ""]
     a = A(); a.batch = 32768; a.slots = 1; a.horizon = 0; a.reps = 1
     w = bench.CONFIGS["5"](a, torch.device("cuda"), 0)
     run = lambda: batched.condense(w.A[0], w.B[0], w.Q_t, w.R_t, w.Q_t, w.N, x0=w.X0_t[0],  # noqa: E731
