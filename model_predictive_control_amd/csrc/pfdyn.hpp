@@ -42,6 +42,25 @@ __device__ __forceinline__ void lds_copy3(float* dst, const float* s1, int n1, c
   }
 }
 
+// The same copy by LDS DMA (global_load_lds_dword: global memory straight
+// into LDS at M0 + 4 lane, no VGPR staging): every load of the whole copy is
+// in flight at once -- one HBM round trip per copy instead of one per
+// register batch -- then vmcnt(0).  The caller syncs before the LDS reads.
+__device__ __forceinline__ void lds_copy3_dma(float* dst, const float* s1, int n1, const float* s2,
+                                              int n2, const float* s3, int n3, int l) {
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  typedef __attribute__((address_space(1))) void* gptr_t;
+  const int cnt = n1 + n2 + n3;
+  for (int e0 = 0; e0 < cnt; e0 += kWave) {
+    const int e = e0 + l;
+    if (e < cnt) {
+      const float* p = e < n1 ? s1 + e : (e < n1 + n2 ? s2 + (e - n1) : s3 + (e - n1 - n2));
+      __builtin_amdgcn_global_load_lds((gptr_t)p, (lptr_t)(dst + e0), 4, 0, 0);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt untouched
+}
+
 __device__ __forceinline__ float bperm(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(lane << 2, __float_as_int(v)));
 }
@@ -90,7 +109,8 @@ __device__ __forceinline__ double group_sum(double v, int P) {
 // stages, visited forward 0..K-1 then backward K-1..0 (`loaded` = the
 // resident run; a horizon that fits one run is loaded once per kernel).
 // Measured: register prefetching of the next run (8-16 VGPRs) cost more in
-// spills and short runs than the round trips it hid.
+// spills and short runs than the round trips it hid; a run is now copied by
+// LDS DMA, all of it in flight at once (lds_copy3_dma).
 // FWD: the forward rollout only (X = x_1..x_N of z into the pool; w untouched)
 // RESIDENT: the whole horizon and the weights are already in the pool (an
 // earlier call loaded them, one run): no load code at all (register pressure)
@@ -131,9 +151,15 @@ __device__ __forceinline__ void dyn_residual(const PfDyn& d, int b, int n, int m
   // first LDS store
   auto load_run = [&](int r) __attribute__((always_inline)) {
     const int s0 = r * cap, S = run_len(r);
+#ifndef MPCQP_DYN_VGPR_COPY
+    lds_copy3_dma(ch, Ab + (tv ? (int64_t)s0 * sfA : 0), tv ? S * sfA : sfA,
+                  Bb + (tv ? (int64_t)s0 * sfB : 0), tv ? S * sfB : sfB,
+                  cb ? cb + (int64_t)s0 * nx : nullptr, cb ? S * nx : 0, l);
+#else  // (A/B: through VGPRs in register batches)
     lds_copy3<NXP >= 8 ? 8 : 16>(ch, Ab + (tv ? (int64_t)s0 * sfA : 0), tv ? S * sfA : sfA,
               Bb + (tv ? (int64_t)s0 * sfB : 0), tv ? S * sfB : sfB,
               cb ? cb + (int64_t)s0 * nx : nullptr, cb ? S * nx : 0, l);
+#endif
     loaded = r;
   };
   if (!RESIDENT && loaded < 0)
