@@ -1357,7 +1357,7 @@ void condense_mfma_kernel(CondenseArgs<float> a) {
 // twelve (X, W~, What).  LDS per instance: (What A)_k (4 x 12) and
 // What_k B_k + R (4 x 4) per stage, the footprint What had.
 #ifndef MPCQP_FH_PF
-#define MPCQP_FH_PF 8   // backward prefetch depth (stages)
+#define MPCQP_FH_PF 4   // backward prefetch depth (stages; 8 measured 0.6 % slower, 10 and 20 slower still)
 #endif
 #ifndef MPCQP_FH_PFF
 #define MPCQP_FH_PFF 4  // forward prefetch depth (stages)
@@ -1562,6 +1562,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void co
     const int blk0 = r * nu;
     const int ntact = ((r + 1) * nu + 15) >> 4;
     const int tlo = blk0 >> 4;  // tiles holding block r's columns: tlo..ntact-1
+    auto xchain = [&]() __attribute__((always_inline)) {
+      if (wantX) {
+        // position cl of the sum: xbar_{r+1}[sc] (state lanes), f_r[zb] (H rows)
+        float px = fmaf(aA[2], xv[2], fmaf(aA[1], xv[1], aA[0] * xv[0]));
+        // sum over the four lane groups: permlane16_swap of (v, v) leaves rows
+        // (0, 1) and (2, 3) of the two results holding (v.r0, v.r1) and
+        // (v.r2, v.r3) in some order, so their sum is the pair sum in every
+        // lane without a select; permlane32_swap then pairs the row pairs
+        {
+          const auto s1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(px), __float_as_uint(px), false, false);
+          px = __uint_as_float(s1[0]) + __uint_as_float(s1[1]);
+          const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(px), __float_as_uint(px), false, false);
+          px = __uint_as_float(s2[0]) + __uint_as_float(s2[1]);
+        }
+        bst(px, rf, zc ? fxo + 4 * blk0 : kOOB);
+        bst(px, rX, zc ? kOOB : fxo + 4 * r * nx);
+        int xs = xsrc;
+        asm volatile("" : "+v"(xs));  // (the three addresses are formed here, not held)
+#pragma unroll
+        for (int s = 0; s < 3; ++s)
+          xv[s] = __int_as_float(__builtin_amdgcn_ds_bpermute(xs + 4 * s, __float_as_int(px)));
+      }
+    };
+#ifdef MPCQP_FH_XFIRST
+    xchain();
+#endif
     MPCQP_PHASE(1);
     // K chunk 3 carries the input selectors on the tiles of block r: row
     // 4b + 3 of Gamma~_r is 1 in block r's column b, and the A operand's
@@ -1582,27 +1608,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void co
         for (int s = 0; s < 4; ++s) gB[t][s] = dd[s];
       }
     }
-    if (wantX) {
-      // position cl of the sum: xbar_{r+1}[sc] (state lanes), f_r[zb] (H rows)
-      float px = fmaf(aA[2], xv[2], fmaf(aA[1], xv[1], aA[0] * xv[0]));
-      // sum over the four lane groups: permlane16_swap of (v, v) leaves rows
-      // (0, 1) and (2, 3) of the two results holding (v.r0, v.r1) and
-      // (v.r2, v.r3) in some order, so their sum is the pair sum in every
-      // lane without a select; permlane32_swap then pairs the row pairs
-      {
-        const auto s1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(px), __float_as_uint(px), false, false);
-        px = __uint_as_float(s1[0]) + __uint_as_float(s1[1]);
-        const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(px), __float_as_uint(px), false, false);
-        px = __uint_as_float(s2[0]) + __uint_as_float(s2[1]);
-      }
-      bst(px, rf, zc ? fxo + 4 * blk0 : kOOB);
-      bst(px, rX, zc ? kOOB : fxo + 4 * r * nx);
-      int xs = xsrc;
-      asm volatile("" : "+v"(xs));  // (the three addresses are formed here, not held)
-#pragma unroll
-      for (int s = 0; s < 3; ++s)
-        xv[s] = __int_as_float(__builtin_amdgcn_ds_bpermute(xs + 4 * s, __float_as_int(px)));
-    }
+#ifndef MPCQP_FH_XFIRST
+    xchain();
+#endif
     MPCQP_PHASE(2);
     const int R = blk0 + g;  // the H row of this lane's register 3
     // packed row R from column cl; tile t adds the immediate 64 t.  Tiles
