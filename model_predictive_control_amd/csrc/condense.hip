@@ -1492,10 +1492,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void co
   // tile position 4g (state 3g) in this lane's row (+4 s: state 3g + s)
   float xv[3];
   const int xsrc = 4 * (16 * g + 4 * g);
-  // f_r[zb] (H-row lanes of group 0) at blk0 + zb, xbar_{r+1}[sc] (state
-  // lanes of group 0) at r nx + sc: one per-lane byte base (kOOB elsewhere),
-  // the lane class picks the buffer
-  const int fxo = (g == 0 && (zc ? zb < nu : sc < nx)) ? 4 * (zc ? zb : sc) : kOOB;
+  // f_r[zb] (H-row lanes of group 0) at blk0 + zb: the per-lane byte base
+  // (kOOB elsewhere); xbar_{r+1}[sc] (state lanes of group 0) at r nx + sc
+  const int fo = (g == 0 && zc && zb < nu) ? 4 * zb : kOOB;
   {
     const float* X0b = a.x0 ? a.x0 + (int64_t)b * a.sX0 : nullptr;
 #pragma unroll
@@ -1576,8 +1575,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void co
           const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(px), __float_as_uint(px), false, false);
           px = __uint_as_float(s2[0]) + __uint_as_float(s2[1]);
         }
-        bst(px, rf, zc ? fxo + 4 * blk0 : kOOB);
-        bst(px, rX, zc ? kOOB : fxo + 4 * r * nx);
+        bst(px, rf, fo, 4 * blk0);
+        if (a.xbar)  // (mpcqp_mpc_qp asks for none)
+          bst(px, rX, (g == 0 && !zc && sc < nx) ? 4 * sc : kOOB, 4 * r * nx);
         int xs = xsrc;
         asm volatile("" : "+v"(xs));  // (the three addresses are formed here, not held)
 #pragma unroll
@@ -1629,10 +1629,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void co
           }
         }
 #ifndef MPCQP_FH_NOSTORE
+        // the tile's displacement 64 t rides in the store's SGPR offset
         if (t < tlo)  // (a uniform branch: no per-lane test below the diagonal)
-          bst(d[3], rH, rowb + 64 * t);
+          bst(d[3], rH, rowb, 64 * t);
         else
-          bst(d[3], rH, col <= R ? rowb + 64 * t : kOOB);
+          bst(d[3], rH, col <= R ? rowb : kOOB, 64 * t);
 #else
         if (d[3] == 12345.f) bst(d[3], rH, 0);
 #endif

@@ -47,5 +47,10 @@ __device__ __forceinline__ float bld(rsrc_t r, int off) {
 __device__ __forceinline__ void bst(float v, rsrc_t r, int off) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
+// per-lane byte offset + a wave-uniform one (the instruction's SGPR soffset:
+// a compile-time or uniform displacement costs no VALU address arithmetic)
+__device__ __forceinline__ void bst(float v, rsrc_t r, int off, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, soff, 0);
+}
 
 }  // namespace mpcqp
