@@ -1,5 +1,7 @@
-"""Config-5 condensing alone (condense_mfma_kernel, B = 32,768, outputs H and
-f as in mpcqp_mpc_qp): time it, or run 5 launches for a rocprofv3 --pmc pass.
+"""Config-5 condensing alone (condense_mfma_fh_kernel, B = 32,768, outputs H
+and f as in mpcqp_mpc_qp): time it, or run 5 launches for a rocprofv3 --pmc
+pass.  With MPCQP_LIB pointing at an A/B build (tools/ab_build.sh; the
+MPCQP_FH_* timing-probe macros of condense.hip) it times that build.
 
     python tools/condense5_probe.py [pmc]
 """
