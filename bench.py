@@ -487,10 +487,12 @@ class Config3:
         cb = condense_bytes_survey(nx, nu, N, 4, True) * bsz
         cm = condense_bytes_per_instance(nx, nu, N, 4, tv=True, gam=True, drift=True) * bsz
         wf = sweep_flops_per_instance(n, 0) * bsz
-        # the z-space kernel reads H^-1 (n x n), s0, f, Gamma (m x n: every
-        # row is checked once at the end), the dynamics (A_k, B_k, c_k, x0)
-        # of the refinement, the shared bounds once; writes z, y, status
-        zb = (n * n + 2 * n + m * n + N * (nx * nx + nx * nu + nx) + nx + n + m + 1) * 4 * bsz
+        # the z-space kernel reads H^-1 (n x n), s0, f, Gamma packed (its
+        # lower block triangle, nx nu N(N+1)/2: the row normals), the dynamics
+        # (A_k, B_k, c_k, x0) of the refinement, the shared bounds once;
+        # writes z, y, status
+        gp = nx * nu * N * (N + 1) // 2
+        zb = (n * n + 2 * n + gp + N * (nx * nx + nx * nu + nx) + nx + n + m + 1) * 4 * bsz
         r_c = roof("condense_stream_kernel<float,4,2>", "hbm", cb, t_c, HBM_PEAK_GBS, "GB/s",
                    traffic.get("condense"), {"bytes_per_launch": cb, "bytes_moved_per_launch": cm,
                                              "bytes": "SURVEY 8(d)"})

@@ -455,6 +455,42 @@ int mpcqp_bicycle_sqp_step(int dtype, int batch, int N, double ts, const double*
                            void* stream);
 
 /*
+ * mpcqp_bicycle_sqp_solve: the whole SQP above -- up to max_iter iterations
+ * of linearise -> Hessian -> interior-point QP -> step per instance -- in ONE
+ * launch, one single-wave workgroup per instance (replaces session_4/
+ * main.py:115-116's per-step IPOPT call like the four-call iteration does;
+ * mpc.SqpSolver.solve).  Every instance stops at its own convergence: the
+ * launch lasts as long as the slowest instance's solve, not the sum over
+ * iterations of each iteration's slowest QP.  Arguments as
+ * mpcqp_bicycle_sqp_step (the SQP state U, y, pi, X, rho, kkt, mu, flags,
+ * fix in and out: a warm start continues from them) plus
+ *   hessian: MPCQP_SQP_HESS_GN (Gauss-Newton QPs; fix unused),
+ *            MPCQP_SQP_HESS_EXACT (the exact Lagrangian curvature after the
+ *            switch, projected per stage in PROJ mode: Q and R are the
+ *            projection's stage weights), MPCQP_SQP_HESS_RAW (never projected);
+ *   lam_u (optional, batch x N*2): the last QP's input-bound multipliers;
+ *   qp_status (optional, batch): the last QP's status word;
+ *   qp_max_iter: interior-point iterations per QP (<= 0: 25);
+ *   tol: the KKT tolerance (<= 0: 1e-9).
+ * The linearisation is mpcqp_bicycle_linearise's (FE or RK4).  The QP's
+ * horizon lives in LDS: N * 142 doubles <= 160 KB (N <= 144).  fp64.
+ * workspace: mpcqp_bicycle_sqp_solve_workspace() bytes (N * 90 doubles per
+ * instance).
+ */
+#define MPCQP_SQP_HESS_GN 0
+#define MPCQP_SQP_HESS_EXACT 1
+#define MPCQP_SQP_HESS_RAW 2
+size_t mpcqp_bicycle_sqp_solve_workspace(int batch, int N);
+int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts, const double* params,
+                            int integrator, int hessian, const void* x0, int64_t strideX0,
+                            const void* Q, const void* R, const void* Qf, const void* xlo,
+                            const void* xhi, int64_t strideXb, const void* lb, const void* ub,
+                            int64_t strideLb, void* U, void* y, void* pi, void* X, double* rho,
+                            double* kkt, double* mu, int32_t* flags, int32_t* fix, void* lam_u,
+                            int32_t* qp_status, int max_iter, int qp_max_iter, double tol,
+                            void* ws, size_t ws_bytes, void* stream);
+
+/*
  * The receding-horizon loop on device (rcracers.simulate(x0, dynamics,
  * n_steps, policy=controller), session_4/main.py:270-271; session4_sol.py:
  * 458,465), one step of it per call pair:

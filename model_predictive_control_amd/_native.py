@@ -27,6 +27,7 @@ SQP_DONE = 1
 SQP_EXACT = 2
 SQP_FAIL = 4
 SQP_PROJ = 8
+SQP_HESS = {"gauss-newton": 0, "exact": 1, "exact-raw": 2}  # MPCQP_SQP_HESS_*
 MODEL_FE = 0
 MODEL_RK4 = 1
 PLANT_FE = 0
@@ -98,6 +99,11 @@ SIGNATURES = {
     "mpcqp_bicycle_sqp_step": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _vp, _i64,
                                     _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _vp]),
+    "mpcqp_bicycle_sqp_solve_workspace": (ctypes.c_size_t, [_i, _i]),
+    "mpcqp_bicycle_sqp_solve": (_i, [_i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _i, _vp,
+                                     _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp,
+                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _d, _vp,
+                                     ctypes.c_size_t, _vp]),
     "mpcqp_bicycle_plant": (_i, [_i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _i, _vp, _vp,
                                  _i64, _vp, _vp, _vp]),
     "mpcqp_sqp_shift": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _vp]),

@@ -801,6 +801,42 @@ def bicycle_sqp_step(x0, U, Z, yq, piq, y, pi, X, state: dict, params, ts: float
     nat.check(rc, "mpcqp_bicycle_sqp_step")
 
 
+def bicycle_sqp_solve(x0, U, y, pi, X, state: dict, params, ts: float, Q, R, Qf, *,
+                      hessian: str = "exact", xlo=None, xhi=None, lb=None, ub=None,
+                      tol: float = 1e-9, max_iter: int = 60, qp_max_iter: int = 25,
+                      integrator: int = 0, lam_u=None, qp_status=None,
+                      ws: torch.Tensor | None = None) -> torch.Tensor:
+    """The whole device SQP, up to max_iter iterations per instance, in one
+    launch (include/mpcqp.h ``mpcqp_bicycle_sqp_solve``), in place on the SQP
+    state U (b, N, 2), y (b, N*4), pi (b, N, 4), X (b, N+1, 4) and ``state``
+    (rho, kkt, mu float64 (b,), flags int32 (b,), fix int32 (b, N)) -- the
+    state of ``bicycle_sqp_step``, so a solve continues from it.  hessian:
+    "exact", "exact-raw" or "gauss-newton".  lam_u (b, N*2) and qp_status
+    (b,): optional outputs of the last QP.  Returns the workspace (pass it
+    back as ``ws`` to reuse it)."""
+    b, N = int(U.shape[0]), int(U.shape[1])
+    xlo, xhi, sxb = _bound_pair(xlo, xhi, b, 4 * N, "xlo/xhi")
+    lb, ub, slb = _bound_pair(lb, ub, b, 2 * N, "lb/ub")
+    for name, t, shp, dt in (("U", U, (b, N, 2), torch.float64), ("y", y, (b, N * 4), torch.float64),
+                             ("pi", pi, (b, N, 4), torch.float64),
+                             ("X", X, (b, N + 1, 4), torch.float64),
+                             ("x0", x0, (b, 4), torch.float64)):
+        if tuple(t.shape) != shp or t.dtype != dt or not t.is_contiguous() or t.device != U.device:
+            raise ValueError(f"bicycle_sqp_solve: {name} must be a contiguous {dt} device tensor "
+                             f"of shape {shp}")
+    lib = _lib()
+    wsb = int(lib.mpcqp_bicycle_sqp_solve_workspace(b, N))
+    ws = _workspace(wsb, U.device, ws)
+    rc = lib.mpcqp_bicycle_sqp_solve(
+        nat.F64, b, N, float(ts), _bike_params(params), int(integrator), nat.SQP_HESS[hessian],
+        _ptr(x0), 4, _ptr(Q), _ptr(R), _ptr(Qf), _ptr(xlo), _ptr(xhi), sxb, _ptr(lb), _ptr(ub), slb,
+        _ptr(U), _ptr(y), _ptr(pi), _ptr(X), _ptr(state["rho"]), _ptr(state["kkt"]),
+        _ptr(state["mu"]), _ptr(state["flags"]), _ptr(state.get("fix")), _ptr(lam_u),
+        _ptr(qp_status), int(max_iter), int(qp_max_iter), float(tol), _ptr(ws), wsb, _stream())
+    nat.check(rc, "mpcqp_bicycle_sqp_solve")
+    return ws
+
+
 def bicycle_linearise(x0, U, params, ts: float, integrator: int = 0, out: tuple | None = None):
     """Rollout + linearisation of the prediction model (include/mpcqp.h
     ``mpcqp_bicycle_linearise``; integrator 0 = forward Euler, 1 = RK4):

@@ -1525,11 +1525,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void co
   auto load_fw = [&](int r, float (&ao)[3], float& bo) {
     const float* p = ap + r * astage;
     if constexpr (X3) {
-      typedef float f3 __attribute__((ext_vector_type(3)));
-      const f3 v = *reinterpret_cast<const f3*>(p);
-      ao[0] = v[0];
-      ao[1] = v[1];
-      ao[2] = v[2];
+      // exactly 12 bytes (global_load_dwordx3, 4-byte aligned): a vec3 type
+      // would be a 16-byte vector in the IR, one float past A's last row
+      struct F3 { float v[3]; } t;
+      __builtin_memcpy(&t, p, sizeof(F3));
+      ao[0] = t.v[0];
+      ao[1] = t.v[1];
+      ao[2] = t.v[2];
     } else {
 #pragma unroll
       for (int s = 0; s < 3; ++s) ao[s] = p[ao_[s]];

@@ -55,7 +55,7 @@ class MPCController:
                  max_iter: int = 200, tol: float = 1e-9, hessian: str = "exact",
                  integrator: str = "fe",
                  sqp_iters: int = 3, state_box: bool = True, dtype=torch.float64,
-                 device=None) -> None:
+                 device=None, fused: bool = True) -> None:
         self.N = N
         self.ts = ts
         # The prediction model is linearised on device (mpcqp_bicycle_rti),
@@ -111,7 +111,11 @@ class MPCController:
         self.bounds = dict(lbx=np.tile(self.lb_inputs, N), ubx=np.tile(self.ub_inputs, N),
                            lbg=np.tile(self.lb_states, N), ubg=np.tile(self.ub_states, N))
         self.sqp_iters = sqp_iters
+        # SQP mode: the whole solve in one launch (SqpSolver.solve) or one
+        # launch sequence per iteration over the batch (SqpSolver.iterate)
+        self.fused = fused
         self._warm = None
+        self._last = None
         self.last_status = None
         self.last_kkt = None
         self.last_iters = None
@@ -163,18 +167,28 @@ class MPCController:
                                                **self._box())
             self.last_lam_g = lam
             U = z.view(b, N, nu)
-        # IPOPT's "g" rows and "f" are those of the NLP at the returned inputs:
-        # the states of the prediction model's own rollout of U (not of the
-        # last linearisation), and the objective along it; the multipliers
-        # lam_x / lam_p follow from the adjoint along that rollout
-        Xn, lam_u, lam_0 = self._adjoint(X0, U, self.last_lam_g)
-        self.last_prediction = Xn[:, 1:].to(self.dtype)
-        self.last_lam_u = lam_u
-        self.last_lam_p = lam_0
-        self.last_cost = self._cost(X0, Xn[:, 1:], U)
+        # IPOPT's "g", "f", "lam_x" and "lam_p" are computed by solve() only
+        # (_nlp_terms): a raw batched call pays for the RTI steps alone
+        self._last = dict(X0=X0, U=U, y=self.last_lam_g, X=None)
         self._warm = torch.cat([U[:, 1:], U[:, -1:]], 1).contiguous()
         self.last_status = status
         return z, status
+
+    def _nlp_terms(self):
+        """IPOPT's result terms of the last solve_batch, on demand: "g" and
+        "f" are those of the NLP at the returned inputs -- the states of the
+        prediction model's own rollout (RTI: not the last linearisation's),
+        and the objective along it; lam_p (and lam_x in RTI mode) follow
+        from the adjoint along that rollout."""
+        t = self._last
+        X0, U, y = t["X0"], t["U"], t["y"]
+        Xn, lam_u, lam_0 = self._adjoint(X0, U, y)
+        X = Xn if t["X"] is None else t["X"]
+        self.last_prediction = X[:, 1:].to(self.dtype)
+        if self.mode == "rti":
+            self.last_lam_u = lam_u
+        self.last_lam_p = lam_0
+        self.last_cost = self._cost(X0, X[:, 1:], U)
 
     def _adjoint(self, X0, U, y):
         """The NLP's adjoint at inputs U (fp64, prediction model's rollout):
@@ -207,16 +221,17 @@ class MPCController:
         b = X0.shape[0]
         sqp = SqpSolver(self, b)
         sqp.reset(self._warm_start(b))
-        for _ in range(self.max_iter):
-            sqp.iterate(X0)
-            if bool((sqp.flags & SQP_DONE).all()):
-                break
+        if self.fused:
+            sqp.solve(X0, self.max_iter)
+        else:
+            for _ in range(self.max_iter):
+                sqp.iterate(X0)
+                if bool((sqp.flags & SQP_DONE).all()):
+                    break
         status = sqp.status()
-        self.last_prediction = sqp.X[:, 1:]
         self.last_lam_g = sqp.y
         self.last_lam_u = sqp.qp["lam_u"] if sqp.qp is not None else None
-        self.last_lam_p = self._adjoint(X0, sqp.U, sqp.y)[2]
-        self.last_cost = self._cost(X0, sqp.X[:, 1:], sqp.U)
+        self._last = dict(X0=X0, U=sqp.U, y=sqp.y, X=sqp.X)
         self.last_costates = sqp.pi
         self.last_kkt = sqp.kkt
         self.last_iters = sqp.iters()
@@ -258,6 +273,7 @@ class MPCController:
         single = xa.ndim == 1
         X0 = torch.as_tensor(xa.reshape(-1, self.nx), dtype=self.dtype, device=self.device)
         z, status = self.solve_batch(X0)
+        self._nlp_terms()
         zn = z.cpu().numpy()
         st = batched.status_code(status).cpu().numpy()
         b = X0.shape[0]
@@ -358,6 +374,7 @@ class SqpSolver:
         self.fix = torch.zeros((b, N), dtype=torch.int32, device=dev)
         self.qp = None
         self.box = ctl._box()
+        self.ws = None  # workspace of the one-launch solve
 
     def state(self) -> dict:
         # held inputs exist only for exact-Hessian QPs (the proximal term of
@@ -405,6 +422,26 @@ class SqpSolver:
                                  ctl.QN, xlo=box.get("xlo"), xhi=box.get("xhi"), lb=ctl.lbz,
                                  ub=ctl.ubz, tol=ctl.tol, qp_status=self.qp["status"],
                                  integrator=nat.MODEL_RK4 if ctl.integrator == "rk4" else nat.MODEL_FE)
+
+    def solve(self, X0, max_iter: int):
+        """Up to ``max_iter`` more iterations per instance in ONE launch
+        (mpcqp_bicycle_sqp_solve): each instance iterates until its own KKT
+        residual is below tol, in its own workgroup -- the same iterations as
+        ``iterate`` repeated (linearisation of mpcqp_bicycle_linearise), but
+        the launch lasts as long as the slowest instance's solve instead of
+        the sum over iterations of each iteration's slowest QP.  Continues
+        from the current state (reset() first for a fresh solve)."""
+        ctl = self.ctl
+        if self.qp is None or "ws_solve" not in self.qp:
+            b, N, dev = self.b, ctl.N, ctl.device
+            self.qp = {"lam_u": torch.zeros((b, N * 2), dtype=torch.float64, device=dev),
+                       "status": torch.zeros(b, dtype=torch.int32, device=dev), "ws_solve": True}
+        self.ws = batched.bicycle_sqp_solve(
+            X0, self.U, self.y, self.pi, self.X, self.state(), ctl.params, ctl.ts, ctl.Q, ctl.R,
+            ctl.QN, hessian=ctl.hessian, xlo=self.box.get("xlo"), xhi=self.box.get("xhi"),
+            lb=ctl.lbz, ub=ctl.ubz, tol=ctl.tol, max_iter=max_iter, qp_max_iter=self.QP_MAX_ITER,
+            integrator=nat.MODEL_RK4 if ctl.integrator == "rk4" else nat.MODEL_FE,
+            lam_u=self.qp["lam_u"], qp_status=self.qp["status"], ws=self.ws)
 
     def done(self):
         """Converged instances (KKT <= tol)."""

@@ -28,6 +28,26 @@ def _rand_plant(rng, nx, nu, N, tv, batch):
     return A, B, Q, R, Qf
 
 
+# output sets of the parity tests: (outputs, gam_packed)
+OUTPUT_SETS = {"all": (("H", "F", "f", "Gam", "Phi", "xbar"), False),
+               "noGam": (("H", "F", "f", "Phi", "xbar"), False),
+               "packed": (("H", "f", "Gam"), True)}
+
+
+def _condense_set(dev, dt, A, B, Q, R, Qf, N, x0, c, tv, outs):
+    """mpcqp_condense with the output set `outs` (OUTPUT_SETS); a packed
+    Gamma comes back unpacked, every output in fp64."""
+    names, packed = OUTPUT_SETS[outs]
+    out = batched.condense(_t(A, dev, dt), _t(B, dev, dt), _t(Q, dev, dt), _t(R, dev, dt),
+                           _t(Qf, dev, dt), N, x0=_t(x0, dev, dt),
+                           c=None if c is None else _t(c, dev, dt), tv=tv, outputs=names,
+                           gam_packed=packed)
+    torch.cuda.synchronize()
+    if packed:
+        out["Gam"] = batched.unpack_gam(out["Gam"], N, A.shape[-2], B.shape[-1])
+    return {k: v.double() for k, v in out.items()}
+
+
 def _check(out, ref, n, rtol):
     H = batched.unpack_lower(out["H"], n).cpu().numpy()
     for b, r in enumerate(ref):
@@ -43,16 +63,17 @@ def _check(out, ref, n, rtol):
 @pytest.mark.parametrize("nx,nu,N", [(1, 1, 1), (2, 1, 20), (3, 2, 7), (4, 2, 30), (5, 3, 6),
                                      (8, 2, 10), (12, 4, 12), (16, 1, 5)])
 @pytest.mark.parametrize("tv", [False, True])
-def test_condense_fp64_random(dev, nx, nu, N, tv):
+@pytest.mark.parametrize("outs", list(OUTPUT_SETS))
+def test_condense_fp64_random(dev, nx, nu, N, tv, outs):
+    """Every output set routes to its own kernel: with a dense Gamma to
+    condense_kernel, without one (nx <= 8) to condense_stream_kernel (F, Phi,
+    xbar with padding nx < NX, drift), packed Gamma to either."""
     rng = np.random.default_rng(100 * nx + 10 * nu + N + tv)
     batch = 5
     A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, tv, batch)
     x0 = rng.normal(size=(batch, nx))
     c = rng.normal(size=(batch, N, nx)) if tv else None
-    out = batched.condense(_t(A, dev), _t(B, dev), _t(Q, dev), _t(R, dev), _t(Qf, dev), N,
-                           x0=_t(x0, dev), c=None if c is None else _t(c, dev), tv=tv,
-                           outputs=("H", "F", "f", "Gam", "Phi", "xbar"))
-    torch.cuda.synchronize()
+    out = _condense_set(dev, torch.float64, A, B, Q, R, Qf, N, x0, c, tv, outs)
     ref = [oc.condense(A[b], B[b], Q, R, Qf, N, x0=x0[b], c=None if c is None else c[b])
            for b in range(batch)]
     _check(out, ref, N * nu, 1e-10)
@@ -98,21 +119,51 @@ def test_condense_known_answer_riccati(dev, golden):
         x = A @ x + B @ u
 
 
-@pytest.mark.parametrize("nx,nu,N", [(2, 1, 20), (4, 2, 30), (12, 4, 40)])
-def test_condense_fp32(dev, nx, nu, N):
+@pytest.mark.parametrize("nx,nu,N", [(2, 1, 20), (4, 2, 30), (12, 4, 40), (1, 1, 9), (3, 2, 12),
+                                     (8, 4, 8), (4, 1, 25)])
+@pytest.mark.parametrize("outs", list(OUTPUT_SETS))
+@pytest.mark.parametrize("drift", [False, True])
+def test_condense_fp32(dev, nx, nu, N, outs, drift):
     rng = np.random.default_rng(7 + nx)
     batch = 4
     A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, True, batch)
     A *= 0.8
     x0 = rng.normal(size=(batch, nx))
-    out = batched.condense(_t(A, dev, torch.float32), _t(B, dev, torch.float32),
-                           _t(Q, dev, torch.float32), _t(R, dev, torch.float32),
-                           _t(Qf, dev, torch.float32), N, x0=_t(x0, dev, torch.float32), tv=True,
-                           outputs=("H", "F", "f"))
-    torch.cuda.synchronize()
-    ref = [oc.condense(A[b], B[b], Q, R, Qf, N, x0=x0[b]) for b in range(batch)]
-    out = {k: v.double() for k, v in out.items()}
+    c = rng.normal(size=(batch, N, nx)) * 0.3 if drift else None
+    out = _condense_set(dev, torch.float32, A, B, Q, R, Qf, N, x0, c, True, outs)
+    A32, B32 = A.astype(np.float32).astype(np.float64), B.astype(np.float32).astype(np.float64)
+    ref = [oc.condense(A32[b], B32[b], Q, R, Qf, N, x0=x0[b], c=None if c is None else c[b])
+           for b in range(batch)]
     _check(out, ref, N * nu, 2e-5)
+
+
+@pytest.mark.parametrize("tv", [True, False])
+def test_condense_fh_operand_at_allocation_end(dev, tv):
+    """condense_mfma_fh_kernel's X3 path (nx % 3 == 0, config 5's nx = 12) loads
+    rows of A as 12-byte vectors: with A ending exactly at the end of its
+    allocation (and shared, stride 0, when not tv) the last instance's last
+    row must read no further than A's last element."""
+    rng = np.random.default_rng(91 + tv)
+    nx, nu, N, batch = 12, 4, 8, 3
+    A, B, Q, R, Qf = _rand_plant(rng, nx, nu, N, True, batch)
+    A = A * 0.8 if tv else A[0, 0] * 0.8
+    x0 = rng.normal(size=(batch, nx))
+    f32 = torch.float32
+    numel = A.size
+    # a block of whole 512-byte allocator units whose last element is A's last
+    total = -(-numel * 4 // 512) * 512 // 4
+    buf = torch.zeros(total, dtype=f32, device=dev)
+    At = buf[total - numel:].view(A.shape)
+    At.copy_(torch.as_tensor(A, dtype=f32))
+    Bt = _t(B if tv else B[0, 0], dev, f32)
+    out = batched.condense(At, Bt, _t(Q, dev, f32), _t(R, dev, f32), _t(Qf, dev, f32), N,
+                           x0=_t(x0, dev, f32), tv=tv, outputs=("H", "f"))
+    torch.cuda.synchronize()
+    A32 = A.astype(np.float32).astype(np.float64)
+    B32 = B.astype(np.float32).astype(np.float64)
+    ref = [oc.condense(A32[b] if tv else A32, B32[b] if tv else B32[0, 0], Q, R, Qf, N, x0=x0[b])
+           for b in range(batch)]
+    _check({k: v.double() for k, v in out.items()}, ref, N * nu, 2e-5)
 
 
 def test_condense_large_batch_pointwise(dev):

@@ -381,3 +381,83 @@ def test_rti_mode_result_mapping(golden):
     assert np.abs(lam_x + 2 * grad).max() < 1e-9 * (1 + np.abs(grad).max())
     lp = ocp.lam_p(x0, U, y)
     assert np.abs(np.asarray(sol["lam_p"]).reshape(-1) - lp).max() < 1e-9 * (1 + np.abs(lp).max())
+
+
+def _bench_like_x0(n, seed=20261015 + 6):
+    rng = np.random.default_rng(seed)
+    return np.stack([rng.uniform(-.8, .8, n), rng.uniform(-.4, .4, n), rng.uniform(-.5, .5, n),
+                     rng.uniform(-.2, .2, n)], -1)
+
+
+@pytest.mark.parametrize("hessian,integrator", [("exact", "fe"), ("gauss-newton", "fe"),
+                                                ("exact-raw", "fe"), ("exact", "rk4")])
+def test_one_launch_solve_equals_iteration(hessian, integrator):
+    """mpcqp_bicycle_sqp_solve (SqpSolver.solve: the whole SQP per instance in
+    one launch) runs the same iterations as SqpSolver.iterate repeated: the
+    same converged set, the same iteration count per instance and the same
+    inputs to rounding (the one-launch linearisation is mpcqp_bicycle_
+    linearise's, the iteration's FE path mpcqp_bicycle_rti: equal up to the
+    last bits).  Every Hessian mode and both prediction models."""
+    from model_predictive_control_amd.mpc import SqpSolver
+
+    iters = 40 if hessian != "gauss-newton" else 25
+    ctl = MPCController(30, 0.08, VehicleParameters(), tol=1e-9, hessian=hessian,
+                        integrator=integrator)
+    X0 = torch.as_tensor(_bench_like_x0(192), dtype=torch.float64, device="cuda")
+    out = {}
+    for mode in ("iterate", "solve"):
+        sqp = SqpSolver(ctl, X0.shape[0])
+        sqp.reset()
+        if mode == "solve":
+            sqp.solve(X0, iters)
+        else:
+            for _ in range(iters):
+                sqp.iterate(X0)
+        out[mode] = (sqp.U.reshape(X0.shape[0], -1).cpu().numpy(), sqp.done().cpu().numpy(),
+                     sqp.iters().cpu().numpy(), sqp.kkt.cpu().numpy())
+    Ui, di, ii, ki = out["iterate"]
+    Us, ds, is_, ks = out["solve"]
+    assert (ks[ds] <= 1e-9).all()
+    if hessian == "gauss-newton":
+        # linear convergence: few reach 1e-9 in 25 iterations, and one that
+        # reaches it in the last iteration may take one more on the other path
+        assert (di != ds).sum() <= 3, ((di != ds).sum(), di.sum(), ds.sum())
+        assert np.abs(Ui - Us).max() < 1e-6, np.abs(Ui - Us).max()
+        return
+    assert di.sum() >= 0.8 * di.size, di.sum()
+    assert (di == ds).mean() >= 0.99, (di != ds).sum()
+    both = di & ds
+    assert (ii[both] == is_[both]).mean() >= 0.98
+    assert np.abs(Ui[both] - Us[both]).max() < 1e-9
+
+
+def test_one_launch_solve_continues_from_its_state():
+    """Two launches of 6 + 34 iterations = one of 40 (the state U, y, pi, X,
+    rho, kkt, mu, flags, fix carries over; converged instances stay frozen)."""
+    from model_predictive_control_amd.mpc import SqpSolver
+
+    ctl = MPCController(30, 0.08, VehicleParameters(), tol=1e-9)
+    X0 = torch.as_tensor(_bench_like_x0(64, seed=5), dtype=torch.float64, device="cuda")
+    a, b = SqpSolver(ctl, 64), SqpSolver(ctl, 64)
+    a.reset()
+    b.reset()
+    a.solve(X0, 40)
+    b.solve(X0, 6)
+    b.solve(X0, 34)
+    assert torch.equal(a.U, b.U) and torch.equal(a.flags, b.flags) and torch.equal(a.kkt, b.kkt)
+
+
+def test_one_launch_solve_checks_arguments():
+    from model_predictive_control_amd import _native as nat
+    from model_predictive_control_amd.mpc import SqpSolver
+
+    ctl = MPCController(30, 0.08, VehicleParameters(), tol=1e-9)
+    sqp = SqpSolver(ctl, 4)
+    sqp.reset()
+    with pytest.raises(ValueError):
+        sqp.solve(torch.zeros((4, 3), dtype=torch.float64, device="cuda"), 5)
+    with pytest.raises((ValueError, nat.MpcqpError)):
+        batched.bicycle_sqp_solve(torch.zeros((4, 4), dtype=torch.float64, device="cuda"), sqp.U,
+                                  sqp.y, sqp.pi, sqp.X, sqp.state(), ctl.params, ctl.ts, ctl.Q,
+                                  ctl.R, ctl.QN, max_iter=5,
+                                  ws=torch.empty(16, dtype=torch.uint8, device="cuda"))

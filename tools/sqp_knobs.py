@@ -1,0 +1,75 @@
+"""One SQP configuration on the nlp bench's initial states and the NLP
+fixtures (GPU A/B tool): the knobs come from the environment (MPCQP_SQP_*,
+MPCQP_LIB for a variant build), so one process = one configuration.
+
+Prints one JSON line: converged counts within 20/30/45/60 iterations of the
+bench batch (both slots, 8192 x0), the mean iteration count, the largest
+KKT residual after 60, and the largest input deviation from the oracle
+optima of tests/golden/nlp_tail.npz and nlp_s4.npz (main.py controller).
+
+    MPCQP_SQP_GN_MAX=25 python tools/sqp_knobs.py --tag gn25
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from model_predictive_control_amd._native import SQP_DONE  # noqa: E402
+from model_predictive_control_amd.mpc import MPCController, SqpSolver  # noqa: E402
+from model_predictive_control_amd.parameters import VehicleParameters  # noqa: E402
+from tools.sqp_straggler import bench_x0  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+
+
+def run(ctl, X0, iters):
+    b = X0.shape[0]
+    x0 = torch.as_tensor(X0, dtype=torch.float64, device="cuda")
+    sqp = SqpSolver(ctl, b)
+    sqp.reset()
+    conv = torch.full((b,), -1, dtype=torch.int32, device="cuda")
+    for it in range(1, iters + 1):
+        sqp.iterate(x0)
+        d = sqp.done()
+        conv = torch.where(d & (conv < 0), torch.full_like(conv, it), conv)
+        if bool((sqp.flags & SQP_DONE).all()):
+            break
+    torch.cuda.synchronize()
+    return conv.cpu().numpy(), sqp.U.reshape(b, -1).cpu().numpy(), sqp.kkt.cpu().numpy()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", default="base")
+    ap.add_argument("--iters", type=int, default=60)
+    a = ap.parse_args()
+    ctl = MPCController(30, 0.08, VehicleParameters(), tol=1e-9)
+    X0 = bench_x0()
+    t = time.time()
+    conv, _, kkt = run(ctl, X0, a.iters)
+    dt = time.time() - t
+    ok = conv > 0
+    out = dict(tag=a.tag, n=int(conv.size), **{f"c{k}": int((ok & (conv <= k)).sum()) for k in (20, 30, 45, 60)},
+               mean_it=round(float(np.where(ok, conv, a.iters).mean()), 2), kkt_max=float(kkt.max()),
+               secs=round(dt, 2))
+    dev = 0.0
+    g = np.load(os.path.join(GOLD, "nlp_tail.npz"))
+    c2, U2, _ = run(ctl, g["x0"], 200)
+    tail = np.abs(U2 - g["U"]).max(1)
+    g4 = np.load(os.path.join(GOLD, "nlp_s4.npz"))
+    c3, U3, _ = run(ctl, g4["main_x0"], 200)
+    s4 = np.abs(U3 - g4["main_U"]).max(1)
+    dev = max(float(tail.max()), float(s4.max()))
+    out.update(fixture_dev=dev, tail_bad=int((tail > 1e-7).sum()), s4_bad=int((s4 > 1e-7).sum()),
+               fixture_iters=[int(v) for v in np.concatenate([c2, c3])])
+    print("KNOB", json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

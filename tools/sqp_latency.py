@@ -1,0 +1,73 @@
+"""Per-instance timing of the one-launch SQP (mpcqp_bicycle_sqp_solve) on the
+nlp bench's initial states (GPU tool): the kernel records, per instance,
+s_memrealtime ticks in all and in the QPs, interior-point iterations and SQP
+iterations (the workspace's stats region).  Prints the launch time, the
+distribution of per-instance solve times, the time per interior-point
+iteration and the slowest instances.
+
+    python tools/sqp_latency.py [--iters 60] [--batch 4096]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from model_predictive_control_amd.mpc import MPCController, SqpSolver  # noqa: E402
+from model_predictive_control_amd.parameters import VehicleParameters  # noqa: E402
+from tools.sqp_straggler import bench_x0  # noqa: E402
+
+TICK_US = 0.01  # s_memrealtime runs at 100 MHz
+
+
+def stats_of(sqp, b, N):
+    """The kernel's per-instance stats (int64 x 4) from the solve workspace:
+    after N*90 + 4 doubles per instance of stage data and outputs."""
+    off = b * N * 90 + b * 4
+    return sqp.ws.view(torch.float64)[off:off + 4 * b].view(torch.int64).view(b, 4).cpu().numpy()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=60)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--hessian", default="exact")
+    a = ap.parse_args()
+    N = 30
+    ctl = MPCController(N, 0.08, VehicleParameters(), tol=1e-9, hessian=a.hessian)
+    X0 = bench_x0(a.batch, 1)
+    x0 = torch.as_tensor(X0, dtype=torch.float64, device="cuda")
+    b = X0.shape[0]
+    sqp = SqpSolver(ctl, b)
+    for rep in range(2):
+        sqp.reset()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        sqp.solve(x0, a.iters)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+    st = stats_of(sqp, b, N)
+    tot, tqp, ipm, its = (st[:, i].astype(float) for i in range(4))
+    ok = sqp.done().cpu().numpy()
+    per_ipm = tqp / np.maximum(ipm, 1) * TICK_US
+    per_sqp_other = (tot - tqp) / np.maximum(its, 1) * TICK_US
+    q = lambda v: [round(float(np.percentile(v, p)), 1) for p in (50, 90, 99, 100)]  # noqa: E731
+    print(json.dumps(dict(launch_ms=round(dt * 1e3, 2), converged=int(ok.sum()),
+                          inst_us_p50_90_99_max=q(tot * TICK_US),
+                          ipm_iter_us_p50_90_99_max=q(per_ipm),
+                          sqp_overhead_us_per_iter=q(per_sqp_other),
+                          ipm_iters_per_sqp_iter_mean=round(float(ipm.sum() / its.sum()), 2),
+                          sqp_iters_mean=round(float(its.mean()), 2),
+                          sum_inst_ms=round(float(tot.sum()) * TICK_US / 1e3, 1))), flush=True)
+    for i in np.argsort(-tot)[:8]:
+        print(json.dumps(dict(inst=int(i), us=round(tot[i] * TICK_US, 1), qp_us=round(tqp[i] * TICK_US, 1),
+                              ipm_iters=int(ipm[i]), sqp_iters=int(its[i]), ok=bool(ok[i]))), flush=True)
+
+
+if __name__ == "__main__":
+    main()
