@@ -765,7 +765,7 @@ class ConfigNLP:
     dname = "f64"
     default_batch = 4096
     default_slots = 2
-    default_sqp_iters = 60
+    default_sqp_iters = 150  # a cap per instance: each stops at its own convergence
     default_steps = (5, 1)  # (steps, warmup) when not given: one step is ~30 SQP iterations
 
     def __init__(self, args, dev, rank):
@@ -776,7 +776,8 @@ class ConfigNLP:
         self.N, self.ts = args.horizon or 30, 0.08
         self.iters = args.sqp_iters
         bsz, S = args.batch, args.slots
-        self.ctl = MPCController(self.N, self.ts, VehicleParameters(), tol=1e-9)
+        self.ctl = MPCController(self.N, self.ts, VehicleParameters(), tol=1e-9,
+                                 fused=not args.sqp_iterate)
         self.sqp = SqpSolver(self.ctl, bsz)
         rng = np.random.default_rng(20261015 + 6 + 1000 * rank)
         self.X0 = np.stack([rng.uniform(-.8, .8, (S, bsz)), rng.uniform(-.4, .4, (S, bsz)),
@@ -797,8 +798,11 @@ class ConfigNLP:
     def step(self, s):
         sqp = self.sqp
         sqp.reset()
-        for _ in range(self.iters):
-            sqp.iterate(self.X0_t[s])
+        if self.ctl.fused:  # one launch: every instance iterates to its own convergence
+            sqp.solve(self.X0_t[s], self.iters)
+        else:
+            for _ in range(self.iters):
+                sqp.iterate(self.X0_t[s])
         self.Z[s].copy_(sqp.U.view(self.args.batch, -1))
         self.ST[s].copy_(sqp.status())
         self.KKT[s].copy_(sqp.kkt)
@@ -814,6 +818,52 @@ class ConfigNLP:
         return int(sum(ok[k % S] for k in range(steps)))
 
     def kernels(self, traffic):
+        """The one-launch solve (sqp_solve_kernel, mpcqp_bicycle_sqp_solve)
+        timed on its stream by HIP events over R launches of slot 0, and the
+        kernel's own per-instance clocks (s_memrealtime: solve time, time in
+        the QPs, interior-point iterations, SQP iterations, warm-polished QPs)
+        for the roofline's flop count and the latency profile.  With
+        --sqp-iterate: one iteration's four launches timed separately."""
+        from model_predictive_control_amd.mpc import SqpSolver
+
+        R = self.args.reps
+        sqp, ctl, N, bsz = self.sqp, self.ctl, self.N, self.args.batch
+        x0 = self.X0_t[0]
+        kkt_final, done_final = float(self.KKT[0].max()), self.ST[0].clone()
+        extra = {"kkt_max": kkt_final,
+                 "converged_frac": float((batched.status_code(done_final) == 0).double().mean())}
+        if not ctl.fused:
+            return self._kernels_iterate(traffic, extra)
+        t_s = time_kernel(lambda: self.step(0), max(2, R // 4), self.dev)
+        st = sqp.ws.view(torch.float64)[bsz * N * 90 + bsz * 4:][:4 * bsz].view(torch.int64) \
+            .view(bsz, 4).cpu().numpy().astype(np.float64)
+        tot, tqp, ipm = st[:, 0] * 0.01, st[:, 1] * 0.01, st[:, 2]  # us (100 MHz ticks)
+        its = (st[:, 3].astype(np.int64) & 0xFFFFFFFF).astype(np.float64)
+        hits = (st[:, 3].astype(np.int64) >> 32).astype(np.float64)
+        # algorithmic fp64 flops of one interior-point iteration per stage
+        # (nx = 4, nu = 2): Riccati factorisation ~270 FMA, residuals and
+        # gradients ~90, predictor / corrector sweeps ~180 -> ~540 FMA
+        flops = 2 * 540 * N * float(ipm.sum())
+        pct = lambda v: [round(float(np.percentile(v, q)), 1) for q in (50, 90, 99, 100)]  # noqa: E731
+        r_i = roof("sqp_solve_kernel (whole SQP per instance)", "valu-fp64", flops, t_s,
+                   FP64_PEAK_TFS, "TFLOP/s", traffic.get("sqp_solve"),
+                   {"flops_per_launch": flops, "avg_launch_us": round(t_s * 1e3, 2),
+                    "note": "one single-wave workgroup per instance runs its SQP to convergence "
+                            "(QP: interior point on one DPP quad, horizon in LDS; linearisation, "
+                            "Hessian and line search one lane per stage); flops = 1080 per stage "
+                            "per interior-point iteration summed over the instances' own counts "
+                            "(warm polishes, Hessians and line searches not counted): latency-bound"})
+        extra.update({
+            "kernel_us": {"sqp_solve": round(t_s * 1e3, 2)},
+            "instance_us_p50_p90_p99_max": pct(tot),
+            "qp_time_share": round(float(tqp.sum() / tot.sum()), 3),
+            "ipm_iters_per_sqp_iter": round(float(ipm.sum() / max(1.0, its.sum())), 2),
+            "warm_polished_qp_frac": round(float(hits.sum() / max(1.0, its.sum())), 3),
+            "sqp_iters_mean": round(float(its.mean()), 2), "sqp_iters_max": int(its.max()),
+            "sum_instance_ms": round(float(tot.sum()) / 1e3, 1)})
+        return r_i, {}, extra
+
+    def _kernels_iterate(self, traffic, extra):
         """One SQP iteration's launches timed separately, on the state of slot
         0 after 3 iterations from U = 0 (every instance still iterating): the
         interior point as SqpSolver runs it (STRICT, QP_MAX_ITER), no skip."""
@@ -822,7 +872,6 @@ class ConfigNLP:
         R = self.args.reps
         sqp, ctl, N, bsz = self.sqp, self.ctl, self.N, self.args.batch
         x0 = self.X0_t[0]
-        kkt_final, done_final = float(self.KKT[0].max()), self.ST[0].clone()
         sqp.reset()
         for _ in range(3):
             sqp.iterate(x0)
@@ -846,9 +895,6 @@ class ConfigNLP:
         t_i = time_kernel(ipm, R, self.dev)
         torch.cuda.synchronize()
         its = ((qp["status"] >> 8) & 0xFFFF).double()
-        # algorithmic fp64 flops of one interior-point iteration per stage
-        # (nx = 4, nu = 2): Riccati factorisation ~270 FMA, residuals and
-        # gradients ~90, predictor / corrector sweeps ~180 -> ~540 FMA
         flops = 2 * 540 * N * float(its.sum())
         r_i = roof("ipm_quad_kernel<double,1>", "valu-fp64", flops, t_i,
                    FP64_PEAK_TFS, "TFLOP/s", traffic.get("ipm"),
@@ -858,11 +904,9 @@ class ConfigNLP:
                             "LDS (four per CU, one single-wave workgroup each): latency/LDS-"
                             "bound; flops = 1080 per stage per IPM iteration "
                             "summed over the instances' own iteration counts, polish not counted"})
-        extra = {"kernel_us": {"bicycle_rti": round(t_r * 1e3, 2),
-                               "bicycle_hessian": round(t_h * 1e3, 2),
-                               "mpc_ipm": round(t_i * 1e3, 2)},
-                 "kkt_max": kkt_final,
-                 "converged_frac": float((batched.status_code(done_final) == 0).double().mean())}
+        extra["kernel_us"] = {"bicycle_rti": round(t_r * 1e3, 2),
+                              "bicycle_hessian": round(t_h * 1e3, 2),
+                              "mpc_ipm": round(t_i * 1e3, 2)}
         return r_i, {}, extra
 
     def check(self):
@@ -923,7 +967,8 @@ class ConfigLoop:
         self.N, self.T = args.horizon or 30, args.loop_steps
         self.units_per_step = self.T
         bsz, S = args.batch, args.slots
-        self.ctl = MPCController(self.N, 0.08, VehicleParameters(), tol=1e-9)
+        self.ctl = MPCController(self.N, 0.08, VehicleParameters(), tol=1e-9,
+                                 fused=not args.sqp_iterate)
         self.loop = ClosedLoop(self.ctl, plant="fe", iters_per_step=args.sqp_iters, graph=False)
         rng = np.random.default_rng(20261015 + 7 + 1000 * rank)
         self.X0 = np.stack([rng.uniform(-.8, .8, (S, bsz)), rng.uniform(-.4, .4, (S, bsz)),
@@ -967,12 +1012,66 @@ class ConfigLoop:
         return int(sum(ok[k % S] for k in range(steps)))
 
     def kernels(self, traffic):
+        """Per-kernel time of one warm-started sample (the second of slot 0's
+        episode, replayed from a snapshot of the state before it) on HIP
+        events: the controller's SQP (sqp_solve_kernel; with --sqp-iterate the
+        four launches per iteration), the plant and the shift; the roofline
+        of the SQP kernel from its own interior-point iteration counts."""
         b = self.bufs[0]
         extra = {"success_frac_per_sample": float(b["success"].double().mean()),
                  "episodes_all_converged_frac": float(b["success"].all(0).double().mean()),
                  "iters_per_sample_mean": float(b["iters"].double().mean()),
                  "iters_per_sample_max": int(b["iters"].max())}
-        return None, {}, extra
+        if self.T < 2:
+            return None, {}, extra
+        R, N, bsz, loop = self.args.reps, self.N, self.args.batch, self.loop
+        b["xs"][0].copy_(self.X0_t[0])
+        loop._reset(b)
+        loop._step(b, 0)
+        sqp = b["sqp"]
+        keys = ("U", "y", "pi", "X", "rho", "kkt", "mu", "flags", "fix")
+        snap = {k: getattr(sqp, k).clone() for k in keys}
+        xs1 = b["xs"][1].clone()
+
+        def restore():
+            for k in keys:
+                getattr(sqp, k).copy_(snap[k])
+            b["xs"][1].copy_(xs1)
+
+        def sample_mpc():
+            restore()
+            loop._mpc(b, 1)
+
+        def plant_shift():
+            restore()
+            loop._step_tail(b, 1)
+
+        t_m = time_kernel(sample_mpc, R, self.dev)
+        t_r = time_kernel(restore, R, self.dev)
+        t_p = time_kernel(plant_shift, R, self.dev) - t_r
+        extra["kernel_us"] = {"mpc_solve": round((t_m - t_r) * 1e3, 2),
+                              "plant_and_shift": round(t_p * 1e3, 2),
+                              "state_restore (timing harness)": round(t_r * 1e3, 2)}
+        if not self.ctl.fused:
+            return None, {}, extra
+        sample_mpc()
+        torch.cuda.synchronize()
+        st = sqp.ws.view(torch.float64)[bsz * N * 90 + bsz * 4:][:4 * bsz].view(torch.int64) \
+            .view(bsz, 4).cpu().numpy().astype(np.float64)
+        tot, ipm = st[:, 0] * 0.01, st[:, 2]
+        its = (st[:, 3].astype(np.int64) & 0xFFFFFFFF).astype(np.float64)
+        flops = 2 * 540 * N * float(ipm.sum())
+        r = roof("sqp_solve_kernel (warm-started sample)", "valu-fp64", flops, t_m - t_r,
+                 FP64_PEAK_TFS, "TFLOP/s", traffic.get("sqp_solve"),
+                 {"flops_per_launch": flops,
+                  "note": "one warm-started controller call of the batch: the whole SQP per "
+                          "instance in one workgroup (interior point on one DPP quad); flops = "
+                          "1080 per stage per interior-point iteration: latency-bound"})
+        extra.update({"sample_instance_us_p50_p99_max": [round(float(np.percentile(tot, q)), 1)
+                                                         for q in (50, 99, 100)],
+                      "sample_sqp_iters_mean": round(float(its.mean()), 2),
+                      "sample_ipm_iters_per_sqp_iter": round(float(ipm.sum() / max(1.0, its.sum())), 2)})
+        return r, {}, extra
 
     def check(self):
         """Device episode of 2 instances against the host loop mpc.simulate
@@ -1025,6 +1124,9 @@ def main():
                          "MPCController.solve), loop (on-device receding-horizon loop)")
     ap.add_argument("--sqp-iters", type=int, default=0,
                     help="nlp: SQP iterations per solve (default 60); loop: per sample (12)")
+    ap.add_argument("--sqp-iterate", action="store_true",
+                    help="nlp / loop: one launch sequence per SQP iteration over the batch "
+                         "(SqpSolver.iterate) instead of the one-launch solve")
     ap.add_argument("--loop-steps", type=int, default=0,
                     help="loop / 2loop: closed-loop steps per episode (default 20 / 50)")
     ap.add_argument("--gather", action="store_true",

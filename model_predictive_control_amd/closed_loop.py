@@ -33,9 +33,11 @@ PLANTS = {"fe": nat.PLANT_FE, "rk4": nat.PLANT_RK4, "exact": nat.PLANT_RK4_SUB}
 class ClosedLoop:
     """Batched closed loop of ``controller`` on a kinematic-bicycle plant.
 
-    ``controller.mode == "sqp"``: each step runs ``iters_per_step`` SQP
-    iterations from the shifted previous solution (instances that reach the
-    KKT tolerance earlier are frozen by the step kernel), the first step --
+    ``controller.mode == "sqp"``: each step runs up to ``iters_per_step`` SQP
+    iterations from the shifted previous solution (with ``controller.fused``
+    in one launch, ``mpcqp_bicycle_sqp_solve``, each instance stopping at its
+    own convergence; otherwise one launch sequence per iteration, converged
+    instances frozen by the step kernel), the first step --
     a cold start from U = 0 -- ``iters_first`` (default: the controller's
     ``max_iter``, at most 60); ``"rti"``: each step runs the controller's
     ``sqp_iters`` linearise + QP steps.
@@ -83,15 +85,23 @@ class ClosedLoop:
             sqp.X[:, 1:].copy_(X)
             s["success"][t].copy_(batched.status_code(st) == 0)
             return
-        for _ in range(self.iters_first if t == 0 else self.iters):
-            sqp.iterate(x0)
+        n = self.iters_first if t == 0 else self.iters
+        if ctl.fused:  # every instance iterates to its own convergence, one launch
+            sqp.solve(x0, n)
+        else:
+            for _ in range(n):
+                sqp.iterate(x0)
         s["success"][t].copy_(sqp.done())
         s["iters"][t].copy_(sqp.iters())
 
     def _step(self, s, t):
+        self._mpc(s, t)
+        self._step_tail(s, t)
+
+    def _step_tail(self, s, t):
+        """The ControllerLog record, the plant and the warm-start shift of step t."""
         ctl = self.ctl
         b = s["sqp"].b
-        self._mpc(s, t)
         sqp = s["sqp"]
         # ControllerLog of the step: [x_t; predicted states], the input plan
         s["state_prediction"][t].copy_(sqp.X)

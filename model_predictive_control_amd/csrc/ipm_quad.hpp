@@ -327,8 +327,11 @@ MPCQP_QD void forward_q(const W& at, int N, int i, Body&& body) {
 // ------------------------------------------------------------- polish
 // The polish of ipm_lane.hpp (see there), lane i owning state comp i and
 // (i < 2) input comp i.
+// warm: the active set is the one GA already holds (the previous QP's polish,
+// solve_quad's warm start) and the multipliers start at 0; otherwise it is
+// guessed from the interior-point iterate (lambda > slack) with its duals.
 template <typename T, class W>
-MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i) {
+MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i, bool warm = false) {
   const int N = a.N;
   const bool ou = i < NU;
   for (int k = 0; k < N; ++k) {
@@ -338,13 +341,16 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i) {
       if (part == 1 && !ou) continue;
       const int j = part == 0 ? NU + i : i;
       const double vj = part == 0 ? at.r(k, L::X) : at.r(k, L::U);
-      const double lo = at(k, L::LO + j), hi = at(k, L::HI + j);
-      const double l = at(k, L::LL + j), u = at(k, L::LU + j);
-      const double rl = fin(lo) ? l / (vj - lo) : 0.0;
-      const double ru = fin(hi) ? u / (hi - vj) : 0.0;
-      const double act = (ru > 1.0 && ru >= rl) ? 1.0 : ((rl > 1.0) ? -1.0 : 0.0);
-      at(k, L::GA + j) = act;
-      const double y = act > 0.0 ? u : (act < 0.0 ? -l : 0.0);
+      double y = 0.0;
+      if (!warm) {
+        const double lo = at(k, L::LO + j), hi = at(k, L::HI + j);
+        const double l = at(k, L::LL + j), u = at(k, L::LU + j);
+        const double rl = fin(lo) ? l / (vj - lo) : 0.0;
+        const double ru = fin(hi) ? u / (hi - vj) : 0.0;
+        const double act = (ru > 1.0 && ru >= rl) ? 1.0 : ((rl > 1.0) ? -1.0 : 0.0);
+        at(k, L::GA + j) = act;
+        y = act > 0.0 ? u : (act < 0.0 ? -l : 0.0);
+      }
       if (part == 1) { at.r(k, L::DU) = vj; at.r(k, L::DUA) = y; }
       else { at.r(k, L::DX) = vj; at.r(k, L::DXA) = y; }
     }
@@ -474,13 +480,18 @@ MPCQP_QD void emit_q(const Args<T>& a, int b, const W& at, int i, bool polished,
 
 // One instance on the four lanes of a quad (i = lane & 3), workspace slice W
 // (LD instances interleaved).  Requires nx <= 4, nu <= 2.
+// warm (the one-launch SQP, sqp_solve.hip): the previous QP of this
+// instance ended polished and its active set is still in W's GA fields; the
+// QP is first polished on that active set from the start point, and the
+// interior point runs only if that is not a certified vertex.  Returns true
+// when the QP ended polished (its active set is then in GA for the next one).
 template <typename T, int LD>
-MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
+MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) {
   const int i = (int)(threadIdx.x & 3);
   const WsQ<LD> at(W, i);
   const bool ou = i < NU;
   const int N = a.N, nx = a.nx, nu = a.nu;
-  if (a.skip && (a.skip[b] & a.skip_mask)) return;
+  if (a.skip && (a.skip[b] & a.skip_mask)) return false;
   const double x0i = i < nx ? (double)a.x0[(int64_t)b * a.sX0 + i] : 0.0;
 
   // ---------------------------------------------------------------- start
@@ -557,6 +568,10 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
     }
   }
   const double mcount = qsum(mc);
+  if (warm && mcount > 0.0 && polish_q<T>(a, at, i, x0i, true)) {
+    emit_q<T>(a, b, at, i, true, MPCQP_STATUS_OPTIMAL, 0);
+    return true;
+  }
 
   double alpha = 0.0, sigmu = 0.0;
   double mu_pol = a.mu_polish;
@@ -644,13 +659,13 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
     const double mu = mcount > 0.0 ? qsum(musum) / mcount : 0.0;
     if (!fin(rstat) || !fin(rdyn) || !fin(mu)) {
       emit_q<T>(a, b, at, i, false, MPCQP_STATUS_NONFINITE, it);
-      return;
+      return false;
     }
     if (!pd) {
       dreg = dreg > 0.0 ? 8.0 * dreg : (dlast > 0.0 ? dlast : 1e-4);
       if ((a.strict > 0 && ++ncorr > a.strict) || dreg > 1e12 || it >= max_iter) {
         emit_q<T>(a, b, at, i, false, MPCQP_STATUS_NOT_CONVEX, it);
-        return;
+        return false;
       }
       alpha = 0.0;
       continue;
@@ -664,19 +679,19 @@ MPCQP_QD void solve_quad(const Args<T>& a, int b, double* W) {
         rdyn <= a.tol_polish) {
       if (polish_q<T>(a, at, i, x0i)) {
         emit_q<T>(a, b, at, i, true, MPCQP_STATUS_OPTIMAL, it);
-        return;
+        return true;
       }
       mu_pol *= 1e-2;
       alpha = 0.0;
       if (conv || it >= max_iter) {
         emit_q<T>(a, b, at, i, false, conv ? MPCQP_STATUS_OPTIMAL : MPCQP_STATUS_MAXITER, it);
-        return;
+        return false;
       }
       continue;
     }
     if (conv || it >= max_iter) {
       emit_q<T>(a, b, at, i, false, conv ? MPCQP_STATUS_OPTIMAL : MPCQP_STATUS_MAXITER, it);
-      return;
+      return false;
     }
 
     // ========================================== pass 2: forward predictor

@@ -285,37 +285,64 @@ __device__ inline Merit merit_at(const SqpArgs& a, int64_t b, double alpha) {
   return m;
 }
 
+// The QP of instance b failed (not converged within its budget, or non-
+// convex beyond the inertia correction with the unprojected Hessian): no step.
+// An exact-Hessian iteration raises the damping mu (x4, at least kMuFloor),
+// which changes the next QP; a Gauss-Newton QP would be rebuilt unchanged, so
+// kSqpMaxFails failures in a row stop the instance with the QP's status
+// (never OPTIMAL).  Returns false (nothing written) when the QP succeeded.
+__device__ __forceinline__ bool sqp_qp_failed(const SqpArgs& a, int64_t b, int fl) {
+  if (!a.qp_status || (a.qp_status[b] & 0xFF) == MPCQP_STATUS_OPTIMAL) return false;
+  const int iters = ((fl >> 8) & 0xFFFF) + 1;
+  const int fails = ((fl >> 24) & 0xF) + 1;
+  const int code = a.qp_status[b] & 0x7;
+  if ((fl & kSqpExact) && !(fl & kSqpProj) && a.proj_steps > 0) {
+    // the exact curvature made the QP fail (non-convex): the projected one
+    // next (mpcqp_bicycle_hessian_convex; a caller of the plain
+    // mpcqp_bicycle_hessian gets the damping below at the next failure)
+    a.flags[b] = (iters << 8) | kSqpExact | kSqpProj | (a.proj_steps << 24);
+  } else if (fl & kSqpExact) {
+    a.mu[b] = fmax(4.0 * a.mu[b], kMuFloor);
+    a.flags[b] = (iters << 8) | (fl & (kSqpExact | kSqpProj | (0xF << 24)));
+  } else if (fails >= kSqpMaxFails) {
+    a.flags[b] = (iters << 8) | kSqpDone | kSqpFail | (code << 28);
+  } else {
+    a.flags[b] = (iters << 8) | (fails << 24);
+  }
+  return true;
+}
+
+// After a step of length alpha with KKT residual r at the new point: the
+// damping mu, the Hessian mode (the exact Hessian once r < sw or after gn_max
+// iterations, sticky), the projected-curvature countdown, the watchdog count,
+// DONE below tol; rho and kkt stored.
+__device__ __forceinline__ void sqp_finish(const SqpArgs& a, int64_t b, int fl, double alpha,
+                                           double r, double rho, bool force, int wd) {
+  if (fl & kSqpExact) {
+    double mu = a.mu[b];
+    mu = alpha == 1.0 ? (mu > 4e-12 ? a.mu_dec * mu : 0.0) : fmax(4.0 * mu, kMuFloor);
+    a.mu[b] = mu;
+  }
+  const int iters = ((fl >> 8) & 0xFFFF) + 1;
+  const bool exact = (fl & kSqpExact) || r < a.sw || iters >= a.gn_max;  // sticky
+  // projected curvature: count full steps down, then back to the exact one
+  int pc = (fl & kSqpProj) ? ((fl >> 24) & 0xF) : 0;
+  if (pc > 0 && alpha == 1.0) --pc;
+  const int wdn = (force || alpha == 1.0) ? 0 : (wd < 15 ? wd + 1 : 15);
+  fl = (iters << 8) | (r <= a.tol ? kSqpDone : 0) | (exact ? kSqpExact : 0) |
+       (pc > 0 ? kSqpProj | (pc << 24) : 0) | (wdn << 4);
+  a.flags[b] = fl;
+  a.rho[b] = rho;
+  a.kkt[b] = r;
+}
+
 // One SQP step of instance b (the body of sqp_step_kernel): line search,
 // update, KKT residual, flags.
 __device__ __forceinline__ void sqp_step_one(const SqpArgs& a, int64_t b) {
   int fl = a.flags[b];
   if (fl & kSqpDone) return;
   const int N = a.N;
-  if (a.qp_status && (a.qp_status[b] & 0xFF) != MPCQP_STATUS_OPTIMAL) {
-    // the QP failed (not converged within its budget, or non-convex beyond
-    // the inertia correction with the unprojected Hessian): no step.  An
-    // exact-Hessian iteration raises the damping mu (x4, at least kMuFloor),
-    // which changes the next QP; a Gauss-Newton QP would be rebuilt
-    // unchanged, so kSqpMaxFails failures in a row stop the instance with
-    // the QP's status (never OPTIMAL)
-    const int iters = ((fl >> 8) & 0xFFFF) + 1;
-    const int fails = ((fl >> 24) & 0xF) + 1;
-    const int code = a.qp_status[b] & 0x7;
-    if ((fl & kSqpExact) && !(fl & kSqpProj) && a.proj_steps > 0) {
-      // the exact curvature made the QP fail (non-convex): the projected one
-      // next (mpcqp_bicycle_hessian_convex; a caller of the plain
-      // mpcqp_bicycle_hessian gets the damping below at the next failure)
-      a.flags[b] = (iters << 8) | kSqpExact | kSqpProj | (a.proj_steps << 24);
-    } else if (fl & kSqpExact) {
-      a.mu[b] = fmax(4.0 * a.mu[b], kMuFloor);
-      a.flags[b] = (iters << 8) | (fl & (kSqpExact | kSqpProj | (0xF << 24)));
-    } else if (fails >= kSqpMaxFails) {
-      a.flags[b] = (iters << 8) | kSqpDone | kSqpFail | (code << 28);
-    } else {
-      a.flags[b] = (iters << 8) | (fails << 24);
-    }
-    return;
-  }
+  if (sqp_qp_failed(a, b, fl)) return;
   double* U = a.U + b * N * 2;
   const double* yq = a.yq + b * N * 4;
   const double* piq = a.piq + b * N * 4;
@@ -473,23 +500,7 @@ __device__ __forceinline__ void sqp_step_one(const SqpArgs& a, int64_t b) {
   }
   if (!(r == r)) r = Lim<double>::inf();
 
-  // ---------------------------------------------------- Hessian mode, flags
-  if (fl & kSqpExact) {
-    double mu = a.mu[b];
-    mu = alpha == 1.0 ? (mu > 4e-12 ? a.mu_dec * mu : 0.0) : fmax(4.0 * mu, kMuFloor);
-    a.mu[b] = mu;
-  }
-  const int iters = ((fl >> 8) & 0xFFFF) + 1;
-  const bool exact = (fl & kSqpExact) || r < a.sw || iters >= a.gn_max;  // sticky
-  // projected curvature: count full steps down, then back to the exact one
-  int pc = (fl & kSqpProj) ? ((fl >> 24) & 0xF) : 0;
-  if (pc > 0 && alpha == 1.0) --pc;
-  const int wdn = (force || alpha == 1.0) ? 0 : (wd < 15 ? wd + 1 : 15);
-  fl = (iters << 8) | (r <= a.tol ? kSqpDone : 0) | (exact ? kSqpExact : 0) |
-       (pc > 0 ? kSqpProj | (pc << 24) : 0) | (wdn << 4);
-  a.flags[b] = fl;
-  a.rho[b] = rho;
-  a.kkt[b] = r;
+  sqp_finish(a, b, fl, alpha, r, rho, force, wd);
 }
 
 // ------------------------------------------------------------ host side

@@ -42,6 +42,11 @@ struct SqpSolveArgs {
   SqpArgs s;            // the step: weights, bounds, U, y, pi, X, rho, kkt, mu, flags, fix
   ipm::Args<double> q;  // the QP: stage data and outputs in the workspace
   int max_iter, hmode;
+  // polish a QP first on the previous QP's active set (MPCQP_SQP_WARM): 0 never,
+  // 1 Gauss-Newton QPs, 2 those and exact-Hessian ones once kkt < warm_kkt
+  // (MPCQP_SQP_WARM_KKT), 3 always
+  int warm;
+  double warm_kkt;
   double fix_rho, eps;  // proximal curvature of held inputs, projection floor
   double* Xr;           // (batch, N+1, 4): rollout states of the linearisation
   // per-instance timing of the launch (the workspace's last region, read by
@@ -56,10 +61,330 @@ constexpr int kWsPerStage = 16 + 8 + 4 + 36 + 6 + 4 + 2 + 4 + 4 + 2 + 4;
 
 __device__ __forceinline__ void wg_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
+// ------------------------------------------------- wave-parallel FE pieces
+// The forward-Euler model splits into per-stage trig terms and cheap scalar
+// recurrences: beta_k = atan(k tan delta_k) and sin/cos beta_k depend on u_k
+// alone; psi_{k+1} = psi_k + ts v_k / l_r sin beta_k and v_{k+1} = v_k +
+// ts (acc a_k - fric v_k) need no trig; sin/cos(psi_k + beta_k) then come
+// per stage again, and p_x, p_y are running sums.  So a rollout is two trig
+// rounds on one lane per stage and three short serial scans on lane 0 --
+// every expression written as bike_pt / bike_step write it, so the rollout
+// is bit-identical to model_step's.  Per-stage scratch in LDS after the QP's
+// workspace (kScr doubles per stage, N + 1 stages, then the broadcast slots).
+constexpr int kScr = 14;
+enum { kU0 = 0, kU1, kBeta, kSb, kPx, kPy, kPsi, kV, kSt, kCt, kTJ, kTV, kL0, kL1 };
+constexpr int kScrBcast = 8;
+
+__device__ __forceinline__ double* scr_at(double* scr, int k) { return scr + k * kScr; }
+
+// Rollout of U + alpha d (use_d; d = sqp_dir) or of U; the states of stage k
+// land in scr (kPx, kPy, kPsi, kV) and, when X != nullptr, in X ((N+1) x 4,
+// global); returns 1/2 J and the state-box violation (merit_at's sums, in
+// its order) on every lane.
+__device__ __forceinline__ Merit fe_merit_wave(const SqpArgs& a, int64_t b, double alpha, bool use_d, double* X,
+                               double* scr, int lane) {
+  const int N = a.N;
+  const Bike& p = a.p;
+  const double* U = a.U + b * N * 2;
+  const double kk = p.k();
+  for (int k = lane; k < N; k += kWave) {
+    double u0 = U[2 * k], u1 = U[2 * k + 1];
+    if (use_d) {
+      u0 = fma(alpha, sqp_dir(a, b, 2 * k), u0);
+      u1 = fma(alpha, sqp_dir(a, b, 2 * k + 1), u1);
+    }
+    const double t = tan(u1);
+    const double beta = atan(kk * t);
+    double sb, cb;
+    sincos(beta, &sb, &cb);
+    double* q = scr_at(scr, k);
+    q[kU0] = u0; q[kU1] = u1; q[kBeta] = beta; q[kSb] = sb;
+  }
+  wave_lds_sync();
+  if (lane == 0) {  // psi and v (bike_step's xn[2], xn[3])
+    double x2 = a.x0[b * a.sX0 + 2], x3 = a.x0[b * a.sX0 + 3];
+    for (int k = 0; k < N; ++k) {
+      double* q = scr_at(scr, k);
+      q[kPsi] = x2;
+      q[kV] = x3;
+      const double v = x3;
+      const double n2 = x2 + p.ts * v / p.lr * q[kSb];
+      const double n3 = x3 + p.ts * (p.acc * q[kU0] - p.fric * v);
+      x2 = n2;
+      x3 = n3;
+    }
+    scr_at(scr, N)[kPsi] = x2;
+    scr_at(scr, N)[kV] = x3;
+  }
+  wave_lds_sync();
+  for (int k = lane; k < N; k += kWave) {
+    double* q = scr_at(scr, k);
+    double st, ct;
+    sincos(q[kPsi] + q[kBeta], &st, &ct);
+    q[kSt] = st;
+    q[kCt] = ct;
+  }
+  wave_lds_sync();
+  if (lane == 0) {  // p_x, p_y (xn[0], xn[1])
+    double x0 = a.x0[b * a.sX0], x1 = a.x0[b * a.sX0 + 1];
+    for (int k = 0; k < N; ++k) {
+      double* q = scr_at(scr, k);
+      q[kPx] = x0;
+      q[kPy] = x1;
+      const double v = q[kV];
+      const double n0 = x0 + p.ts * v * q[kCt];
+      const double n1 = x1 + p.ts * v * q[kSt];
+      x0 = n0;
+      x1 = n1;
+    }
+    scr_at(scr, N)[kPx] = x0;
+    scr_at(scr, N)[kPy] = x1;
+  }
+  wave_lds_sync();
+  // per-stage merit terms, and the states out
+  for (int k = lane; k <= N; k += kWave) {
+    const double* q = scr_at(scr, k);
+    const double x[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
+    if (X) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) X[k * 4 + i] = x[i];
+    }
+    if (k < N) {
+      const double u[2] = {q[kU0], q[kU1]};
+      const double* q1 = scr_at(scr, k + 1);
+      const double x1[4] = {q1[kPx], q1[kPy], q1[kPsi], q1[kV]};
+      scr_at(scr, k)[kTJ] = 0.5 * (sq_form(a.Q, 4, x) + sq_form(a.R, 2, u));
+      scr_at(scr, k)[kTV] = box_viol(a, b, k, x1);
+    }
+  }
+  wave_lds_sync();
+  double* bc = scr_at(scr, N + 1);
+  if (lane == 0) {  // merit_at's running sums
+    Merit m{0.0, 0.0};
+    for (int k = 0; k < N; ++k) {
+      m.J += scr_at(scr, k)[kTJ];
+      m.viol += scr_at(scr, k)[kTV];
+    }
+    const double* q = scr_at(scr, N);
+    const double xN[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
+    m.J += 0.5 * sq_form(a.Qf, 4, xN);
+    bc[0] = m.J;
+    bc[1] = m.viol;
+  }
+  wave_lds_sync();
+  return Merit{bc[0], bc[1]};
+}
+
+// A_k, B_k, c_k of every stage from the rollout in scr (model_step_jac at
+// (x_k, u_k), as mpcqp_bicycle_linearise writes them), lane per stage.
+__device__ __forceinline__ void fe_linearise_wave(const SqpArgs& a, int N, double* A, double* B, double* c,
+                                  const double* scr, int lane) {
+  for (int k = lane; k < N; k += kWave) {
+    const double* q = scr_at(const_cast<double*>(scr), k);
+    const double x[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
+    const double u[2] = {q[kU0], q[kU1]};
+    double Aj[4][4], Bj[4][2], xn[4];
+    model_step_jac(a.p, 0, x, u, xn, Aj, Bj);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double t = xn[i] - Bj[i][0] * u[0] - Bj[i][1] * u[1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        A[k * 16 + i * 4 + j] = Aj[i][j];
+        t -= Aj[i][j] * x[j];
+      }
+      B[k * 8 + i * 2] = Bj[i][0];
+      B[k * 8 + i * 2 + 1] = Bj[i][1];
+      c[k * 4 + i] = t;
+    }
+  }
+}
+
+// sqp_step_one on the whole wave for the forward-Euler model: the same line
+// search, update, KKT residual and flags, with every rollout from
+// fe_merit_wave and the per-stage work one lane per stage; the serial parts
+// (the directional derivative's forward sensitivities, the adjoint) run on
+// lane 0 from the stored Jacobians.  The Jacobians at the accepted point are
+// the next iteration's linearisation: they overwrite A, B, c, and the
+// function returns true when it wrote them.
+__device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, double* A, double* B, double* c,
+                              double* scr, int lane) {
+  const int fl = a.flags[b];
+  if (fl & kSqpDone) return false;
+  const int N = a.N;
+  if (a.qp_status && (a.qp_status[b] & 0xFF) != MPCQP_STATUS_OPTIMAL) {
+    if (lane == 0) sqp_qp_failed(a, b, fl);
+    return false;
+  }
+  double* U = a.U + b * N * 2;
+  const double* yq = a.yq + b * N * 4;
+  const double* piq = a.piq + b * N * 4;
+  double* y = a.y + b * N * 4;
+  double* pi = a.pi + b * N * 4;
+  double* X = a.X + b * (N + 1) * 4;
+
+  // ----------------------------------------- merit, directional derivative
+  double ymax = 0.0, dmax = 0.0, umax = 0.0;
+  for (int i = lane; i < 4 * N; i += kWave) ymax = fmax(ymax, fabs(yq[i]));
+  for (int i = lane; i < 2 * N; i += kWave) {
+    dmax = fmax(dmax, fabs(sqp_dir(a, b, i)));
+    umax = fmax(umax, fabs(U[i]));
+  }
+  ymax = wave_max(ymax);
+  dmax = wave_max(dmax);
+  umax = wave_max(umax);
+  const double rho = fmax(a.rho[b], 2.0 * ymax);
+  const Merit m0 = fe_merit_wave(a, b, 0.0, false, nullptr, scr, lane);
+  double* bc = scr_at(scr, N + 1);
+  if (lane == 0) {  // D = d(1/2 J)/dU . d, sqp_step_one's loop on the stored A_k, B_k
+    double D = 0.0;
+    double dx[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < N; ++k) {
+      const double* q = scr_at(scr, k);
+      const double x[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
+      const double u[2] = {U[2 * k], U[2 * k + 1]};
+      const double d[2] = {sqp_dir(a, b, 2 * k), sqp_dir(a, b, 2 * k + 1)};
+      for (int i = 0; i < 4; ++i) {
+        double t = 0.0;
+        for (int j = 0; j < 4; ++j) t = fma(a.Q[i * 4 + j], x[j], t);
+        D = fma(t, dx[i], D);
+      }
+      for (int r = 0; r < 2; ++r) {
+        double t = 0.0;
+        for (int q2 = 0; q2 < 2; ++q2) t = fma(a.R[r * 2 + q2], u[q2], t);
+        D = fma(t, d[r], D);
+      }
+      const double* Ak = A + k * 16;
+      const double* Bk = B + k * 8;
+      double dxn[4];
+      for (int i = 0; i < 4; ++i) {
+        double s = Bk[i * 2] * d[0] + Bk[i * 2 + 1] * d[1];
+        for (int j = 0; j < 4; ++j) s = fma(Ak[i * 4 + j], dx[j], s);
+        dxn[i] = s;
+      }
+      for (int i = 0; i < 4; ++i) dx[i] = dxn[i];
+    }
+    const double* q = scr_at(scr, N);
+    const double xN[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
+    for (int i = 0; i < 4; ++i) {
+      double t = 0.0;
+      for (int j = 0; j < 4; ++j) t = fma(a.Qf[i * 4 + j], xN[j], t);
+      D = fma(t, dx[i], D);
+    }
+    bc[2] = D;
+  }
+  wave_lds_sync();
+  const double D = bc[2];
+  const double phi0 = m0.J + rho * m0.viol;
+  const double Dm = D - rho * m0.viol;
+
+  // --------------------------- backtracking (quadratic interpolation), Armijo
+  double alpha = 1.0;
+  const double noise = 1e-14 * (1.0 + fabs(phi0));
+  const int wd = (fl >> 4) & 0xF;
+  const bool force = a.watchdog > 0 && (fl & kSqpExact) && wd >= a.watchdog;
+  if (!force && dmax > 1e-14 * (1.0 + umax)) {
+    for (int t = 0; t < 40; ++t) {
+      const Merit m = fe_merit_wave(a, b, alpha, true, nullptr, scr, lane);
+      const double phi = m.J + rho * m.viol;
+      if (phi <= phi0 + 1e-4 * alpha * Dm + noise) break;
+      const double den = 2.0 * (phi - phi0 - alpha * Dm);
+      const double at = den > 0.0 ? -Dm * alpha * alpha / den : 0.5 * alpha;
+      alpha = fmin(0.5 * alpha, fmax(0.1 * alpha, at));
+      if (alpha < 1e-10) break;
+    }
+  }
+  // the update (inputs within 1e-9 of a bound put on it), elementwise
+  for (int i = lane; i < 2 * N; i += kWave) {
+    double u = fma(alpha, sqp_dir(a, b, i), U[i]);
+    const int64_t o = b * a.sLb + i;
+    if (a.lb && u <= a.lb[o] + 1e-9 * (1.0 + fabs(a.lb[o]))) u = a.lb[o];
+    if (a.ub && u >= a.ub[o] - 1e-9 * (1.0 + fabs(a.ub[o]))) u = a.ub[o];
+    U[i] = u;
+  }
+  for (int i = lane; i < 4 * N; i += kWave) {
+    y[i] = fma(alpha, yq[i] - y[i], y[i]);
+    pi[i] = fma(alpha, piq[i] - pi[i], pi[i]);
+  }
+  wg_fence();
+
+  // ------------------------------------------ KKT residual at the new point
+  fe_merit_wave(a, b, 0.0, false, X, scr, lane);
+  fe_linearise_wave(a, N, A, B, c, scr, lane);
+  wg_fence();
+  if (lane == 0) {  // the adjoint lambda_{k+1} of every stage, sqp_step_one's order
+    double lam[4];
+    const double* q = scr_at(scr, N);
+    const double xN[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
+    for (int i = 0; i < 4; ++i) {
+      double s = y[(N - 1) * 4 + i];
+      for (int j = 0; j < 4; ++j) s = fma(a.Qf[i * 4 + j], xN[j], s);
+      lam[i] = s;
+    }
+    for (int k = N - 1; k >= 0; --k) {
+      double* qk = scr_at(scr, k);
+      qk[kL0] = lam[0];  // (lambda_{k+1} in four slots: kL0, kL1, kTJ, kTV)
+      qk[kL1] = lam[1];
+      qk[kTJ] = lam[2];
+      qk[kTV] = lam[3];
+      if (k > 0) {
+        const double x[4] = {qk[kPx], qk[kPy], qk[kPsi], qk[kV]};
+        const double* Ak = A + k * 16;
+        double ln[4];
+        for (int i = 0; i < 4; ++i) {
+          double s = y[(k - 1) * 4 + i];
+          for (int j = 0; j < 4; ++j) s = fma(a.Q[i * 4 + j], x[j], s);
+          for (int j = 0; j < 4; ++j) s = fma(Ak[j * 4 + i], lam[j], s);
+          ln[i] = s;
+        }
+        for (int i = 0; i < 4; ++i) lam[i] = ln[i];
+      }
+    }
+  }
+  wave_lds_sync();
+  double r = 0.0;
+  for (int k = lane; k < N; k += kWave) {
+    const double* qk = scr_at(scr, k);
+    const double lam[4] = {qk[kL0], qk[kL1], qk[kTJ], qk[kTV]};
+    const double u[2] = {U[2 * k], U[2 * k + 1]};
+    const double* Bk = B + k * 8;
+    int32_t fb = 0;
+    for (int q = 0; q < 2; ++q) {
+      double g = 0.0;
+      for (int j = 0; j < 2; ++j) g = fma(a.R[q * 2 + j], u[j], g);
+      for (int i = 0; i < 4; ++i) g = fma(Bk[i * 2 + q], lam[i], g);
+      const int64_t o = b * a.sLb + (int64_t)k * 2 + q;
+      const double lo = a.lb ? a.lb[o] : -Lim<double>::inf();
+      const double hi = a.ub ? a.ub[o] : Lim<double>::inf();
+      const double t = fmin(fmax(u[q] - g, lo), hi);
+      r = fmax(r, fabs(u[q] - t));
+      if ((u[q] <= lo + 1e-9 * (1.0 + fabs(lo)) && g > a.fix_grad) ||
+          (u[q] >= hi - 1e-9 * (1.0 + fabs(hi)) && g < -a.fix_grad))
+        fb |= 1 << q;
+    }
+    if (a.fix) a.fix[b * N + k] = a.fix_mode ? fb : 0;
+    const double* q1 = scr_at(const_cast<double*>(scr), k + 1);
+    const double xk1[4] = {q1[kPx], q1[kPy], q1[kPsi], q1[kV]};
+    for (int i = 0; i < 4; ++i) {
+      const int64_t o = b * a.sXb + (int64_t)k * 4 + i;
+      const double hi = a.xhi ? a.xhi[o] : Lim<double>::inf();
+      const double lo = a.xlo ? a.xlo[o] : -Lim<double>::inf();
+      const double yi = y[k * 4 + i];
+      r = fmax(r, fmax(xk1[i] - hi, lo - xk1[i]));
+      if (yi > 0.0) r = fmax(r, fmin(yi, hi - xk1[i]));
+      if (yi < 0.0) r = fmax(r, fmin(-yi, xk1[i] - lo));
+    }
+  }
+  r = wave_max(r);
+  if (!(r == r)) r = Lim<double>::inf();
+  if (lane == 0) sqp_finish(a, b, fl, alpha, r, rho, force, wd);
+  return true;
+}
+
+
 __global__ __launch_bounds__(64, 1) void sqp_solve_kernel(SqpSolveArgs g) {
   extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
   const int lane = threadIdx.x;
-  if (lane >= 4) return;
   const int64_t b = blockIdx.x;
   const SqpArgs& s = g.s;
   const int N = s.N;
@@ -67,63 +392,91 @@ __global__ __launch_bounds__(64, 1) void sqp_solve_kernel(SqpSolveArgs g) {
   double* A = const_cast<double*>(g.q.A) + b * N * 16;
   double* B = const_cast<double*>(g.q.B) + b * N * 8;
   double* c = const_cast<double*>(g.q.c) + b * N * 4;
-  double* Xr = g.Xr + b * (N + 1) * 4;
+  double* X = s.X + b * (N + 1) * 4;
   const double* U = s.U + b * N * 2;
+  double* scr = ipm_lds + (size_t)N * ipm::Layout<4, 2>::F;
+  const bool fe = s.integ == MPCQP_MODEL_FE;
+  bool lin = false;   // A, B, c and X hold the linearisation at the current U
+  bool warm = false;  // the last QP ended polished: its active set is in LDS
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t tqp = 0;
-  int64_t ipm_its = 0;
+  int64_t ipm_its = 0, warm_hits = 0;
   int it = 0;
   for (; it < g.max_iter; ++it) {
     if (s.flags[b] & kSqpDone) break;
     // ------------------------------------------- 1. rollout + linearisation
-    {
+    if (fe) {
+      if (!lin) {
+        fe_merit_wave(s, b, 0.0, false, X, scr, lane);
+        fe_linearise_wave(s, N, A, B, c, scr, lane);
+        wg_fence();
+        lin = true;
+      }
+    } else {  // RK4: the serial rollout on every lane, stage k's Jacobians on lane k
       double x[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) Xr[i] = x[i] = s.x0[b * s.sX0 + i];
+      for (int i = 0; i < 4; ++i) X[i] = x[i] = s.x0[b * s.sX0 + i];
       for (int k = 0; k < N; ++k) {
         const double u[2] = {U[2 * k], U[2 * k + 1]};
         double xn[4];
         model_step(p, s.integ, x, u, xn);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) Xr[(k + 1) * 4 + i] = x[i] = xn[i];
+        for (int i = 0; i < 4; ++i) X[(k + 1) * 4 + i] = x[i] = xn[i];
       }
-    }
-    // every lane wrote the same rollout; stage k's data on lane k % 4 from
-    // its own copy
-    for (int k = lane; k < N; k += 4) {
-      const double* x = Xr + k * 4;
-      const double u[2] = {U[2 * k], U[2 * k + 1]};
-      double Aj[4][4], Bj[4][2], xn[4];
-      model_step_jac(p, s.integ, x, u, xn, Aj, Bj);
+      for (int k = lane; k < N; k += kWave) {
+        const double* xk = X + k * 4;
+        const double u[2] = {U[2 * k], U[2 * k + 1]};
+        double Aj[4][4], Bj[4][2], xn[4];
+        model_step_jac(p, s.integ, xk, u, xn, Aj, Bj);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        double t = xn[i] - Bj[i][0] * u[0] - Bj[i][1] * u[1];
+        for (int i = 0; i < 4; ++i) {
+          double t = xn[i] - Bj[i][0] * u[0] - Bj[i][1] * u[1];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          A[k * 16 + i * 4 + j] = Aj[i][j];
-          t -= Aj[i][j] * x[j];
+          for (int j = 0; j < 4; ++j) {
+            A[k * 16 + i * 4 + j] = Aj[i][j];
+            t -= Aj[i][j] * xk[j];
+          }
+          B[k * 8 + i * 2] = Bj[i][0];
+          B[k * 8 + i * 2 + 1] = Bj[i][1];
+          c[k * 4 + i] = t;
         }
-        B[k * 8 + i * 2] = Bj[i][0];
-        B[k * 8 + i * 2 + 1] = Bj[i][1];
-        c[k * 4 + i] = t;
       }
-      if (g.hmode != kHessGN) {
-        const bool cvx = g.hmode == kHessExact;
-        hess_stage(b, N, k, p, s.integ, g.Xr, s.U, s.pi, s.flags, s.mu, s.fix, g.fix_rho,
+      wg_fence();
+    }
+    // ------------------------------------------------ 2. stage Hessians
+    if (g.hmode != kHessGN) {
+      const bool cvx = g.hmode == kHessExact;
+      for (int k = lane; k < N; k += kWave)
+        hess_stage(b, N, k, p, s.integ, s.X, s.U, s.pi, s.flags, s.mu, s.fix, g.fix_rho,
                    cvx ? s.Q : nullptr, cvx ? s.R : nullptr, g.eps,
                    const_cast<double*>(g.q.H2) + (b * N + k) * 36,
                    const_cast<double*>(g.q.q2) + (b * N + k) * 6);
-      }
     }
     wg_fence();
-    // ------------------------------------------------------------- 2. QP
+    // ------------------------------------------------------------- 3. QP
+    // (one DPP quad; the warm polish where the QP's solution is the one the
+    // interior point would find: Gauss-Newton QPs are convex, a unique
+    // solution; an exact-Hessian QP may have several KKT points, and far from
+    // the NLP's solution the previous active set can pick another one than
+    // the interior point -- which changes the local minimum the SQP ends in
+    // -- so there only once the KKT residual is below warm_kkt)
     const uint64_t q0 = __builtin_amdgcn_s_memrealtime();
-    ipmq::solve_quad<double, 1>(g.q, (int)b, ipm_lds);
+    if (lane < 4) {
+      const int fl = s.flags[b];
+      const bool use_warm = warm && (g.warm == 3 || (g.warm >= 1 && !(fl & kSqpExact)) ||
+                                     (g.warm == 2 && s.kkt[b] < g.warm_kkt));
+      warm = ipmq::solve_quad<double, 1>(g.q, (int)b, ipm_lds, use_warm);
+      warm_hits += (use_warm && warm && ((g.q.status[b] >> 8) & 0xFFFF) == 0) ? 1 : 0;
+    }
     wg_fence();
     tqp += __builtin_amdgcn_s_memrealtime() - q0;
     ipm_its += (g.q.status[b] >> 8) & 0xFFFF;
-    // ----------------------------------------------------------- 3. step
-    if (lane == 0) sqp_step_one(s, b);
+    // ----------------------------------------------------------- 4. step
+    if (fe) {
+      sqp_step_wave(s, b, A, B, c, scr, lane);
+    } else if (lane == 0) {
+      sqp_step_one(s, b);
+    }
     wg_fence();
   }
   if (lane == 0) {
@@ -131,7 +484,7 @@ __global__ __launch_bounds__(64, 1) void sqp_solve_kernel(SqpSolveArgs g) {
     st[0] = (int64_t)(__builtin_amdgcn_s_memrealtime() - t0);
     st[1] = (int64_t)tqp;
     st[2] = ipm_its;
-    st[3] = it;
+    st[3] = it | (warm_hits << 32);
   }
 }
 
@@ -171,7 +524,8 @@ extern "C" int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts,
   const size_t need = mpcqp_bicycle_sqp_solve_workspace(batch, N);
   MPCQP_CHECK_ARG(ws && ws_bytes >= need, "mpcqp_bicycle_sqp_solve: workspace %zu bytes < %zu",
                   ws_bytes, need);
-  const size_t lds = (size_t)N * ipm::Layout<4, 2>::F * sizeof(double);
+  // the QP's workspace, then the step's per-stage scratch (N + 2 rows)
+  const size_t lds = ((size_t)N * ipm::Layout<4, 2>::F + (size_t)(N + 2) * kScr) * sizeof(double);
   MPCQP_CHECK_ARG(lds <= 160 * 1024, "mpcqp_bicycle_sqp_solve: N = %d exceeds the LDS horizon", N);
   SqpSolveArgs g{};
   // ---- the step (mpcqp_bicycle_sqp_step's arguments)
@@ -204,7 +558,8 @@ extern "C" int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts,
   double* wX = w;                 w += bN * 4;
   g.stats = (int64_t*)w;          w += (int64_t)batch * 4;  // (tools/sqp_latency.py reads it here)
   int32_t* wst = qp_status ? qp_status : (int32_t*)w;
-  g.Xr = wXr;
+  g.Xr = a.X;  // (the linearisation's rollout is the SQP state X)
+  (void)wXr;
   a.Z = wz; a.yq = wy; a.piq = wpi; a.qp_status = wst;
   // ---- the QP (mpc.SqpSolver.iterate's mpcqp_mpc_ipm call)
   ipm::Args<double>& q = g.q;
@@ -223,6 +578,16 @@ extern "C" int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts,
   q.z = wz; q.y = wy; q.X = wX; q.lam_u = wlu; q.pi = wpi; q.status = wst;
   q.skip = nullptr; q.skip_mask = 0;
   q.ws = nullptr; q.list = nullptr; q.list_count = nullptr; q.list_begin = 0;
+  static const int warm_qp = [] {
+    const char* e = getenv("MPCQP_SQP_WARM");
+    return e ? atoi(e) : 2;
+  }();
+  static const double warm_kkt = [] {
+    const char* e = getenv("MPCQP_SQP_WARM_KKT");
+    return e ? atof(e) : 1e-3;
+  }();
+  g.warm = warm_qp;
+  g.warm_kkt = warm_kkt;
   g.max_iter = max_iter;
   g.hmode = hessian;
   g.fix_rho = fix_rho();

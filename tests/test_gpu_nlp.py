@@ -432,8 +432,11 @@ def test_one_launch_solve_equals_iteration(hessian, integrator):
 
 
 def test_one_launch_solve_continues_from_its_state():
-    """Two launches of 6 + 34 iterations = one of 40 (the state U, y, pi, X,
-    rho, kkt, mu, flags, fix carries over; converged instances stay frozen)."""
+    """Two launches of 6 + 34 iterations end where one of 40 does (the state
+    U, y, pi, X, rho, kkt, mu, flags, fix carries over; converged instances
+    stay frozen).  Only the QP's warm polish (the previous QP's active set,
+    kept in LDS within a launch) starts cold in the second launch, so the
+    iterates agree to the QP's rounding, not bit for bit."""
     from model_predictive_control_amd.mpc import SqpSolver
 
     ctl = MPCController(30, 0.08, VehicleParameters(), tol=1e-9)
@@ -444,7 +447,10 @@ def test_one_launch_solve_continues_from_its_state():
     a.solve(X0, 40)
     b.solve(X0, 6)
     b.solve(X0, 34)
-    assert torch.equal(a.U, b.U) and torch.equal(a.flags, b.flags) and torch.equal(a.kkt, b.kkt)
+    da, db = a.done(), b.done()
+    assert int(da.sum()) >= 56 and torch.equal(da, db)
+    assert float((a.U - b.U).abs().max()) < 1e-9
+    assert int((a.iters() - b.iters()).abs().max()) <= 1
 
 
 def test_one_launch_solve_checks_arguments():

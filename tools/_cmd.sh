@@ -1,0 +1,3 @@
+set -o pipefail
+for it in 60 150; do timeout -k 10 300 python -u bench.py --config nlp --no-cpu --sqp-iters $it > gpurun_out/b_nlp_$it.json 2> gpurun_out/b_nlp_$it.err || exit 1; done
+for it in 12 30; do timeout -k 10 300 python -u bench.py --config loop --no-cpu --sqp-iters $it > gpurun_out/b_loop_$it.json 2> gpurun_out/b_loop_$it.err || exit 1; done

@@ -52,7 +52,8 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
     st = stats_of(sqp, b, N)
-    tot, tqp, ipm, its = (st[:, i].astype(float) for i in range(4))
+    tot, tqp, ipm = (st[:, i].astype(float) for i in range(3))
+    its, hits = (st[:, 3] & 0xFFFFFFFF).astype(float), (st[:, 3] >> 32).astype(float)
     ok = sqp.done().cpu().numpy()
     per_ipm = tqp / np.maximum(ipm, 1) * TICK_US
     per_sqp_other = (tot - tqp) / np.maximum(its, 1) * TICK_US
@@ -63,11 +64,47 @@ def main():
                           sqp_overhead_us_per_iter=q(per_sqp_other),
                           ipm_iters_per_sqp_iter_mean=round(float(ipm.sum() / its.sum()), 2),
                           sqp_iters_mean=round(float(its.mean()), 2),
+                          warm_qp_frac=round(float(hits.sum() / its.sum()), 3),
                           sum_inst_ms=round(float(tot.sum()) * TICK_US / 1e3, 1))), flush=True)
     for i in np.argsort(-tot)[:8]:
         print(json.dumps(dict(inst=int(i), us=round(tot[i] * TICK_US, 1), qp_us=round(tqp[i] * TICK_US, 1),
                               ipm_iters=int(ipm[i]), sqp_iters=int(its[i]), ok=bool(ok[i]))), flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("SQP_LAT_IPM"):
     main()
+
+
+def ipm_alone(ctl, X0):
+    """The stand-alone interior point (mpcqp_mpc_ipm, the quad kernel) on the
+    Gauss-Newton QP at U = 0: launch time at batch 1 and at the full batch
+    against the iteration counts -- the per-iteration latency without the
+    one-launch kernel's register pressure."""
+    from model_predictive_control_amd import batched
+
+    out = []
+    for b in (1, 64, X0.shape[0]):
+        x0 = X0[:b]
+        U = torch.zeros((b, ctl.N, 2), dtype=torch.float64, device="cuda")
+        A, B, c = batched.bicycle_rti(x0, U, ctl.params, ctl.ts)
+        box = ctl._box()
+        run = lambda: batched.mpc_ipm(A, B, ctl.Q, ctl.R, ctl.QN, ctl.N, x0, lb=ctl.lbz,  # noqa: E731
+                                      ub=ctl.ubz, c=c, tv=True, max_iter=25, **box)
+        o = run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            o = run()
+        e1.record()
+        e1.synchronize()
+        its = ((o["status"] >> 8) & 0xFFFF).cpu().numpy()
+        ms = e0.elapsed_time(e1) / 5
+        out.append(dict(b=b, ms=round(ms, 3), iters_max=int(its.max()), iters_mean=round(float(its.mean()), 2),
+                        us_per_iter_of_max=round(ms * 1e3 / max(1, its.max()), 1)))
+    print("IPM_ALONE", json.dumps(out), flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("SQP_LAT_IPM"):
+    ctl = MPCController(30, 0.08, VehicleParameters(), tol=1e-9)
+    ipm_alone(ctl, torch.as_tensor(bench_x0(4096, 1), dtype=torch.float64, device="cuda"))
