@@ -491,6 +491,34 @@ int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts, const double
                             void* ws, size_t ws_bytes, void* stream);
 
 /*
+ * mpcqp_bicycle_mpc_loop: the receding-horizon loop of the controller above
+ * (rcracers.simulate(x0, dynamics, n_steps, policy=controller), session_4/
+ * main.py:270-271; session4_sol.py:458,465) for T samples in ONE launch, one
+ * workgroup per instance (closed_loop.ClosedLoop in fused mode).  Per sample
+ * t: the SQP of mpcqp_bicycle_sqp_solve from x_t = xs[t] (up to iters_first
+ * iterations at t = 0, iters after), the ControllerLog record
+ * (session_2/log.py:8-12: success[t] (int8), iters_out[t], state_prediction
+ * [t] = the SQP's X ((N+1) x 4), input_prediction[t] = U (N x 2)), the plant
+ * xs[t+1] = F(x_t, U[0]) with its own parameters plant_params and model
+ * plant (MPCQP_PLANT_*, substeps) and us[t] = U[0], then the warm start of
+ * mpcqp_sqp_shift (U, y, pi one stage forward; flags, rho 0; mu = mu0; kkt
+ * = inf).  Every instance runs its own episode.  xs (T+1) x batch x 4 with
+ * xs[0] given; the SQP state as mpcqp_bicycle_sqp_solve's (reset by the
+ * caller before the first sample).  N <= 64.  workspace:
+ * mpcqp_bicycle_sqp_solve_workspace().  fp64.
+ */
+int mpcqp_bicycle_mpc_loop(int dtype, int batch, int N, int T, double ts, const double* params,
+                           int integrator, int hessian, const double* plant_params, int plant,
+                           int substeps, const void* Q, const void* R, const void* Qf,
+                           const void* xlo, const void* xhi, int64_t strideXb, const void* lb,
+                           const void* ub, int64_t strideLb, void* U, void* y, void* pi, void* X,
+                           double* rho, double* kkt, double* mu, int32_t* flags, int32_t* fix,
+                           int iters_first, int iters, int qp_max_iter, double tol, double mu0,
+                           void* xs, void* us, void* success, int32_t* iters_out,
+                           void* state_prediction, void* input_prediction, void* ws,
+                           size_t ws_bytes, void* stream);
+
+/*
  * The receding-horizon loop on device (rcracers.simulate(x0, dynamics,
  * n_steps, policy=controller), session_4/main.py:270-271; session4_sol.py:
  * 458,465), one step of it per call pair:

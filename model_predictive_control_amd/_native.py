@@ -104,6 +104,11 @@ SIGNATURES = {
                                      _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp,
                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _d, _vp,
                                      ctypes.c_size_t, _vp]),
+    "mpcqp_bicycle_mpc_loop": (_i, [_i, _i, _i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _i,
+                                    ctypes.POINTER(ctypes.c_double), _i, _i, _vp, _vp, _vp, _vp,
+                                    _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _vp, _vp, _i, _i, _i, _d, _d, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _vp, ctypes.c_size_t, _vp]),
     "mpcqp_bicycle_plant": (_i, [_i, _i, _d, ctypes.POINTER(ctypes.c_double), _i, _i, _vp, _vp,
                                  _i64, _vp, _vp, _vp]),
     "mpcqp_sqp_shift": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _vp]),

@@ -837,6 +837,44 @@ def bicycle_sqp_solve(x0, U, y, pi, X, state: dict, params, ts: float, Q, R, Qf,
     return ws
 
 
+def bicycle_mpc_loop(xs, us, success, iters, state_prediction, input_prediction, U, y, pi, X,
+                     state: dict, params, ts: float, Q, R, Qf, *, plant_params, plant: int = 0,
+                     substeps: int = 20, hessian: str = "exact", xlo=None, xhi=None, lb=None,
+                     ub=None, tol: float = 1e-9, iters_first: int = 60, iters_per_step: int = 10,
+                     qp_max_iter: int = 25, integrator: int = 0, mu0: float = 1e-3,
+                     ws: torch.Tensor | None = None) -> torch.Tensor:
+    """The receding-horizon loop, every sample in one launch (include/mpcqp.h
+    ``mpcqp_bicycle_mpc_loop``): xs (T+1, b, 4) with xs[0] given, us (T, b, 2),
+    success (T, b) bool, iters (T, b) int32, state_prediction (T, b, N+1, 4),
+    input_prediction (T, b, N, 2); the SQP state as ``bicycle_sqp_solve``'s
+    (reset before).  Returns the workspace."""
+    T, b = int(us.shape[0]), int(U.shape[0])
+    N = int(U.shape[1])
+    xlo, xhi, sxb = _bound_pair(xlo, xhi, b, 4 * N, "xlo/xhi")
+    lb, ub, slb = _bound_pair(lb, ub, b, 2 * N, "lb/ub")
+    for name, t, shp, dt in (("xs", xs, (T + 1, b, 4), torch.float64), ("us", us, (T, b, 2), torch.float64),
+                             ("success", success, (T, b), torch.bool),
+                             ("iters", iters, (T, b), torch.int32),
+                             ("state_prediction", state_prediction, (T, b, N + 1, 4), torch.float64),
+                             ("input_prediction", input_prediction, (T, b, N, 2), torch.float64)):
+        if tuple(t.shape) != shp or t.dtype != dt or not t.is_contiguous() or t.device != U.device:
+            raise ValueError(f"bicycle_mpc_loop: {name} must be a contiguous {dt} device tensor "
+                             f"of shape {shp}")
+    lib = _lib()
+    wsb = int(lib.mpcqp_bicycle_sqp_solve_workspace(b, N))
+    ws = _workspace(wsb, U.device, ws)
+    rc = lib.mpcqp_bicycle_mpc_loop(
+        nat.F64, b, N, T, float(ts), _bike_params(params), int(integrator), nat.SQP_HESS[hessian],
+        _bike_params(plant_params), int(plant), int(substeps), _ptr(Q), _ptr(R), _ptr(Qf),
+        _ptr(xlo), _ptr(xhi), sxb, _ptr(lb), _ptr(ub), slb, _ptr(U), _ptr(y), _ptr(pi), _ptr(X),
+        _ptr(state["rho"]), _ptr(state["kkt"]), _ptr(state["mu"]), _ptr(state["flags"]),
+        _ptr(state.get("fix")), int(iters_first), int(iters_per_step), int(qp_max_iter), float(tol),
+        float(mu0), _ptr(xs), _ptr(us), _ptr(success), _ptr(iters), _ptr(state_prediction),
+        _ptr(input_prediction), _ptr(ws), wsb, _stream())
+    nat.check(rc, "mpcqp_bicycle_mpc_loop")
+    return ws
+
+
 def bicycle_linearise(x0, U, params, ts: float, integrator: int = 0, out: tuple | None = None):
     """Rollout + linearisation of the prediction model (include/mpcqp.h
     ``mpcqp_bicycle_linearise``; integrator 0 = forward Euler, 1 = RK4):

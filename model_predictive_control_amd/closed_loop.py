@@ -120,6 +120,29 @@ class ClosedLoop:
                                  batched._stream())
         nat.check(rc, "mpcqp_sqp_shift")
 
+    def _episode(self, s, T: int):
+        """All T steps from s["xs"][0]: one launch (mpcqp_bicycle_mpc_loop,
+        every instance its own episode) when the controller runs the fused
+        SQP, else T calls of _step."""
+        ctl = self.ctl
+        if ctl.mode == "sqp" and ctl.fused and ctl.N <= 64:
+            sqp = s["sqp"]
+            sqp.reset()
+            sqp.ws = batched.bicycle_mpc_loop(
+                s["xs"], s["us"], s["success"], s["iters"], s["state_prediction"],
+                s["input_prediction"], sqp.U, sqp.y, sqp.pi, sqp.X, sqp.state(), ctl.params,
+                ctl.ts, ctl.Q, ctl.R, ctl.QN, plant_params=self.plant_params, plant=self.plant,
+                substeps=self.substeps, hessian=ctl.hessian, xlo=sqp.box.get("xlo"),
+                xhi=sqp.box.get("xhi"), lb=ctl.lbz, ub=ctl.ubz, tol=ctl.tol,
+                iters_first=self.iters_first, iters_per_step=self.iters,
+                qp_max_iter=sqp.QP_MAX_ITER,
+                integrator=nat.MODEL_RK4 if ctl.integrator == "rk4" else nat.MODEL_FE,
+                mu0=sqp.MU0, ws=sqp.ws)
+            return
+        self._reset(s)
+        for t in range(T):
+            self._step(s, t)
+
     # ---------------------------------------------------------------- run
     def run(self, X0, steps: int) -> dict:
         """X0 (b, 4) -> dict of device tensors: xs (T+1, b, 4), us (T, b, 2),
@@ -141,9 +164,7 @@ class ClosedLoop:
                 torch.cuda.current_stream().wait_stream(side)
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
-                    self._reset(s)
-                    for t in range(T):
-                        self._step(s, t)
+                    self._episode(s, T)
                 g = self._graphs[key] = (graph, s)
             graph, s = g
             s["xs"][0].copy_(X0)
@@ -151,8 +172,7 @@ class ClosedLoop:
         else:
             s = self._alloc(b, T)
             s["xs"][0].copy_(X0)
-            for t in range(T):
-                self._step(s, t)
+            self._episode(s, T)
         keys = ("xs", "us", "success", "iters", "state_prediction", "input_prediction")
         # graph mode replays into buffers cached per (b, T): hand out copies, so a
         # later run() of the same shape cannot overwrite results the caller holds

@@ -99,48 +99,13 @@ __global__ void model_jac_kernel(int batch, int N, Bike p, int integ, const doub
 //      (exact_integration, main.py:150-170)
 // with the plant's own parameters (e.g. friction x 0.8, session4_sol.py:
 // 461-462).  One lane per instance; writes x_{t+1} and records u_t.
-__device__ void bike_f(const Bike& p, const double* x, const double* u, double* f) {
-  const double kk = p.k();
-  const double beta = atan(kk * tan(u[1]));
-  double s, c;
-  sincos(x[2] + beta, &s, &c);
-  f[0] = x[3] * c;
-  f[1] = x[3] * s;
-  f[2] = x[3] / p.lr * sin(beta);
-  f[3] = p.acc * u[0] - p.fric * x[3];
-}
-
-__device__ void bike_rk4(const Bike& p, double h, const double* x, const double* u, double* xn) {
-  double k1[4], k2[4], k3[4], k4[4], t[4];
-  bike_f(p, x, u, k1);
-  for (int i = 0; i < 4; ++i) t[i] = x[i] + 0.5 * h * k1[i];
-  bike_f(p, t, u, k2);
-  for (int i = 0; i < 4; ++i) t[i] = x[i] + 0.5 * h * k2[i];
-  bike_f(p, t, u, k3);
-  for (int i = 0; i < 4; ++i) t[i] = x[i] + h * k3[i];
-  bike_f(p, t, u, k4);
-  for (int i = 0; i < 4; ++i) xn[i] = x[i] + h / 6.0 * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
-}
-
 __global__ void plant_kernel(int batch, Bike p, int integrator, int substeps, const double* x,
                              const double* U, int64_t sU, double* xn, double* u_rec) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= batch) return;
   double xs[4], u[2] = {U[(int64_t)b * sU], U[(int64_t)b * sU + 1]};
   for (int i = 0; i < 4; ++i) xs[i] = x[(int64_t)b * 4 + i];
-  if (integrator == 0) {
-    double f[4];
-    bike_f(p, xs, u, f);
-    for (int i = 0; i < 4; ++i) xs[i] += p.ts * f[i];
-  } else {
-    const int m = integrator == 1 ? 1 : substeps;
-    const double h = p.ts / m;
-    for (int s = 0; s < m; ++s) {
-      double t[4];
-      bike_rk4(p, h, xs, u, t);
-      for (int i = 0; i < 4; ++i) xs[i] = t[i];
-    }
-  }
+  plant_step(p, integrator, substeps, xs, u);
   for (int i = 0; i < 4; ++i) xn[(int64_t)b * 4 + i] = xs[i];
   if (u_rec) {
     u_rec[(int64_t)b * 2] = u[0];

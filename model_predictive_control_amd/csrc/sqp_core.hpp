@@ -503,6 +503,51 @@ __device__ __forceinline__ void sqp_step_one(const SqpArgs& a, int64_t b) {
   sqp_finish(a, b, fl, alpha, r, rho, force, wd);
 }
 
+// ------------------------------------------- the closed loop's plant
+// (rcracers.simulate(x0, dynamics, n_steps, policy), main.py:270-271)
+__device__ inline void bike_f(const Bike& p, const double* x, const double* u, double* f) {
+  const double kk = p.k();
+  const double beta = atan(kk * tan(u[1]));
+  double s, c;
+  sincos(x[2] + beta, &s, &c);
+  f[0] = x[3] * c;
+  f[1] = x[3] * s;
+  f[2] = x[3] / p.lr * sin(beta);
+  f[3] = p.acc * u[0] - p.fric * x[3];
+}
+
+__device__ inline void bike_rk4(const Bike& p, double h, const double* x, const double* u, double* xn) {
+  double k1[4], k2[4], k3[4], k4[4], t[4];
+  bike_f(p, x, u, k1);
+  for (int i = 0; i < 4; ++i) t[i] = x[i] + 0.5 * h * k1[i];
+  bike_f(p, t, u, k2);
+  for (int i = 0; i < 4; ++i) t[i] = x[i] + 0.5 * h * k2[i];
+  bike_f(p, t, u, k3);
+  for (int i = 0; i < 4; ++i) t[i] = x[i] + h * k3[i];
+  bike_f(p, t, u, k4);
+  for (int i = 0; i < 4; ++i) xn[i] = x[i] + h / 6.0 * (k1[i] + 2.0 * k2[i] + 2.0 * k3[i] + k4[i]);
+}
+
+
+// One step of the closed loop's plant, in place on x: 0 forward Euler, 1 RK4,
+// 2 RK4 over `substeps` sub-intervals (the stand-in for odeint)
+__device__ inline void plant_step(const Bike& p, int integrator, int substeps, double* xs,
+                                  const double* u) {
+  if (integrator == 0) {
+    double f[4];
+    bike_f(p, xs, u, f);
+    for (int i = 0; i < 4; ++i) xs[i] += p.ts * f[i];
+  } else {
+    const int m = integrator == 1 ? 1 : substeps;
+    const double h = p.ts / m;
+    for (int s = 0; s < m; ++s) {
+      double t[4];
+      bike_rk4(p, h, xs, u, t);
+      for (int i = 0; i < 4; ++i) xs[i] = t[i];
+    }
+  }
+}
+
 // ------------------------------------------------------------ host side
 inline Bike bike_of(double ts, const double* prm) {
   Bike p;

@@ -382,10 +382,17 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
 }
 
 
-__global__ __launch_bounds__(64, 1) void sqp_solve_kernel(SqpSolveArgs g) {
-  extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
-  const int lane = threadIdx.x;
-  const int64_t b = blockIdx.x;
+// Per-instance clocks of a launch (the workspace's stats region).
+struct SolveClock {
+  uint64_t tqp = 0;
+  int64_t ipm_its = 0, warm_hits = 0, sqp_its = 0;
+};
+
+// Up to max_iter SQP iterations of instance b, to its own convergence: the
+// body of both kernels below.  All 64 lanes (the QP on lanes 0..3).
+__device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_t b, int max_iter,
+                                                   double* ipm_lds, double* scr, int lane,
+                                                   SolveClock& clk) {
   const SqpArgs& s = g.s;
   const int N = s.N;
   const Bike p = s.p;
@@ -394,15 +401,11 @@ __global__ __launch_bounds__(64, 1) void sqp_solve_kernel(SqpSolveArgs g) {
   double* c = const_cast<double*>(g.q.c) + b * N * 4;
   double* X = s.X + b * (N + 1) * 4;
   const double* U = s.U + b * N * 2;
-  double* scr = ipm_lds + (size_t)N * ipm::Layout<4, 2>::F;
   const bool fe = s.integ == MPCQP_MODEL_FE;
   bool lin = false;   // A, B, c and X hold the linearisation at the current U
   bool warm = false;  // the last QP ended polished: its active set is in LDS
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t tqp = 0;
-  int64_t ipm_its = 0, warm_hits = 0;
   int it = 0;
-  for (; it < g.max_iter; ++it) {
+  for (; it < max_iter; ++it) {
     if (s.flags[b] & kSqpDone) break;
     // ------------------------------------------- 1. rollout + linearisation
     if (fe) {
@@ -466,11 +469,11 @@ __global__ __launch_bounds__(64, 1) void sqp_solve_kernel(SqpSolveArgs g) {
       const bool use_warm = warm && (g.warm == 3 || (g.warm >= 1 && !(fl & kSqpExact)) ||
                                      (g.warm == 2 && s.kkt[b] < g.warm_kkt));
       warm = ipmq::solve_quad<double, 1>(g.q, (int)b, ipm_lds, use_warm);
-      warm_hits += (use_warm && warm && ((g.q.status[b] >> 8) & 0xFFFF) == 0) ? 1 : 0;
+      clk.warm_hits += (use_warm && warm && ((g.q.status[b] >> 8) & 0xFFFF) == 0) ? 1 : 0;
     }
     wg_fence();
-    tqp += __builtin_amdgcn_s_memrealtime() - q0;
-    ipm_its += (g.q.status[b] >> 8) & 0xFFFF;
+    clk.tqp += __builtin_amdgcn_s_memrealtime() - q0;
+    clk.ipm_its += (g.q.status[b] >> 8) & 0xFFFF;
     // ----------------------------------------------------------- 4. step
     if (fe) {
       sqp_step_wave(s, b, A, B, c, scr, lane);
@@ -479,13 +482,121 @@ __global__ __launch_bounds__(64, 1) void sqp_solve_kernel(SqpSolveArgs g) {
     }
     wg_fence();
   }
+  clk.sqp_its += it;
+}
+
+__device__ __forceinline__ void write_clock(const SqpSolveArgs& g, int64_t b, uint64_t t0,
+                                            const SolveClock& clk, int lane) {
   if (lane == 0) {
     int64_t* st = g.stats + b * 4;
     st[0] = (int64_t)(__builtin_amdgcn_s_memrealtime() - t0);
-    st[1] = (int64_t)tqp;
-    st[2] = ipm_its;
-    st[3] = it | (warm_hits << 32);
+    st[1] = (int64_t)clk.tqp;
+    st[2] = clk.ipm_its;
+    st[3] = clk.sqp_its | (clk.warm_hits << 32);
   }
+}
+
+__global__ __launch_bounds__(64, 1) void sqp_solve_kernel(SqpSolveArgs g) {
+  extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  double* scr = ipm_lds + (size_t)g.s.N * ipm::Layout<4, 2>::F;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  SolveClock clk;
+  sqp_solve_instance(g, b, g.max_iter, ipm_lds, scr, lane, clk);
+  write_clock(g, b, t0, clk, lane);
+}
+
+// ------------------------------------------------ the whole closed loop
+// rcracers.simulate(x0, dynamics, n_steps, policy=controller) of main.py:
+// 270-271 (session4_sol.py:458,465) for one instance per workgroup: per
+// sample t the controller's SQP from the shifted previous solution
+// (sqp_solve_instance, up to iters_first / iters iterations), the
+// ControllerLog record (session_2/log.py:8-12), the plant x_{t+1} =
+// F(x_t, u_0), and the warm-start shift -- ClosedLoop._step's sequence, in
+// one launch.  Every instance runs its own episode: the launch lasts as long
+// as the slowest episode, not the sum over samples of each sample's slowest
+// solve.
+struct SqpLoopArgs {
+  int T, iters_first, iters;
+  double mu0;
+  Bike plant;
+  int plant_integ, substeps;
+  double* xs;           // (T+1, batch, 4); xs[0] given
+  double* us;           // (T, batch, 2)
+  int8_t* success;      // (T, batch)
+  int32_t* iters_out;   // (T, batch)
+  double* state_pred;   // (T, batch, N+1, 4)
+  double* input_pred;   // (T, batch, N, 2)
+  double* x0buf;        // (batch, 4): the sample's x0 (g.s.x0, g.q.x0)
+};
+
+__global__ __launch_bounds__(64, 1) void sqp_loop_kernel(SqpSolveArgs g, SqpLoopArgs e) {
+  extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const SqpArgs& s = g.s;
+  const int N = s.N, batch = s.batch;
+  double* scr = ipm_lds + (size_t)N * ipm::Layout<4, 2>::F;
+  double* U = s.U + b * N * 2;
+  double* y = s.y + b * N * 4;
+  double* pi = s.pi + b * N * 4;
+  const double* X = s.X + b * (N + 1) * 4;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  SolveClock clk;
+  for (int t = 0; t < e.T; ++t) {
+    const double* xt = e.xs + ((int64_t)t * batch + b) * 4;
+    if (lane < 4) e.x0buf[b * 4 + lane] = xt[lane];
+    wg_fence();
+    sqp_solve_instance(g, b, t == 0 ? e.iters_first : e.iters, ipm_lds, scr, lane, clk);
+    // ControllerLog: solver_success, the iteration count, [x_t; X], U
+    const int fl = s.flags[b];
+    const int64_t tb = (int64_t)t * batch + b;
+    if (lane == 0) {
+      e.success[tb] = ((fl & kSqpDone) && !(fl & kSqpFail)) ? 1 : 0;
+      e.iters_out[tb] = (fl >> 8) & 0xFFFF;
+    }
+    for (int j = lane; j < (N + 1) * 4; j += kWave) e.state_pred[tb * (N + 1) * 4 + j] = X[j];
+    for (int j = lane; j < N * 2; j += kWave) e.input_pred[tb * N * 2 + j] = U[j];
+    // the plant with u_t = U[0] (mpcqp_bicycle_plant)
+    if (lane == 0) {
+      double x[4] = {xt[0], xt[1], xt[2], xt[3]};
+      const double u[2] = {U[0], U[1]};
+      plant_step(e.plant, e.plant_integ, e.substeps, x, u);
+      double* xn = e.xs + ((int64_t)(t + 1) * batch + b) * 4;
+      for (int i = 0; i < 4; ++i) xn[i] = x[i];
+      e.us[tb * 2] = u[0];
+      e.us[tb * 2 + 1] = u[1];
+    }
+    // the warm start of the next sample (mpcqp_sqp_shift): every per-stage
+    // array one stage forward, the last stage repeated; the SQP state reset
+    double su[2] = {0.0, 0.0}, sy[4] = {0.0, 0.0, 0.0, 0.0}, sp[4] = {0.0, 0.0, 0.0, 0.0};
+    const int k = lane;
+    const bool mv = k + 1 < N;
+    if (mv) {
+      for (int j = 0; j < 2; ++j) su[j] = U[(k + 1) * 2 + j];
+      for (int j = 0; j < 4; ++j) {
+        sy[j] = y[(k + 1) * 4 + j];
+        sp[j] = pi[(k + 1) * 4 + j];
+      }
+    }
+    wg_fence();
+    if (mv) {
+      for (int j = 0; j < 2; ++j) U[k * 2 + j] = su[j];
+      for (int j = 0; j < 4; ++j) {
+        y[k * 4 + j] = sy[j];
+        pi[k * 4 + j] = sp[j];
+      }
+    }
+    if (lane == 0) {
+      s.flags[b] = 0;
+      s.rho[b] = 0.0;
+      s.mu[b] = e.mu0;
+      s.kkt[b] = Lim<double>::inf();
+    }
+    wg_fence();
+  }
+  write_clock(g, b, t0, clk, lane);
 }
 
 }  // namespace mpcqp
@@ -498,36 +609,30 @@ extern "C" size_t mpcqp_bicycle_sqp_solve_workspace(int batch, int N) {
          256;
 }
 
-extern "C" int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts,
-                                       const double* params, int integrator, int hessian,
-                                       const void* x0, int64_t strideX0, const void* Q,
-                                       const void* R, const void* Qf, const void* xlo,
-                                       const void* xhi, int64_t strideXb, const void* lb,
-                                       const void* ub, int64_t strideLb, void* U, void* y, void* pi,
-                                       void* X, double* rho, double* kkt, double* mu,
-                                       int32_t* flags, int32_t* fix, void* lam_u,
-                                       int32_t* qp_status, int max_iter, int qp_max_iter,
-                                       double tol, void* ws, size_t ws_bytes, void* stream) {
-  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_bicycle_sqp_solve: MPCQP_F64 only");
-  MPCQP_CHECK_ARG(batch >= 0 && N >= 1 && max_iter >= 0, "mpcqp_bicycle_sqp_solve: bad sizes");
+// The arguments both entry points share (checks, the step's and the QP's
+// argument blocks, the workspace regions); x0 with stride strideX0.
+static int setup_solve(const char* fn, SqpSolveArgs& g, int batch, int N, double ts,
+                       const double* params, int integrator, int hessian, const void* x0,
+                       int64_t strideX0, const void* Q, const void* R, const void* Qf,
+                       const void* xlo, const void* xhi, int64_t strideXb, const void* lb,
+                       const void* ub, int64_t strideLb, void* U, void* y, void* pi, void* X,
+                       double* rho, double* kkt, double* mu, int32_t* flags, int32_t* fix,
+                       void* lam_u, int32_t* qp_status, int max_iter, int qp_max_iter, double tol,
+                       void* ws, size_t ws_bytes, size_t& lds) {
+  MPCQP_CHECK_ARG(batch >= 0 && N >= 1 && max_iter >= 0, "%s: bad sizes", fn);
   MPCQP_CHECK_ARG(params && x0 && Q && R && Qf && U && y && pi && X && rho && kkt && mu && flags,
-                  "mpcqp_bicycle_sqp_solve: null pointer");
-  MPCQP_CHECK_ARG(params[1] > 0 && params[0] + params[1] > 0,
-                  "mpcqp_bicycle_sqp_solve: bad axle lengths");
-  MPCQP_CHECK_ARG(strideX0 >= 4 && strideXb >= 0 && strideLb >= 0,
-                  "mpcqp_bicycle_sqp_solve: bad strides");
+                  "%s: null pointer", fn);
+  MPCQP_CHECK_ARG(params[1] > 0 && params[0] + params[1] > 0, "%s: bad axle lengths", fn);
+  MPCQP_CHECK_ARG(strideX0 >= 4 && strideXb >= 0 && strideLb >= 0, "%s: bad strides", fn);
   MPCQP_CHECK_ARG(integrator == MPCQP_MODEL_FE || integrator == MPCQP_MODEL_RK4,
-                  "mpcqp_bicycle_sqp_solve: integrator %d", integrator);
-  MPCQP_CHECK_ARG(hessian >= kHessGN && hessian <= kHessRaw,
-                  "mpcqp_bicycle_sqp_solve: hessian mode %d", hessian);
-  if (batch == 0 || max_iter == 0) return MPCQP_OK;
+                  "%s: integrator %d", fn, integrator);
+  MPCQP_CHECK_ARG(hessian >= kHessGN && hessian <= kHessRaw, "%s: hessian mode %d", fn, hessian);
   const size_t need = mpcqp_bicycle_sqp_solve_workspace(batch, N);
-  MPCQP_CHECK_ARG(ws && ws_bytes >= need, "mpcqp_bicycle_sqp_solve: workspace %zu bytes < %zu",
+  MPCQP_CHECK_ARG(batch == 0 || (ws && ws_bytes >= need), "%s: workspace %zu bytes < %zu", fn,
                   ws_bytes, need);
   // the QP's workspace, then the step's per-stage scratch (N + 2 rows)
-  const size_t lds = ((size_t)N * ipm::Layout<4, 2>::F + (size_t)(N + 2) * kScr) * sizeof(double);
-  MPCQP_CHECK_ARG(lds <= 160 * 1024, "mpcqp_bicycle_sqp_solve: N = %d exceeds the LDS horizon", N);
-  SqpSolveArgs g{};
+  lds = ((size_t)N * ipm::Layout<4, 2>::F + (size_t)(N + 2) * kScr) * sizeof(double);
+  MPCQP_CHECK_ARG(lds <= 160 * 1024, "%s: N = %d exceeds the LDS horizon", fn, N);
   // ---- the step (mpcqp_bicycle_sqp_step's arguments)
   SqpArgs& a = g.s;
   a.batch = batch; a.N = N; a.p = bike_of(ts, params); a.integ = integrator;
@@ -550,7 +655,7 @@ extern "C" int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts,
   double* wc = w;                 w += bN * 4;
   double* wH = w;                 w += bN * 36;
   double* wq = w;                 w += bN * 6;
-  double* wXr = w;                w += bN * 4 + (int64_t)batch * 4;
+  double* wx0 = w;                w += bN * 4 + (int64_t)batch * 4;  // (the loop's x0 per sample)
   double* wz = w;                 w += bN * 2;
   double* wy = w;                 w += bN * 4;
   double* wpi = w;                w += bN * 4;
@@ -558,8 +663,7 @@ extern "C" int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts,
   double* wX = w;                 w += bN * 4;
   g.stats = (int64_t*)w;          w += (int64_t)batch * 4;  // (tools/sqp_latency.py reads it here)
   int32_t* wst = qp_status ? qp_status : (int32_t*)w;
-  g.Xr = a.X;  // (the linearisation's rollout is the SQP state X)
-  (void)wXr;
+  g.Xr = wx0;
   a.Z = wz; a.yq = wy; a.piq = wpi; a.qp_status = wst;
   // ---- the QP (mpc.SqpSolver.iterate's mpcqp_mpc_ipm call)
   ipm::Args<double>& q = g.q;
@@ -592,12 +696,84 @@ extern "C" int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts,
   g.hmode = hessian;
   g.fix_rho = fix_rho();
   g.eps = 1e-6;  // mpcqp_bicycle_hessian_convex's floor (batched.bicycle_hessian)
+  return MPCQP_OK;
+}
+
+template <class K>
+static int set_lds(K kern, size_t lds) {
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)sqp_solve_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(sqp_solve)");
   }
+  return MPCQP_OK;
+}
+
+extern "C" int mpcqp_bicycle_sqp_solve(int dtype, int batch, int N, double ts,
+                                       const double* params, int integrator, int hessian,
+                                       const void* x0, int64_t strideX0, const void* Q,
+                                       const void* R, const void* Qf, const void* xlo,
+                                       const void* xhi, int64_t strideXb, const void* lb,
+                                       const void* ub, int64_t strideLb, void* U, void* y, void* pi,
+                                       void* X, double* rho, double* kkt, double* mu,
+                                       int32_t* flags, int32_t* fix, void* lam_u,
+                                       int32_t* qp_status, int max_iter, int qp_max_iter,
+                                       double tol, void* ws, size_t ws_bytes, void* stream) {
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_bicycle_sqp_solve: MPCQP_F64 only");
+  SqpSolveArgs g{};
+  size_t lds = 0;
+  const int rc = setup_solve("mpcqp_bicycle_sqp_solve", g, batch, N, ts, params, integrator,
+                             hessian, x0, strideX0, Q, R, Qf, xlo, xhi, strideXb, lb, ub, strideLb,
+                             U, y, pi, X, rho, kkt, mu, flags, fix, lam_u, qp_status, max_iter,
+                             qp_max_iter, tol, ws, ws_bytes, lds);
+  if (rc != MPCQP_OK) return rc;
+  if (batch == 0 || max_iter == 0) return MPCQP_OK;
+  if (set_lds(sqp_solve_kernel, lds) != MPCQP_OK) return MPCQP_EHIP;
   hipLaunchKernelGGL(sqp_solve_kernel, dim3((unsigned)batch), dim3(64), lds, (hipStream_t)stream, g);
   MPCQP_CHECK_LAUNCH("sqp_solve_kernel");
+  return MPCQP_OK;
+}
+
+extern "C" int mpcqp_bicycle_mpc_loop(int dtype, int batch, int N, int T, double ts,
+                                      const double* params, int integrator, int hessian,
+                                      const double* plant_params, int plant, int substeps,
+                                      const void* Q, const void* R, const void* Qf,
+                                      const void* xlo, const void* xhi, int64_t strideXb,
+                                      const void* lb, const void* ub, int64_t strideLb, void* U,
+                                      void* y, void* pi, void* X, double* rho, double* kkt,
+                                      double* mu, int32_t* flags, int32_t* fix, int iters_first,
+                                      int iters, int qp_max_iter, double tol, double mu0, void* xs,
+                                      void* us, void* success, int32_t* iters_out,
+                                      void* state_prediction, void* input_prediction, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  MPCQP_CHECK_ARG(dtype == MPCQP_F64, "mpcqp_bicycle_mpc_loop: MPCQP_F64 only");
+  MPCQP_CHECK_ARG(T >= 0 && iters_first >= 0 && iters >= 0 && N <= kWave,
+                  "mpcqp_bicycle_mpc_loop: bad sizes (T=%d, N=%d <= 64)", T, N);
+  MPCQP_CHECK_ARG(plant_params && plant_params[1] > 0 && plant_params[0] + plant_params[1] > 0,
+                  "mpcqp_bicycle_mpc_loop: bad plant parameters");
+  MPCQP_CHECK_ARG(plant >= MPCQP_PLANT_FE && plant <= MPCQP_PLANT_RK4_SUB &&
+                      (plant != MPCQP_PLANT_RK4_SUB || substeps >= 1),
+                  "mpcqp_bicycle_mpc_loop: plant %d / substeps %d", plant, substeps);
+  MPCQP_CHECK_ARG(xs && us && success && iters_out && state_prediction && input_prediction,
+                  "mpcqp_bicycle_mpc_loop: null output");
+  SqpSolveArgs g{};
+  size_t lds = 0;
+  // the sample's x0 lives in the workspace (written per sample by the kernel)
+  double* x0buf = (double*)ws + (int64_t)batch * N * (16 + 8 + 4 + 36 + 6);
+  const int rc = setup_solve("mpcqp_bicycle_mpc_loop", g, batch, N, ts, params, integrator,
+                             hessian, x0buf, 4, Q, R, Qf, xlo, xhi, strideXb, lb, ub, strideLb,
+                             U, y, pi, X, rho, kkt, mu, flags, fix, nullptr, nullptr,
+                             std::max(iters_first, iters), qp_max_iter, tol, ws, ws_bytes, lds);
+  if (rc != MPCQP_OK) return rc;
+  if (batch == 0 || T == 0) return MPCQP_OK;
+  SqpLoopArgs e{};
+  e.T = T; e.iters_first = iters_first; e.iters = iters; e.mu0 = mu0;
+  e.plant = bike_of(ts, plant_params); e.plant_integ = plant; e.substeps = substeps;
+  e.xs = (double*)xs; e.us = (double*)us; e.success = (int8_t*)success; e.iters_out = iters_out;
+  e.state_pred = (double*)state_prediction; e.input_pred = (double*)input_prediction;
+  e.x0buf = x0buf;
+  if (set_lds(sqp_loop_kernel, lds) != MPCQP_OK) return MPCQP_EHIP;
+  hipLaunchKernelGGL(sqp_loop_kernel, dim3((unsigned)batch), dim3(64), lds, (hipStream_t)stream, g, e);
+  MPCQP_CHECK_LAUNCH("sqp_loop_kernel");
   return MPCQP_OK;
 }

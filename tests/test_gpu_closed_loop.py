@@ -107,3 +107,30 @@ def test_plant_kernel_vs_numpy(dev, plant):
     for i in range(b):
         assert np.abs(xn[i].cpu().numpy() - step(x[i], U[i, 0])).max() < tol
     assert np.array_equal(ur.cpu().numpy(), U[:, 0])
+
+
+@pytest.mark.parametrize("plant", ["fe", "exact"])
+def test_closed_loop_one_launch_episode_equals_steps(dev, plant):
+    """mpcqp_bicycle_mpc_loop (every sample of every instance in one launch)
+    against the same loop one step at a time (one one-launch SQP solve, the
+    plant and the shift per step): the trajectories, the ControllerLog
+    fields and the iteration counts agree (the two differ only in the QP
+    warm polish, which the per-step path restarts per sample as well)."""
+    rng = np.random.default_rng(11)
+    X0 = np.stack([rng.uniform(-.8, .8, 48), rng.uniform(-.4, .4, 48), rng.uniform(-.5, .5, 48),
+                   rng.uniform(-.2, .2, 48)], -1)
+    ctl = mpc.MPCController(30, 0.08, VehicleParameters(), tol=1e-9)
+    pp = VehicleParameters()
+    loop = ClosedLoop(ctl, plant=plant, iters_per_step=30, graph=False,
+                      plant_params=pp)
+    one = loop.run(X0, 8)
+    s = loop._alloc(48, 8)
+    s["xs"][0].copy_(torch.as_tensor(X0, dtype=torch.float64, device=dev))
+    loop._reset(s)
+    for t in range(8):
+        loop._step(s, t)
+    assert torch.equal(one["success"], s["success"])
+    assert torch.equal(one["iters"], s["iters"])
+    for k in ("xs", "us", "state_prediction", "input_prediction"):
+        assert float((one[k] - s[k]).abs().max()) < 1e-12, k
+    assert bool(one["success"].float().mean() > 0.9)
