@@ -159,6 +159,96 @@ __device__ __forceinline__ void project_stage(double* Hl, const double* Qw, cons
     }
 }
 
+// project_stage with its two 6 x 6 work matrices in memory (W, V: 36
+// doubles each, row-major; the one-launch SQP passes dead LDS of the QP's
+// workspace) and plain loops: the same cyclic Jacobi sweeps without the
+// register file the unrolled version needs (it would set the register
+// allocation of a whole fused kernel).  Hl <- V diag(max(lambda, eps)) V' -
+// blkdiag(Q, R) where W = Hl + blkdiag(Q, R) is not positive definite.
+__device__ __forceinline__ void project_stage_mem(double* Hl, const double* Qw, const double* Rw,
+                                                  double eps, double* W, double* V) {
+#pragma unroll 1
+  for (int i = 0; i < 6; ++i)
+#pragma unroll 1
+    for (int j = 0; j < 6; ++j) {
+      const double bd = (i < 4 && j < 4) ? Qw[i * 4 + j] : ((i >= 4 && j >= 4) ? Rw[(i - 4) * 2 + (j - 4)] : 0.0);
+      W[i * 6 + j] = Hl[i * 6 + j] + bd;
+    }
+  // Cholesky test (L in V)
+  bool pd = true;
+#pragma unroll 1
+  for (int j = 0; j < 6; ++j) {
+    double d = W[j * 6 + j];
+#pragma unroll 1
+    for (int k = 0; k < j; ++k) d = fma(-V[j * 6 + k], V[j * 6 + k], d);
+    pd = pd && d > eps;
+    const double ljj = sqrt(fmax(d, eps));
+    V[j * 6 + j] = ljj;
+#pragma unroll 1
+    for (int i = j + 1; i < 6; ++i) {
+      double t = W[i * 6 + j];
+#pragma unroll 1
+      for (int k = 0; k < j; ++k) t = fma(-V[i * 6 + k], V[j * 6 + k], t);
+      V[i * 6 + j] = t / ljj;
+    }
+  }
+  if (pd) return;
+#pragma unroll 1
+  for (int i = 0; i < 36; ++i) V[i] = (i % 7 == 0) ? 1.0 : 0.0;
+#pragma unroll 1
+  for (int sweep = 0; sweep < 8; ++sweep) {
+    double off = 0.0, dia = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < 6; ++i) {
+      dia = fma(W[i * 7], W[i * 7], dia);
+#pragma unroll 1
+      for (int j = i + 1; j < 6; ++j) off = fma(W[i * 6 + j], W[i * 6 + j], off);
+    }
+    if (!(off > 1e-30 * dia)) break;
+#pragma unroll 1
+    for (int pp = 0; pp < 5; ++pp) {
+#pragma unroll 1
+      for (int q = pp + 1; q < 6; ++q) {
+        const double apq = W[pp * 6 + q];
+        if (apq == 0.0) continue;
+        const double th = (W[q * 7] - W[pp * 7]) / (2.0 * apq);
+        const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(fma(th, th, 1.0)));
+        const double c = 1.0 / sqrt(fma(t, t, 1.0)), sn = t * c;
+#pragma unroll 1
+        for (int k = 0; k < 6; ++k) {  // columns pp, q
+          const double wkp = W[k * 6 + pp], wkq = W[k * 6 + q];
+          W[k * 6 + pp] = c * wkp - sn * wkq;
+          W[k * 6 + q] = sn * wkp + c * wkq;
+        }
+#pragma unroll 1
+        for (int k = 0; k < 6; ++k) {  // rows pp, q
+          const double wpk = W[pp * 6 + k], wqk = W[q * 6 + k];
+          W[pp * 6 + k] = c * wpk - sn * wqk;
+          W[q * 6 + k] = sn * wpk + c * wqk;
+        }
+#pragma unroll 1
+        for (int k = 0; k < 6; ++k) {
+          const double vkp = V[k * 6 + pp], vkq = V[k * 6 + q];
+          V[k * 6 + pp] = c * vkp - sn * vkq;
+          V[k * 6 + q] = sn * vkp + c * vkq;
+        }
+      }
+    }
+  }
+#pragma unroll 1
+  for (int i = 0; i < 6; ++i) W[i] = fmax(W[i * 7], eps);  // the eigenvalues, lifted (row 0 of W)
+#pragma unroll 1
+  for (int i = 0; i < 6; ++i)
+#pragma unroll 1
+    for (int j = 0; j < 6; ++j) {
+      double s = 0.0;
+#pragma unroll 1
+      for (int k = 0; k < 6; ++k) s = fma(V[i * 6 + k] * W[k], V[j * 6 + k], s);
+      const double bd = (i < 4 && j < 4) ? Qw[i * 4 + j] : ((i >= 4 && j >= 4) ? Rw[(i - 4) * 2 + (j - 4)] : 0.0);
+      Hl[i * 6 + j] = s - bd;
+    }
+}
+
 // H2, q2 of stage k of instance b (the body of bike_hess_kernel): the
 // Lagrangian curvature of the prediction model's step at (x_k, u_k) weighted
 // by the costate of x_{k+1}, projected per stage in PROJ mode (Qw, Rw given),
@@ -168,7 +258,8 @@ __device__ __forceinline__ void hess_stage(int64_t b, int N, int k, const Bike& 
                                            const double* X, const double* U, const double* pi,
                                            const int32_t* flags, const double* mu,
                                            const int32_t* fix, double fix_rho, const double* Qw,
-                                           const double* Rw, double eps, double* H, double* q) {
+                                           const double* Rw, double eps, double* H, double* q,
+                                           double* pw = nullptr, double* pv = nullptr) {
   const bool exact = flags == nullptr || (flags[b] & kSqpExact);
   const bool proj = Qw && Rw && (flags == nullptr || (flags[b] & kSqpProj));
   if (!exact) {
@@ -181,7 +272,15 @@ __device__ __forceinline__ void hess_stage(int64_t b, int N, int k, const Bike& 
   const double* lam = pi + (b * N + k) * 4;  // costate of x_{k+1} = fe(x_k, u_k)
   double Hl[36];
   model_lag_hess(p, integ, x, u, lam, Hl);
-  if (proj) project_stage(Hl, Qw, Rw, eps);
+  if (proj) {
+    if (pw) {  // work matrices pw, pv and the stage block itself (H) in memory
+      for (int i = 0; i < 36; ++i) H[i] = Hl[i];
+      project_stage_mem(H, Qw, Rw, eps, pw, pv);
+      for (int i = 0; i < 36; ++i) Hl[i] = H[i];
+    } else {
+      project_stage(Hl, Qw, Rw, eps);
+    }
+  }
   if (mu)
     for (int i = 0; i < 6; ++i) Hl[i * 6 + i] += mu[b];
   if (fix) {

@@ -449,11 +449,17 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
     // ------------------------------------------------ 2. stage Hessians
     if (g.hmode != kHessGN) {
       const bool cvx = g.hmode == kHessExact;
+      // the projection's work matrices in stage k's slice of the QP's LDS
+      // workspace, dead between QPs except the active flags GA the warm
+      // polish keeps: fields U..PV (69 doubles) and DA..QU (55)
+      using LQ = ipm::Layout<4, 2>;
+      static_assert(LQ::GA >= 36 && LQ::LO - LQ::DA >= 36, "projection scratch");
       for (int k = lane; k < N; k += kWave)
         hess_stage(b, N, k, p, s.integ, s.X, s.U, s.pi, s.flags, s.mu, s.fix, g.fix_rho,
                    cvx ? s.Q : nullptr, cvx ? s.R : nullptr, g.eps,
                    const_cast<double*>(g.q.H2) + (b * N + k) * 36,
-                   const_cast<double*>(g.q.q2) + (b * N + k) * 6);
+                   const_cast<double*>(g.q.q2) + (b * N + k) * 6,
+                   ipm_lds + (size_t)k * LQ::F + LQ::DA, ipm_lds + (size_t)k * LQ::F);
     }
     wg_fence();
     // ------------------------------------------------------------- 3. QP

@@ -321,6 +321,69 @@ def make_nlp_tail(count=10, min_active=24):
                         xlo=xlo, lbu=lbu)
 
 
+def _oracle_solve_one(args):
+    from oracle import nlp
+    x0, Q, QN, R, xlo, lbu = args
+    ocp = nlp.OCP(30, 0.08, Q, QN, R, xlo, -xlo, lbu, -lbu)
+    U, y, k = ocp.solve(x0)
+    if k >= 1e-9:  # the polish did not contract from the 1e-7 point: Gauss-Newton on to 1e-10
+        U, y, k, _ = ocp.solve_sqp(x0, U0=U, tol=1e-10, hessian="gauss-newton", max_iter=8000)
+        U2, y2, k2 = ocp.newton_polish(x0, U, y, tol=1e-13)
+        if k2 < k:
+            U, y, k = U2, y2, k2
+    return U, y, k, ocp.cost(x0, U)
+
+
+def make_nlp_maxiter(dump=os.path.join(REPO, "gpurun_out", "sqp_straggler.npz")):
+    """The 64 x0 of the nlp bench (seed 20261015 + 6, both slots) that the
+    round-5 device SQP left at MAXITER after 60 iterations, from
+    tools/sqp_straggler.py's dump (per-iteration KKT, flags, mu and QP status of
+    each, run on to convergence): the oracle's optimum of each (oracle/nlp.py:
+    Gauss-Newton SQP to 1e-7, Newton polish to KKT < 1e-12), the device's
+    converged inputs, and a classification --
+      minimum: 0 = the oracle's (|U_dev - U*| < 1e-7), 1 = another local
+               minimum with a lower cost, 2 = another with a higher cost;
+      cause:   0 = slow convergence (at most two switches to the projected
+               curvature), 1 = cycling between the exact and the projected
+               curvature (three or more), with the Gauss-Newton stall before
+               the switch (15 iterations still above KKT 0.3) in gn_stall."""
+    from multiprocessing import Pool
+
+    d = np.load(dump)
+    xlo = np.array([-3.0, -2.0, -2 * np.pi, -0.5])
+    lbu = np.array([-1.0, -0.384])
+    Q = np.diag([1., 6., .2, .05])
+    QN, R = 100 * Q, np.diag([1., .01])
+    X0 = d["x0"]
+    with Pool(8) as pool:
+        res = pool.map(_oracle_solve_one, [(x0, Q, QN, R, xlo, lbu) for x0 in X0])
+    from oracle import nlp
+    ocp = nlp.OCP(30, 0.08, Q, QN, R, xlo, -xlo, lbu, -lbu)
+    U = np.array([r[0] for r in res]); Y = np.array([r[1] for r in res])
+    K = np.array([r[2] for r in res]); J = np.array([r[3] for r in res])
+    Ud = d["U_end"].reshape(len(X0), -1)
+    Jd = np.array([ocp.cost(x0, u) for x0, u in zip(X0, Ud)])
+    dev = np.abs(Ud - U).max(1)
+    minimum = np.where(dev < 1e-7, 0, np.where(Jd < J, 1, 2))
+    fl = d["flags"]
+    # projected-curvature episodes: entries into PROJ mode (flag 8 rising)
+    proj = ((fl[1:] & 8) != 0) & ((fl[:-1] & 8) == 0)
+    n_proj = proj.sum(0) + ((fl[0] & 8) != 0)
+    exact_from = np.argmax((fl & 2) != 0, 0) + 1
+    kk = d["kkt"]
+    gn_stall = np.array([exact_from[j] >= 15 and kk[13, j] > 0.3 for j in range(len(X0))])
+    cause = (n_proj >= 3).astype(int)
+    conv = d["conv_it"][d["idx"]]
+    assert (K < 1e-9).all(), K
+    np.savez_compressed(os.path.join(HERE, "nlp_maxiter.npz"), x0=X0, bench_index=d["idx"],
+                        U=U, y=Y, kkt=K, J=J, U_device=Ud, J_device=Jd, conv_it_r05=conv,
+                        minimum=minimum, cause=cause, gn_stall=gn_stall, n_proj=n_proj,
+                        qp_fail=((d["qp_status"] & 0xFF) != 0).sum(0), N=np.array(30),
+                        ts=np.array(0.08), Q=Q, QN=QN, R=R, xlo=xlo, lbu=lbu)
+    print("minimum", np.bincount(minimum, minlength=3), "cause", np.bincount(cause, minlength=2),
+          "gn_stall", int(gn_stall.sum()), "oracle kkt max", float(K.max()))
+
+
 def make_cfg3_tail(dump=os.path.join(REPO, "tools", "cfg3_tail_inputs.npz")):
     """The config-3 parity tail: the instances of the full B = 65,536 config-3
     batch (seed 20261015 + 3, bicycle linearised about the zero-input rollout;
@@ -376,4 +439,6 @@ if __name__ == "__main__":
         make_cfg3_tail()
     if not only or "nlp_tail" in only:
         make_nlp_tail()
+    if "nlp_maxiter" in only:  # needs tools/sqp_straggler.py's GPU dump
+        make_nlp_maxiter()
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))

@@ -164,3 +164,23 @@ def test_oracle_lam_p_is_value_sensitivity(golden):
             J.append(ocp.cost(xp, Up))
         fd[i] = (J[0] - J[1]) / (2 * h)
     assert np.abs(fd + lp).max() < 1e-5 * (1 + np.abs(lp).max()), (fd, -lp)
+
+
+def test_nlp_maxiter_fixture_certified(golden):
+    """tests/golden/nlp_maxiter.npz (the 64 bench x0 the round-5 device SQP
+    left at MAXITER after 60 iterations): every oracle optimum is a KKT point
+    to 1e-11 on the oracle's own evaluation, and where the device converged
+    to another local minimum (minimum == 1) that point is a KKT point too,
+    with a lower cost (none is higher: minimum == 2 never occurs)."""
+    from oracle import nlp
+
+    g = golden("nlp_maxiter.npz")
+    ocp = nlp.OCP(int(g["N"]), float(g["ts"]), g["Q"], g["QN"], g["R"], g["xlo"], -g["xlo"],
+                  g["lbu"], -g["lbu"])
+    assert g["x0"].shape == (64, 4) and (g["minimum"] != 2).all()
+    for i in range(0, 64, 4):  # every fourth: the KKT evaluation is complex-step heavy
+        x0 = g["x0"][i]
+        assert ocp.kkt(x0, g["U"][i], g["y"][i]) < 1e-11, i
+        assert abs(ocp.cost(x0, g["U"][i]) - g["J"][i]) < 1e-9 * (1 + abs(g["J"][i]))
+    other = np.nonzero(g["minimum"] == 1)[0]
+    assert (g["J_device"][other] < g["J"][other]).all()
