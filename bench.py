@@ -955,7 +955,7 @@ class ConfigLoop:
     dname = "f64"
     default_batch = 1024
     default_slots = 2
-    default_sqp_iters = 60  # per sample (a cap: each instance stops at its own convergence)
+    default_sqp_iters = 100  # per sample (a cap: each instance stops at its own convergence)
     default_steps = (3, 1)  # one step is a whole episode
 
     def __init__(self, args, dev, rank):
@@ -969,7 +969,10 @@ class ConfigLoop:
         bsz, S = args.batch, args.slots
         self.ctl = MPCController(self.N, 0.08, VehicleParameters(), tol=1e-9,
                                  fused=not args.sqp_iterate)
-        self.loop = ClosedLoop(self.ctl, plant="fe", iters_per_step=args.sqp_iters, graph=False)
+        # the cold first sample gets the nlp line's cap (a cap: each instance stops at its own
+        # convergence)
+        self.loop = ClosedLoop(self.ctl, plant="fe", iters_per_step=args.sqp_iters, graph=False,
+                               iters_first=max(args.sqp_iters, ConfigNLP.default_sqp_iters))
         rng = np.random.default_rng(20261015 + 7 + 1000 * rank)
         self.X0 = np.stack([rng.uniform(-.8, .8, (S, bsz)), rng.uniform(-.4, .4, (S, bsz)),
                             rng.uniform(-.5, .5, (S, bsz)), rng.uniform(-.2, .2, (S, bsz))], -1)

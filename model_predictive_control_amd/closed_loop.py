@@ -53,8 +53,11 @@ class ClosedLoop:
         self.plant_params = plant_params or controller.params
         self.substeps = int(substeps)
         self.iters = int(iters_per_step)
+        # the cold first step: the controller's own budget when the SQP runs
+        # in one launch (a cap: each instance stops at its own convergence),
+        # else at most 60 batch-wide iterations
         self.iters_first = int(iters_first) if iters_first is not None else \
-            max(self.iters, min(controller.max_iter, 60))
+            max(self.iters, controller.max_iter if controller.fused else min(controller.max_iter, 60))
         self.graph = graph
         self._graphs: dict = {}
 
