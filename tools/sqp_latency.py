@@ -66,6 +66,15 @@ def main():
                           sqp_iters_mean=round(float(its.mean()), 2),
                           warm_qp_frac=round(float(hits.sum() / its.sum()), 3),
                           sum_inst_ms=round(float(tot.sum()) * TICK_US / 1e3, 1))), flush=True)
+    if os.environ.get("MPCQP_LIB", "").endswith("passclk.so"):
+        # the timing build's per-pass clocks: in the workspace after the stage data
+        off = b * N * 70
+        pc = sqp.ws.view(torch.float64)[off:off + 7 * b].view(torch.int64).view(b, 7).cpu().numpy()
+        names = ["pass1_backward_factor", "pass2_fwd_predictor", "pass3_bwd_corrector_rhs",
+                 "pass4_fwd_corrector", "polish", "refactor_and_head", "start_and_warm_polish"]
+        totq = pc.sum()
+        print("PASSCLK", json.dumps({n: round(float(pc[:, i].sum() / totq), 3) for i, n in enumerate(names)}),
+              flush=True)
     for i in np.argsort(-tot)[:8]:
         print(json.dumps(dict(inst=int(i), us=round(tot[i] * TICK_US, 1), qp_us=round(tqp[i] * TICK_US, 1),
                               ipm_iters=int(ipm[i]), sqp_iters=int(its[i]), ok=bool(ok[i]))), flush=True)
