@@ -849,7 +849,7 @@ class ConfigNLP:
                    FP64_PEAK_TFS, "TFLOP/s", traffic.get("sqp_solve"),
                    {"flops_per_launch": flops, "avg_launch_us": round(t_s * 1e3, 2),
                     "note": "one single-wave workgroup per instance runs its SQP to convergence "
-                            "(QP: interior point on one DPP quad, horizon in LDS; linearisation, "
+                            "(QP: interior point on the whole wave, per-stage work on 16 quads and the Riccati chains on one, horizon in LDS; linearisation, "
                             "Hessian and line search one lane per stage); flops = 1080 per stage "
                             "per interior-point iteration summed over the instances' own counts "
                             "(warm polishes, Hessians and line searches not counted): latency-bound"})

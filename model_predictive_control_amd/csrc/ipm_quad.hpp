@@ -362,7 +362,14 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i, bool wa
 #else
   constexpr int kPolishEarly = kSteps;  // (off: every round runs all four steps)
 #endif
-  for (int round = 0; round < kRounds; ++round) {
+#ifdef MPCQP_WARM_ROUNDS
+  // a warm polish whose active set needs corrections hands over to the
+  // interior point after this many rounds (timing builds)
+  const int rounds = warm ? MPCQP_WARM_ROUNDS : kRounds;
+#else
+  const int rounds = kRounds;
+#endif
+  for (int round = 0; round < rounds; ++round) {
     bool good = true, changed = false;
     for (int step = 0; step < kSteps; ++step) {
       const double rho = step == 0 ? 1e8 : (step == 1 ? 1e6 : 1e4);

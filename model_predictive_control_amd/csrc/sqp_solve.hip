@@ -8,8 +8,9 @@
 // single-wave workgroup runs one instance's iterations back to back:
 //   1. rollout of U and the per-stage linearisation A_k, B_k, c_k;
 //   2. the stage Hessians H2_k, q2_k (exact-Hessian iterations);
-//   3. the QP on the interior point, four lanes per instance, the horizon in
-//      LDS (ipmq::solve_quad, the kernel of mpcqp_mpc_ipm);
+//   3. the QP on the interior point, the horizon in LDS (ipmw::solve_wave:
+//      ipmq::solve_quad's algorithm with the per-stage work on all 16 quads
+//      and the Riccati chains on one);
 //   4. the merit line search, update and KKT residual (sqp_step_one, the
 //      body of mpcqp_bicycle_sqp_step)
 // until the KKT residual is below tol or max_iter iterations.  The launch
@@ -19,8 +20,8 @@
 // the four-launch iteration, so the iterates are those of SqpSolver.iterate
 // with the linearisation of mpcqp_bicycle_linearise.
 //
-// Lanes: 0..3 (one DPP quad; 4..63 exit at once).  The rollout runs on every
-// lane; stage k's Jacobians and Hessian on lane k % 4; the step on lane 0.
+// Lanes: the whole wave.  Stage k's trig terms, Jacobians and Hessian on lane
+// k; the QP's per-stage work on quad k % 16; the scalar scans on lane 0.
 // Data between the phases goes through the caller's workspace (HBM) with a
 // workgroup-scope fence after each phase (one wave: no barrier needed).
 #include <algorithm>
@@ -38,6 +39,14 @@
 #endif
 #include "ipm_lane.hpp"
 #include "ipm_quad.hpp"
+// the QPs on the whole wave (ipm_wave.hpp: per-stage work on 16 quads, the
+// Riccati chains on one): A/B on the nlp line (tools/sqp_knobs.py, the quad
+// solver built with -DMPCQP_IPM_QUAD): sum of instance times 113.4 -> 73.8 s
+// with the interior point alone, launch 259 -> 170 ms, the same fixture optima
+#ifndef MPCQP_IPM_QUAD
+#define MPCQP_IPM_WAVE 1
+#include "ipm_wave.hpp"
+#endif
 
 namespace mpcqp {
 
@@ -80,7 +89,6 @@ __device__ __forceinline__ void wg_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ
 // workspace (kScr doubles per stage, N + 1 stages, then the broadcast slots).
 constexpr int kScr = 14;
 enum { kU0 = 0, kU1, kBeta, kSb, kPx, kPy, kPsi, kV, kSt, kCt, kTJ, kTV, kL0, kL1 };
-constexpr int kScrBcast = 8;
 
 __device__ __forceinline__ double* scr_at(double* scr, int k) { return scr + k * kScr; }
 
@@ -485,6 +493,22 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
       for (int k = lane >> 2; k < N; k += kWave / 4) ipmq::stage_in_q(g.q, (int)b, at, lane & 3, k);
     }
     wave_lds_sync();
+#ifdef MPCQP_IPM_WAVE
+    {
+      const int fl = s.flags[b];
+      const bool use_warm = warm && (g.warm == 3 || (g.warm >= 1 && !(fl & kSqpExact)) ||
+                                     (g.warm == 2 && s.kkt[b] < g.warm_kkt));
+      warm = ipmw::solve_wave<double>(g.q, (int)b, ipm_lds, use_warm,
+#ifdef MPCQP_IPM_PASSCLK
+                                      clk.pass
+#else
+                                      nullptr
+#endif
+      );
+      if (lane == 0)
+        clk.warm_hits += (use_warm && warm && ((g.q.status[b] >> 8) & 0xFFFF) == 0) ? 1 : 0;
+    }
+#else
     if (lane < 4) {
       const int fl = s.flags[b];
       const bool use_warm = warm && (g.warm == 3 || (g.warm >= 1 && !(fl & kSqpExact)) ||
@@ -498,6 +522,7 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
                                          true);
       clk.warm_hits += (use_warm && warm && ((g.q.status[b] >> 8) & 0xFFFF) == 0) ? 1 : 0;
     }
+#endif
     wg_fence();
     clk.tqp += __builtin_amdgcn_s_memrealtime() - q0;
     clk.ipm_its += (g.q.status[b] >> 8) & 0xFFFF;
