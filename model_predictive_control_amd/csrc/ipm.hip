@@ -23,6 +23,7 @@
 #define MPCQP_HD __host__ __device__
 #include "ipm_lane.hpp"
 #include "ipm_quad.hpp"
+#include "ipm_wave.hpp"
 
 namespace mpcqp {
 
@@ -77,6 +78,30 @@ __global__ __launch_bounds__(64, 1) void ipm_quad_kernel(ipm::Args<T> a) {
   const int b = blockIdx.x * G + g;
   if (b >= a.batch) return;
   ipmq::solve_quad<T, G>(a, b, ipm_lds + g);
+}
+
+// One instance per single-wave workgroup on the whole wave (ipm_wave.hpp):
+// the stage data staged one quad per stage, the per-stage work of every pass
+// on the 16 quads, the Riccati chains on quad 0.  Same iterates as
+// ipm_quad_kernel<T, 1> up to the summation order of the reductions.
+template <typename T>
+__global__ __launch_bounds__(64, 1) void ipm_wave_kernel(ipm::Args<T> a) {
+  extern __shared__ __attribute__((aligned(16))) double ipm_lds[];
+  const int lane = threadIdx.x;
+  const ipmq::WsQ<1> at(ipm_lds, lane & 3);
+  auto one = [&](int b) {
+    if (a.skip && (a.skip[b] & a.skip_mask)) return;
+    for (int k = lane >> 2; k < a.N; k += kWave / 4) ipmq::stage_in_q(a, b, at, lane & 3, k);
+    wave_lds_sync();
+    ipmw::solve_wave<T>(a, b, ipm_lds);
+    wave_lds_sync();
+  };
+  if (a.list) {
+    const int cnt = *a.list_count;
+    for (int k = a.list_begin + blockIdx.x; k < cnt; k += gridDim.x) one(a.list[k]);
+    return;
+  }
+  if ((int)blockIdx.x < a.batch) one((int)blockIdx.x);
 }
 
 static int64_t ipm_ldb(int batch) { return ((int64_t)batch + 63) / 64 * 64; }
@@ -135,6 +160,8 @@ static int ipm_quad_launch(ipm::Args<T>& a, hipStream_t st) {
     if ((g == 1 || g == 2 || g == 4) && (size_t)g * per <= 160 * 1024) G = g;
   }
   const size_t bytes = (size_t)G * per;
+  const char* wenv = getenv("MPCQP_IPM_WAVE");  // A/B: 0 = the quad kernel at G = 1
+  const bool wave = G == 1 && !(wenv && atoi(wenv) == 0);
   auto launch = [&](auto kern) -> int {
     if (bytes > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -147,6 +174,7 @@ static int ipm_quad_launch(ipm::Args<T>& a, hipStream_t st) {
   };
   if (G == 4) return launch(ipm_quad_kernel<T, 4>);
   if (G == 2) return launch(ipm_quad_kernel<T, 2>);
+  if (wave) return launch(ipm_wave_kernel<T>);
   return launch(ipm_quad_kernel<T, 1>);
 }
 
