@@ -58,6 +58,15 @@ struct PhaseClock {
 
 constexpr int kWave = 64;  // CDNA wavefront width (hard-coded, never warpSize)
 
+// DPP moves: old value 0 with bound_ctrl set.  A lane whose source is out of
+// range (or disabled) gets 0 either way, but with bound_ctrl clear the
+// compiler must first materialise the old value 0 in the destination -- one
+// v_mov per DPP move (60 of the 462 instructions of the SQP kernel's serial
+// Riccati step).  -DMPCQP_DPP_BC=false restores the old encoding (A/B builds).
+#ifndef MPCQP_DPP_BC
+#define MPCQP_DPP_BC true
+#endif
+
 // LDS exchange inside the single-wave workgroup: a wave's LDS operations
 // execute in issue order, so only the compiler must not move them (no
 // s_barrier, and no fence that would drain the outstanding global loads)
@@ -128,13 +137,13 @@ __device__ __forceinline__ unsigned lane_id() {
 template <int X>
 __device__ __forceinline__ int lane_step(int v) {
   if constexpr (X == 1) {
-    return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);
+    return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, MPCQP_DPP_BC);
   } else if constexpr (X == 2) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);
+    return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, MPCQP_DPP_BC);
   } else if constexpr (X == 4) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);
+    return __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, MPCQP_DPP_BC);
   } else if constexpr (X == 8) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);
+    return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, MPCQP_DPP_BC);
   } else if constexpr (X == 16) {
     const auto s = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
     return (int)((lane_id() & 16) ? s[0] : s[1]);

@@ -83,8 +83,8 @@ __device__ __forceinline__ V pick(const V (&x)[NR], int i) {
 template <int CTRL>
 __device__ __forceinline__ double dppd(double v) {
   const long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffffll), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffffll), CTRL, 0xF, 0xF, MPCQP_DPP_BC);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xF, 0xF, MPCQP_DPP_BC);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 

@@ -37,6 +37,11 @@
 //     instead of O((n+m)^2) reads.
 #include <cstdlib>
 
+// DPP moves keep the old encoding here (bound_ctrl clear, common.hpp): A/B on
+// config 5 (tools/ab_run.sh 5 dppold, 200-step lines): the new encoding made
+// qp_pf_kernel 3.97 -> 4.14 ms, while every other kernel gained 0.5-5 %
+#define MPCQP_DPP_BC false
+
 #include "mfma.hpp"
 #include "pfdyn.hpp"
 

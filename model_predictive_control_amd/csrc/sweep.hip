@@ -58,7 +58,7 @@ __device__ __forceinline__ mf4 mm(const mf4& p, const mf4& y, mf4 acc) {
 template <int P>
 __device__ __forceinline__ float row_bcast(float v) {
   // lane P of each 16-lane row to the whole row
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + P, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + P, 0xf, 0xf, MPCQP_DPP_BC));
 }
 
 // Inverse Cholesky factor of a symmetric positive definite 16 x 16 C-layout

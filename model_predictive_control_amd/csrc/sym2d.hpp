@@ -21,18 +21,18 @@ namespace mpcqp {
 // (i <-> i+8 within a 16-lane row, i.e. xor 8).
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, MPCQP_DPP_BC));
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, MPCQP_DPP_BC);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, MPCQP_DPP_BC);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 template <int CTRL>
 __device__ __forceinline__ int dpp(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, MPCQP_DPP_BC);
 }
 
 // Sum over the 8 lanes of a row block (lanes bi*8 .. bi*8+7); every lane of
