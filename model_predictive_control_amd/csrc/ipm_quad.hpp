@@ -127,13 +127,13 @@ MPCQP_QD bool inv2(const double (&G)[3], double (&Gi)[3]) {
 // later stages), ph_i, e_i, gx (the state gradient g_x[i]), gu[2] (input
 // gradients, replicated), sx (Sigma of state comp i), su2[2] (Sigma of the
 // inputs, replicated).  Out: P row i, p_i, K (2 x 4, replicated), kk, Gi,
-// and Ph, ph overwritten with the cost-to-go of x_k.
+// Kc = column i of K, and Ph, ph overwritten with the cost-to-go of x_k.
 template <class W>
 MPCQP_QD bool riccati_q(const W& at, const StageQ& S, int k, int i, double (&Ph)[4], double& ph,
                         double e,
                         double gx, const double (&gu)[2], double sx, const double (&su2)[2],
                         double dreg, double (&P)[4], double& p, double (&K)[2][4],
-                        double (&kk)[2], double (&Gi)[3]) {
+                        double (&kk)[2], double (&Gi)[3], double (&Kc)[2]) {
   // P_{k+1} row i = Q' + H2xx_{k+1} + Sigma_x + Ph,  p = g_x + ph
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -206,20 +206,32 @@ MPCQP_QD bool riccati_q(const W& at, const StageQ& S, int k, int i, double (&Ph)
     for (int j = 0; j < 4; ++j) K[r][j] = -(Gi[pk(r, 0)] * Hx[0][j] + Gi[pk(r, 1)] * Hx[1][j]);
     kk[r] = -(Gi[pk(r, 0)] * h[0] + Gi[pk(r, 1)] * h[1]);
   }
-  // row i of the cost-to-go of x_k: A'PA + Hx'K,  ph_i = (A'Pe)_i + (Hx'kk)_i
-  double Hxi[2];
+  // row i of the cost-to-go of x_k: A'PA + Hx'K,  ph_i = (A'Pe)_i + (Hx'kk)_i.
+  // Column i of Hx from the lane's own column of A: (B'PA)_ri = (A'PB)_ir
+  // (P symmetric) -- a runtime-indexed select of the replicated Hx compiled
+  // to exec-mask branches
+  double Ai[4], Hxi[2];
 #pragma unroll
-  for (int r = 0; r < 2; ++r) Hxi[r] = sel4(Hx[r], i);
+  for (int q = 0; q < 4; ++q) Ai[q] = at.r(k, L::DA + q * NX);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    double t = at.rb(k, L::WXU + r);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t = fma(Ai[q], PBa[q][r], t);
+    Hxi[r] = t;
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) Kc[r] = -(Gi[pk(r, 0)] * Hxi[0] + Gi[pk(r, 1)] * Hxi[1]);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     double s = 0.0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s = fma(at.r(k, L::DA + q * NX), PAa[q][j], s);
+    for (int q = 0; q < 4; ++q) s = fma(Ai[q], PAa[q][j], s);
     Ph[j] = fma(Hxi[1], K[1][j], fma(Hxi[0], K[0][j], s));
   }
   double s = 0.0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) s = fma(at.r(k, L::DA + q * NX), Pea[q], s);
+  for (int q = 0; q < 4; ++q) s = fma(Ai[q], Pea[q], s);
   ph = fma(Hxi[1], kk[1], fma(Hxi[0], kk[0], s));
   return ok;
 }
@@ -227,13 +239,13 @@ MPCQP_QD bool riccati_q(const W& at, const StageQ& S, int k, int i, double (&Ph)
 // Store the factor data of stage k (lane i: its rows / columns).
 template <class W>
 MPCQP_QD void store_factor_q(const W& at, int k, int i, const double (&P)[4], double p,
-                             const double (&K)[2][4], const double (&kk)[2], const double (&Gi)[3],
+                             const double (&Kc)[2], const double (&kk)[2], const double (&Gi)[3],
                              double e) {
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     if (j <= i) at.p(k, L::PP, j) = P[j];
 #pragma unroll
-  for (int r = 0; r < 2; ++r) at.r(k, L::KM + r * NX) = sel4(K[r], i);
+  for (int r = 0; r < 2; ++r) at.r(k, L::KM + r * NX) = Kc[r];
   at.r(k, L::E) = e;
   at.r(k, L::PV) = p;
   if (i < 2) at.r(k, L::KV) = sel2(kk, i);
@@ -412,9 +424,9 @@ MPCQP_QD bool polish_q(const Args<T>& a, const W& at, int i, double x0i, bool wa
         double su2[2] = {qb<0>(sui), qb<1>(sui)};
         gu[0] += qb<0>(gum);
         gu[1] += qb<1>(gum);
-        double P[4], p, K[2][4], kk[2], Gi[3];
-        good = riccati_q(at, S, k, i, Ph, ph, e, gx, gu, sx, su2, 0.0, P, p, K, kk, Gi) && good;
-        store_factor_q(at, k, i, P, p, K, kk, Gi, e);
+        double P[4], p, K[2][4], kk[2], Gi[3], Kc[2];
+        good = riccati_q(at, S, k, i, Ph, ph, e, gx, gu, sx, su2, 0.0, P, p, K, kk, Gi, Kc) && good;
+        store_factor_q(at, k, i, P, p, Kc, kk, Gi, e);
         gx1 = next_gx1_q(at, S, k, i, pia, ua);
       }
       const bool last = step == kSteps - 1;
@@ -697,10 +709,10 @@ MPCQP_QD bool solve_quad(const Args<T>& a, int b, double* W, bool warm = false,
         at.r(k, L::GA) = gui;
       }
       const double su2[2] = {qb<0>(sui), qb<1>(sui)};
-      double P[4], p, K[2][4], kk[2], Gi[3];
-      const bool ok = riccati_q(at, S, k, i, Ph, ph, e, gx, gu, sx, su2, dreg, P, p, K, kk, Gi);
+      double P[4], p, K[2][4], kk[2], Gi[3], Kc[2];
+      const bool ok = riccati_q(at, S, k, i, Ph, ph, e, gx, gu, sx, su2, dreg, P, p, K, kk, Gi, Kc);
       pd = pd && ok;
-      store_factor_q(at, k, i, P, p, K, kk, Gi, e);
+      store_factor_q(at, k, i, P, p, Kc, kk, Gi, e);
       gx1 = next_gx1_q(at, S, k, i, pia, ua);
     }
     rstat = qmax(rstat);

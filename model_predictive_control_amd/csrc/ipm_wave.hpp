@@ -182,9 +182,9 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
           const double e = at.r(k, L::E), gx = at.r(k, L::PV), sx = at.r(k, L::KM);
           const double gu[2] = {at(k, L::KV), at(k, L::KV + 1)};
           const double su2[2] = {at(k, L::GI), at(k, L::GI + 1)};
-          double P[4], p, K[2][4], kk[2], Gi[3];
-          good = riccati_q(at, S, k, i, Ph, ph, e, gx, gu, sx, su2, 0.0, P, p, K, kk, Gi) && good;
-          store_factor_q(at, k, i, P, p, K, kk, Gi, e);
+          double P[4], p, K[2][4], kk[2], Gi[3], Kc[2];
+          good = riccati_q(at, S, k, i, Ph, ph, e, gx, gu, sx, su2, 0.0, P, p, K, kk, Gi, Kc) && good;
+          store_factor_q(at, k, i, P, p, Kc, kk, Gi, e);
         }
         forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&)[4]) {
           at.r(k, L::E) = dxn;
@@ -422,10 +422,10 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
         const double e = at.r(k, L::E), gx = at.r(k, L::GA + NU), sx = at.r(k, L::DXA);
         const double gu[2] = {at(k, L::GA), at(k, L::GA + 1)};
         const double su2[2] = {at(k, L::DUA), at(k, L::DUA + 1)};
-        double P[4], p, K[2][4], kk[2], Gi[3];
-        const bool ok = riccati_q(at, S, k, i, Ph, ph, e, gx, gu, sx, su2, dreg, P, p, K, kk, Gi);
+        double P[4], p, K[2][4], kk[2], Gi[3], Kc[2];
+        const bool ok = riccati_q(at, S, k, i, Ph, ph, e, gx, gu, sx, su2, dreg, P, p, K, kk, Gi, Kc);
         pd = pd && ok;
-        store_factor_q(at, k, i, P, p, K, kk, Gi, e);
+        store_factor_q(at, k, i, P, p, Kc, kk, Gi, e);
       }
     }
     pd = from_lane0(pd);
