@@ -176,8 +176,8 @@ MPCQP_QD bool riccati_q(const W& at, const StageQ& S, int k, int i, double (&Ph)
     PAa[3][j] = qb<3>(PA[j]);
   }
   bcast4(Pe, Pea);
-  // replicated: G = R + H2uu + Sigma_u + B'PB, h = g_u + B'Pe, Hx = H2xu' + B'PA
-  double G[3], h[2], Hx[2][4];
+  // replicated: G = R + H2uu + Sigma_u + B'PB, h = g_u + B'Pe
+  double G[3], h[2];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
 #pragma unroll
@@ -191,25 +191,14 @@ MPCQP_QD bool riccati_q(const W& at, const StageQ& S, int k, int i, double (&Ph)
 #pragma unroll
     for (int q = 0; q < 4; ++q) s = fma(S.B[q][r], Pea[q], s);
     h[r] = s;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      double t = S.WXU[j][r];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) t = fma(S.B[q][r], PAa[q][j], t);
-      Hx[r][j] = t;
-    }
   }
   const bool ok = inv2(G, Gi);
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) K[r][j] = -(Gi[pk(r, 0)] * Hx[0][j] + Gi[pk(r, 1)] * Hx[1][j]);
-    kk[r] = -(Gi[pk(r, 0)] * h[0] + Gi[pk(r, 1)] * h[1]);
-  }
-  // row i of the cost-to-go of x_k: A'PA + Hx'K,  ph_i = (A'Pe)_i + (Hx'kk)_i.
-  // Column i of Hx from the lane's own column of A: (B'PA)_ri = (A'PB)_ir
-  // (P symmetric) -- a runtime-indexed select of the replicated Hx compiled
-  // to exec-mask branches
+  for (int r = 0; r < 2; ++r) kk[r] = -(Gi[pk(r, 0)] * h[0] + Gi[pk(r, 1)] * h[1]);
+  // column i of Hx = H2xu' + B'PA from the lane's own column of A:
+  // (B'PA)_ri = (A'PB)_ir (P symmetric); the gains K = -G^-1 Hx by columns
+  // (Kc, lane i), then to every lane -- replicating Hx and K on the four lanes
+  // cost 48 VALU per stage against 16 DPP moves
   double Ai[4], Hxi[2];
 #pragma unroll
   for (int q = 0; q < 4; ++q) Ai[q] = at.r(k, L::DA + q * NX);
@@ -221,7 +210,11 @@ MPCQP_QD bool riccati_q(const W& at, const StageQ& S, int k, int i, double (&Ph)
     Hxi[r] = t;
   }
 #pragma unroll
-  for (int r = 0; r < 2; ++r) Kc[r] = -(Gi[pk(r, 0)] * Hxi[0] + Gi[pk(r, 1)] * Hxi[1]);
+  for (int r = 0; r < 2; ++r) {
+    Kc[r] = -(Gi[pk(r, 0)] * Hxi[0] + Gi[pk(r, 1)] * Hxi[1]);
+    bcast4(Kc[r], K[r]);
+  }
+  // row i of the cost-to-go of x_k: A'PA + Hx'K,  ph_i = (A'Pe)_i + (Hx'kk)_i
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     double s = 0.0;
@@ -567,7 +560,9 @@ MPCQP_QD void stage_in_q(const Args<T>& a, int b, const W& at, int i, int k) {
 // interior point runs only if that is not a certified vertex.  Returns true
 // when the QP ended polished (its active set is then in GA for the next one).
 // MPCQP_IPM_PASSCLK (timing builds, tools/sqp_latency.py): s_memrealtime
-// ticks of the four passes and of the polish accumulated into pclk[0..4]
+// ticks accumulated into pclk[0..7]: the four passes, the polish, factorisations
+// that failed the inertia test (solve_wave; solve_quad: + the loop head), the
+// start, the warm polish (solve_wave)
 #ifdef MPCQP_IPM_PASSCLK
 #define MPCQP_PCLK(i) do { if (pclk) { const uint64_t _t = __builtin_amdgcn_s_memrealtime(); pclk[i] += _t - pclk_t; pclk_t = _t; } } while (0)
 #else

@@ -68,6 +68,46 @@ MPCQP_QD bool from_lane0(bool v) { return __builtin_amdgcn_readfirstlane(v ? 1 :
 
 constexpr int kQuads = kWave / 4;
 
+// The backward sweep of a right-hand side on the stored factorisation (quad
+// 0; pass 3 of the interior point, solve_quad's expressions): g_x row i from
+// field FGX (lane-relative), g_u (both inputs) from FGU; writes k -> KV and
+// p -> PV (each stage's fields are read before they are written).
+template <int FGX, int FGU>
+MPCQP_QD void rhs_sweep_q(const WsQ<1>& at, int N, int i) {
+  const bool ou = i < NU;
+  double phc = 0.0;
+  for (int k = N - 1; k >= 0; --k) {
+    const double gx = at.r(k, FGX);
+    const double gu[2] = {at(k, FGU), at(k, FGU + 1)};
+    const double p = gx + phc;
+    double Pe = p;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) Pe = fma(at.p(k, L::PP, j), at(k, L::E + j), Pe);
+    double Pea[4];
+    bcast4(Pe, Pea);
+    double h[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      double s = gu[r];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s = fma(at(k, L::DB + q * NU + r), Pea[q], s);
+      h[r] = s;
+    }
+    const double Gi[3] = {at(k, L::GI + 0), at(k, L::GI + 1), at(k, L::GI + 2)};
+    double kk[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) kk[r] = -(Gi[pk(r, 0)] * h[0] + Gi[pk(r, 1)] * h[1]);
+    if (ou) at.r(k, L::KV) = sel2(kk, i);
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s = fma(at.r(k, L::DA + q * NX), Pea[q], s);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) s = fma(at.r(k, L::KM + r * NX), h[r], s);
+    phc = s;
+    at.r(k, L::PV) = p;
+  }
+}
+
 // polish_q (ipm_quad.hpp) on the whole wave: each method-of-multipliers step
 // is the per-stage residual / gradient / penalty (one quad per stage, into
 // the factor fields the serial sweep overwrites after reading: e -> E, g_x ->
@@ -118,6 +158,8 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
     bool good = true, changed = false;
     for (int step = 0; step < kSteps; ++step) {
       const double rho = step == 0 ? 1e8 : (step == 1 ? 1e6 : 1e4);
+      // the last step keeps the penalty of the one before: same factorisation
+      const bool refactor = step < 3;
       // per stage: residual, gradients and the active components' penalty
       for (int k = qd; k < N; k += kQuads) {
         const double xi = at.r(k, L::DX), pii = at.r(k, L::DPI);
@@ -167,14 +209,14 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
         gu[1] += qb<1>(gum);
         at.r(k, L::E) = e;
         at.r(k, L::PV) = gx;
-        at.r(k, L::KM) = sx;
-        if (ou) {
-          at.r(k, L::KV) = sel2(gu, i);
-          at.r(k, L::GI) = sui;
+        if (ou) at.r(k, L::KV) = sel2(gu, i);
+        if (refactor) {  // (a kept factorisation keeps its K and G^-1 fields)
+          at.r(k, L::KM) = sx;
+          if (ou) at.r(k, L::GI) = sui;
         }
       }
       wave_lds_sync();
-      if (q0) {
+      if (q0 && refactor) {
         double Ph[4] = {0.0, 0.0, 0.0, 0.0}, ph = 0.0;
         for (int k = N - 1; k >= 0; --k) {
           StageQ S;
@@ -186,6 +228,12 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
           good = riccati_q(at, S, k, i, Ph, ph, e, gx, gu, sx, su2, 0.0, P, p, K, kk, Gi, Kc) && good;
           store_factor_q(at, k, i, P, p, Kc, kk, Gi, e);
         }
+      } else if (q0) {
+        // the penalty and the active set of the previous step: its factors
+        // stand, only the right-hand side is swept (e back in E first)
+        rhs_sweep_q<L::PV, L::KV>(at, N, i);
+      }
+      if (q0) {
         forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&)[4]) {
           at.r(k, L::E) = dxn;
           at.r(k, L::DX) += dxn;
@@ -305,7 +353,9 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
   wave_lds_sync();
   MPCQP_PCLK(6);
   if (warm && mcount > 0.0) {
-    if (polish_w<T>(a, at, qd, i, x0i, true)) {
+    const bool wp = polish_w<T>(a, at, qd, i, x0i, true);
+    MPCQP_PCLK(7);
+    if (wp) {
       if (q0) emit_q<T>(a, b, at, i, true, MPCQP_STATUS_OPTIMAL, 0);
       return true;
     }
@@ -317,7 +367,6 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
   int ncorr = 0;
   const int max_iter = a.max_iter;
   for (int it = 0;; ++it) {
-    MPCQP_PCLK(5);
     // ========================= pass 1a: per stage, the neighbours' values
     // x_k after the previous step (stage k-1's state, not yet updated in
     // solve_quad's backward order) -> E; the later stage's A'pi + H2xu u
@@ -443,6 +492,7 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
         if (q0) emit_q<T>(a, b, at, i, false, MPCQP_STATUS_NOT_CONVEX, it);
         return false;
       }
+      MPCQP_PCLK(5);
       alpha = 0.0;
       continue;
     }
@@ -545,39 +595,7 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
       at.r(k, L::GA + NU) = gx;
     }
     wave_lds_sync();
-    if (q0) {
-      double phc = 0.0;
-      for (int k = N - 1; k >= 0; --k) {
-        const double gx = at.r(k, L::GA + NU);
-        const double gu[2] = {at(k, L::GA), at(k, L::GA + 1)};
-        const double p = gx + phc;
-        double Pe = p;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Pe = fma(at.p(k, L::PP, j), at(k, L::E + j), Pe);
-        double Pea[4];
-        bcast4(Pe, Pea);
-        double h[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          double s = gu[r];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) s = fma(at(k, L::DB + q * NU + r), Pea[q], s);
-          h[r] = s;
-        }
-        const double Gi[3] = {at(k, L::GI + 0), at(k, L::GI + 1), at(k, L::GI + 2)};
-        double kk[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) kk[r] = -(Gi[pk(r, 0)] * h[0] + Gi[pk(r, 1)] * h[1]);
-        if (ou) at.r(k, L::KV) = sel2(kk, i);
-        double s = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s = fma(at.r(k, L::DA + q * NX), Pea[q], s);
-#pragma unroll
-        for (int r = 0; r < 2; ++r) s = fma(at.r(k, L::KM + r * NX), h[r], s);
-        phc = s;
-        at.r(k, L::PV) = p;
-      }
-    }
+    if (q0) rhs_sweep_q<L::GA + NU, L::GA>(at, N, i);
     wave_lds_sync();
 
     MPCQP_PCLK(2);

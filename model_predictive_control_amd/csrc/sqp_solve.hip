@@ -402,7 +402,7 @@ struct SolveClock {
   uint64_t tqp = 0;
   int64_t ipm_its = 0, warm_hits = 0, sqp_its = 0;
 #ifdef MPCQP_IPM_PASSCLK
-  uint64_t pass[7] = {0, 0, 0, 0, 0, 0, 0};  // passes 1-4, polish, rest, start (timing builds)
+  uint64_t pass[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // passes 1-4, polish, failed factorisations, start, warm polish (timing builds)
 #endif
 };
 
@@ -547,7 +547,7 @@ __device__ __forceinline__ void write_clock(const SqpSolveArgs& g, int64_t b, ui
     st[3] = clk.sqp_its | (clk.warm_hits << 32);
 #ifdef MPCQP_IPM_PASSCLK
     // (the workspace region of g.Xr, unused by sqp_solve_kernel)
-    for (int i = 0; i < 7; ++i) reinterpret_cast<int64_t*>(g.Xr)[b * 7 + i] = (int64_t)clk.pass[i];
+    for (int i = 0; i < 8; ++i) reinterpret_cast<int64_t*>(g.Xr)[b * 8 + i] = (int64_t)clk.pass[i];
 #endif
   }
 }

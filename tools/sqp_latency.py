@@ -69,9 +69,9 @@ def main():
     if os.environ.get("MPCQP_LIB", "").endswith("passclk.so"):
         # the timing build's per-pass clocks: in the workspace after the stage data
         off = b * N * 70
-        pc = sqp.ws.view(torch.float64)[off:off + 7 * b].view(torch.int64).view(b, 7).cpu().numpy()
+        pc = sqp.ws.view(torch.float64)[off:off + 8 * b].view(torch.int64).view(b, 8).cpu().numpy()
         names = ["pass1_backward_factor", "pass2_fwd_predictor", "pass3_bwd_corrector_rhs",
-                 "pass4_fwd_corrector", "polish", "refactor_and_head", "start_and_warm_polish"]
+                 "pass4_fwd_corrector", "polish", "failed_factorisation", "start", "warm_polish"]
         totq = pc.sum()
         print("PASSCLK", json.dumps({n: round(float(pc[:, i].sum() / totq), 3) for i, n in enumerate(names)}),
               flush=True)
