@@ -68,6 +68,94 @@ MPCQP_QD bool from_lane0(bool v) { return __builtin_amdgcn_readfirstlane(v ? 1 :
 
 constexpr int kQuads = kWave / 4;
 
+// ------------------------------------------------ Riccati on the matrix cores
+// The factorisation sweep of riccati_q as 4 x 4 fp64 matrix products on
+// v_mfma_f64_4x4x4_4b_f64 (measured on gfx950, tools/mfma64_probe): four
+// independent 4 x 4 x 4 blocks, block m = (lane >> 2) & 3; in a block the B,
+// C and D operands hold X[r][c] at lane 16 r + 4 m + c ("D layout") and the A
+// operand reads a D-layout matrix as its transpose.  So with every stage
+// matrix in D layout (lane (r, c) loads its element):
+//   M1a = P'A = PA,  M1b = P [B | e] + [0 | p]        (2 products)
+//   A'PA, A'M1b, B'PA, B'M1b                           (4 products)
+//   K = -G^-1 Hx,  Ph = A'PA + Hx'K,  ph = A'Pe + Hx'k (3 products)
+// with Hx = H2xu' + B'PA; the 2 x 2 block G, h is read from block 0 and
+// inverted on every lane.  One stage is ~50 instructions with a dependency
+// chain of 5 products, against ~285 VALU for the quad step (each fp64 VALU
+// op issues in 4 cycles; a dependent 4x4x4 product returns in 23-29, a
+// dependent FMA in 6.5: profiles/r06/mfma64_probe.txt).  All four blocks
+// compute the same stage; block 0 stores.  Fields: the factor data as
+// store_factor_q writes them (PP, KM, GI, KV, PV; E is not rewritten);
+// the gradient g_x, the input gradients, Sigma_x and Sigma_u come from the
+// lane-relative field FGX, the fields FGU, FGU+1, the lane-relative FSX and
+// FSU, FSU+1.  Returns (uniformly) whether every G was positive definite.
+MPCQP_QD double mfma44(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+MPCQP_QD double lane_bcast(double v, int l) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int FGX, int FGU, int FSX, int FSU>
+MPCQP_QD bool riccati_mfma(double* W, int N, double dreg) {
+  const int lane = (int)threadIdx.x;
+  const int r = lane >> 4, c = lane & 3;
+  const bool store = ((lane >> 2) & 3) == 0;
+  const bool isB = c < 2, isE = c == 2, isD = r == c, rowU = r < 2;
+  // lane-constant offsets of the lane's element in a stage's fields
+  const int oA = L::DA + r * NX + c;
+  const int oB = L::DB + r * NU + (c & 1);
+  const int oE = L::E + r;
+  const int oWXX = L::WXX + pk(r, c);
+  const int oSX = FSX + r, oGX = FGX + r;
+  const int oWXU = L::WXU + c * NU + (r & 1);
+  const int oPP = L::PP + pk(r, c), oKM = L::KM + (r & 1) * NX + c;
+  double Ph = 0.0, phc = 0.0;
+  bool ok = true;
+  for (int k = N - 1; k >= 0; --k) {
+    double* S = W + k * L::F;
+    const double a = S[oA], bq = S[oB], e = S[oE], wxx = S[oWXX];
+    const double sx = S[oSX], gx = S[oGX], wxu = S[oWXU];
+    const double wuu0 = S[L::WUU], wuu1 = S[L::WUU + 1], wuu2 = S[L::WUU + 2];
+    const double su0 = S[FSU], su1 = S[FSU + 1], gu0 = S[FGU], gu1 = S[FGU + 1];
+    // P = Q' + H2xx + Ph + Sigma_x (+ shift), p = g_x + ph (column 2)
+    const double P = wxx + Ph + (isD ? sx + dreg : 0.0);
+    const double p = gx + phc;
+    const double M1a = mfma44(P, a, 0.0);
+    const double M1b = mfma44(P, isB ? bq : (isE ? e : 0.0), isE ? p : 0.0);
+    const double Bz = isB ? bq : 0.0;
+    const double AtPA = mfma44(a, M1a, 0.0);
+    const double AtM1b = mfma44(a, M1b, 0.0);
+    const double BtPA = mfma44(Bz, M1a, 0.0);
+    const double BtM1b = mfma44(Bz, M1b, 0.0);
+    // G = R + H2uu + Sigma_u + B'PB, h = g_u + B'Pe (block 0, lanes 0, 16, 17; 2, 18)
+    double G[3], Gi[3];
+    G[0] = wuu0 + su0 + dreg + lane_bcast(BtM1b, 0);
+    G[1] = wuu1 + lane_bcast(BtM1b, 16);
+    G[2] = wuu2 + su1 + dreg + lane_bcast(BtM1b, 17);
+    const double h0 = gu0 + lane_bcast(BtM1b, 2), h1 = gu1 + lane_bcast(BtM1b, 18);
+    ok = inv2(G, Gi) && ok;
+    const double kk0 = -(Gi[0] * h0 + Gi[1] * h1), kk1 = -(Gi[1] * h0 + Gi[2] * h1);
+    const double Hx = rowU ? BtPA + wxu : 0.0;
+    const double mGi = (rowU && isB) ? -(r == c ? (r == 0 ? Gi[0] : Gi[2]) : Gi[1]) : 0.0;
+    const double K = mfma44(mGi, Hx, 0.0);
+    const double kkv = (rowU && isE) ? (r == 0 ? kk0 : kk1) : 0.0;
+    Ph = mfma44(Hx, K, AtPA);
+    phc = mfma44(Hx, kkv, AtM1b);
+    if (store) {
+      if (c <= r) S[oPP] = P;
+      if (rowU) {
+        S[oKM] = K;
+        if (isE) S[L::KV + r] = kkv;
+      }
+      if (isE) S[L::PV + r] = p;
+      if (r == 0 && c < 3) S[L::GI + c] = Gi[c];
+    }
+  }
+  return ok;
+}
+
 // The backward sweep of a right-hand side on the stored factorisation (quad
 // 0; pass 3 of the interior point, solve_quad's expressions): g_x row i from
 // field FGX (lane-relative), g_u (both inputs) from FGU; writes k -> KV and
@@ -216,6 +304,12 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
         }
       }
       wave_lds_sync();
+#ifndef MPCQP_RICCATI_QUAD
+      if (refactor) {
+        good = riccati_mfma<L::PV, L::KV, L::KM, L::GI>(at.W, N, 0.0) && good;
+        wave_lds_sync();
+      } else if (q0) {
+#else
       if (q0 && refactor) {
         double Ph[4] = {0.0, 0.0, 0.0, 0.0}, ph = 0.0;
         for (int k = N - 1; k >= 0; --k) {
@@ -229,6 +323,7 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
           store_factor_q(at, k, i, P, p, Kc, kk, Gi, e);
         }
       } else if (q0) {
+#endif
         // the penalty and the active set of the previous step: its factors
         // stand, only the right-hand side is swept (e back in E first)
         rhs_sweep_q<L::PV, L::KV>(at, N, i);
@@ -463,6 +558,9 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
     wave_lds_sync();
     // ==================== pass 1c: the Riccati factorisation (quad 0, serial)
     bool pd = true;
+#ifndef MPCQP_RICCATI_QUAD
+    pd = riccati_mfma<L::GA + NU, L::GA, L::DXA, L::DUA>(W, N, dreg);
+#else
     if (q0) {
       double Ph[4] = {0.0, 0.0, 0.0, 0.0}, ph = 0.0;
       for (int k = N - 1; k >= 0; --k) {
@@ -478,6 +576,7 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
       }
     }
     pd = from_lane0(pd);
+#endif
     rstat = wave_max(rstat);
     rdyn = wave_max(rdyn);
     const double mu = mcount > 0.0 ? wsum(musum) / mcount : 0.0;
