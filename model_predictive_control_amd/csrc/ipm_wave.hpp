@@ -156,6 +156,84 @@ MPCQP_QD bool riccati_mfma(double* W, int N, double dreg) {
   return ok;
 }
 
+// The two recursions that remain after the factorisation, on the matrix cores
+// (same operand layouts as riccati_mfma; block 0 stores):
+//  forward_mfma  dx_{k+1} = Acl_k dx_k + (e_k + B_k k_k), Acl = A + B K, the
+//                state direction of x_{k+1} into the lane-relative field FOUT
+//                (one dependent product per stage; the input direction
+//                du_k = K_k dx_k + k_k is left to the per-stage phase after it,
+//                du_of_stage);
+//  rhs_mfma      the right-hand side sweep of rhs_sweep_q: p = g_x + phc,
+//                Pe = P e + p, k = -G^-1 (g_u + B'Pe), phc = Acl'Pe + K'g_u
+//                (one dependent product per stage).
+// Acl' / Acl, P e + g_x and K'g_u do not depend on the recursion and are
+// formed from the stage's fields ahead of it.
+template <int FOUT>
+MPCQP_QD void forward_mfma(double* W, int N) {
+  const int lane = (int)threadIdx.x;
+  const int r = lane >> 4, c = lane & 3;
+  const bool store = ((lane >> 2) & 3) == 0 && c == 0, rowU = r < 2, col0 = c == 0;
+  const int oKM = L::KM + (r & 1) * NX + c;
+  const int oBt = L::DB + c * NU + (r & 1);
+  const int oAt = L::DA + c * NX + r;
+  const int oB0 = L::DB + r * NU, oE = L::E + r;
+  double dx = 0.0;  // column 0: the direction of x_k
+  for (int k = 0; k < N; ++k) {
+    double* S = W + k * L::F;
+    const double Kd = rowU ? S[oKM] : 0.0, Bt = rowU ? S[oBt] : 0.0, At = S[oAt];
+    const double b0 = S[oB0], b1 = S[oB0 + 1], e = S[oE];
+    const double kk0 = S[L::KV], kk1 = S[L::KV + 1];
+    const double AclT = mfma44(Kd, Bt, At);  // (A + B K)'
+    const double ccl = col0 ? fma(b1, kk1, fma(b0, kk0, e)) : 0.0;
+    dx = mfma44(AclT, dx, ccl);
+    if (store) S[FOUT + r] = dx;
+  }
+}
+
+template <int FGX, int FGU>
+MPCQP_QD void rhs_mfma(double* W, int N) {
+  const int lane = (int)threadIdx.x;
+  const int r = lane >> 4, c = lane & 3;
+  const bool blk0 = ((lane >> 2) & 3) == 0, rowU = r < 2, col0 = c == 0, isB = c < 2;
+  const int oPP = L::PP + pk(r, c), oE = L::E + r, oGX = FGX + r;
+  const int oA = L::DA + r * NX + c, oKM = L::KM + (r & 1) * NX + c;
+  const int oBt = L::DB + c * NU + (r & 1), oB = L::DB + r * NU + (c & 1);
+  double phc = 0.0;  // column 0
+  for (int k = N - 1; k >= 0; --k) {
+    double* S = W + k * L::F;
+    const double P = S[oPP], e = col0 ? S[oE] : 0.0, gx = col0 ? S[oGX] : 0.0;
+    const double A = S[oA], Kd = rowU ? S[oKM] : 0.0, Bt = rowU ? S[oBt] : 0.0;
+    const double Bz = isB ? S[oB] : 0.0;
+    const double gu0 = S[FGU], gu1 = S[FGU + 1];
+    const double Gi0 = S[L::GI], Gi1 = S[L::GI + 1], Gi2 = S[L::GI + 2];
+    const double Pe0 = mfma44(P, e, gx);                     // P e + g_x (column 0)
+    const double Acl = mfma44(Bt, Kd, A);                    // A + B K
+    const double guc = (rowU && col0) ? (r == 0 ? gu0 : gu1) : 0.0;
+    const double Ktgu = mfma44(Kd, guc, 0.0);                // K'g_u (column 0)
+    const double p = col0 ? gx + phc : 0.0;
+    const double Pe = Pe0 + phc;
+    const double BtPe = mfma44(Bz, Pe, 0.0);                 // rows 0, 1: B'Pe
+    phc = mfma44(Acl, Pe, Ktgu);
+    const double h0 = gu0 + lane_bcast(BtPe, 0), h1 = gu1 + lane_bcast(BtPe, 16);
+    if (blk0 && col0) {
+      S[L::PV + r] = p;
+      if (rowU) S[L::KV + r] = -(r == 0 ? Gi0 * h0 + Gi1 * h1 : Gi1 * h0 + Gi2 * h1);
+    }
+  }
+}
+
+// du_k = K_k dx_k + k_k of stage k, lane i < 2 (dx_k: the state direction of
+// stage k-1 in the lane-relative field FDX, 0 at k = 0)
+template <int FDX>
+MPCQP_QD double du_of_stage(const WsQ<1>& at, int k, int i) {
+  double s = at(k, L::KV + (i & 1));
+  if (k > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s = fma(at(k, L::KM + (i & 1) * NX + j), at(k - 1, FDX + j), s);
+  }
+  return s;
+}
+
 // The backward sweep of a right-hand side on the stored factorisation (quad
 // 0; pass 3 of the interior point, solve_quad's expressions): g_x row i from
 // field FGX (lane-relative), g_u (both inputs) from FGU; writes k -> KV and
@@ -208,7 +286,10 @@ template <typename T>
 MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double x0i,
                        bool warm) {
   const int N = a.N;
-  const bool ou = i < NU, q0 = qd == 0;
+  const bool ou = i < NU;
+#ifdef MPCQP_RICCATI_QUAD
+  const bool q0 = qd == 0;
+#endif
   for (int k = qd; k < N; k += kQuads) {
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
@@ -307,8 +388,20 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
 #ifndef MPCQP_RICCATI_QUAD
       if (refactor) {
         good = riccati_mfma<L::PV, L::KV, L::KM, L::GI>(at.W, N, 0.0) && good;
-        wave_lds_sync();
-      } else if (q0) {
+      } else {
+        // the penalty and the active set of the previous step: its factors
+        // stand, only the right-hand side is swept (e back in E first)
+        rhs_mfma<L::PV, L::KV>(at.W, N);
+      }
+      wave_lds_sync();
+      forward_mfma<L::E>(at.W, N);
+      wave_lds_sync();
+      // the step: x, u += the directions (the state direction of stage k is
+      // in E(k); du_k needs that of stage k-1, so the updates of DX follow)
+      for (int k = qd; k < N; k += kQuads)
+        if (ou) at.r(k, L::DU) += du_of_stage<L::E>(at, k, i);
+      wave_lds_sync();
+      for (int k = qd; k < N; k += kQuads) at.r(k, L::DX) += at.r(k, L::E);
 #else
       if (q0 && refactor) {
         double Ph[4] = {0.0, 0.0, 0.0, 0.0}, ph = 0.0;
@@ -323,9 +416,6 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
           store_factor_q(at, k, i, P, p, Kc, kk, Gi, e);
         }
       } else if (q0) {
-#endif
-        // the penalty and the active set of the previous step: its factors
-        // stand, only the right-hand side is swept (e back in E first)
         rhs_sweep_q<L::PV, L::KV>(at, N, i);
       }
       if (q0) {
@@ -335,6 +425,7 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
           if (ou) at.r(k, L::DU) += sel2(du, i);
         });
       }
+#endif
       wave_lds_sync();
       const bool last = step == kSteps - 1;
       const bool probe = !last && step >= kPolishEarly;
@@ -624,14 +715,22 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
 
     MPCQP_PCLK(0);
     // ============ pass 2: the predictor's forward sweep (quad 0), then per stage
+#ifndef MPCQP_RICCATI_QUAD
+    forward_mfma<L::DXA>(W, N);
+    wave_lds_sync();
+#else
     if (q0)
       forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&)[4]) {
         at.r(k, L::DXA) = dxn;
         if (ou) at.r(k, L::DUA) = sel2(du, i);
       });
     wave_lds_sync();
+#endif
     double amax = 1.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
     for (int k = qd; k < N; k += kQuads) {
+#ifndef MPCQP_RICCATI_QUAD
+      if (ou) at.r(k, L::DUA) = du_of_stage<L::DXA>(at, k, i);
+#endif
       auto comp = [&](double vj, double dv, double lo, double hi, double l, double lu) {
         if (fin(lo)) {
           const double sl = vj - lo;
@@ -694,19 +793,31 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
       at.r(k, L::GA + NU) = gx;
     }
     wave_lds_sync();
+#ifndef MPCQP_RICCATI_QUAD
+    rhs_mfma<L::GA + NU, L::GA>(W, N);
+#else
     if (q0) rhs_sweep_q<L::GA + NU, L::GA>(at, N, i);
+#endif
     wave_lds_sync();
 
     MPCQP_PCLK(2);
     // ========== pass 4: the corrector's forward sweep (quad 0), then per stage
+#ifndef MPCQP_RICCATI_QUAD
+    forward_mfma<L::DX>(W, N);
+    wave_lds_sync();
+#else
     if (q0)
       forward_q(at, N, i, [&](int k, const double (&du)[2], double dxn, const double (&)[4]) {
         at.r(k, L::DX) = dxn;
         if (ou) at.r(k, L::DU) = sel2(du, i);
       });
     wave_lds_sync();
+#endif
     amax = 1.0;
     for (int k = qd; k < N; k += kQuads) {
+#ifndef MPCQP_RICCATI_QUAD
+      if (ou) at.r(k, L::DU) = du_of_stage<L::DX>(at, k, i);
+#endif
       const double dxn = at.r(k, L::DX);
       double s = at.r(k, L::PV);
 #pragma unroll
