@@ -111,33 +111,51 @@ MPCQP_QD bool riccati_mfma(double* W, int N, double dreg) {
   const int oSX = FSX + r, oGX = FGX + r;
   const int oWXU = L::WXU + c * NU + (r & 1);
   const int oPP = L::PP + pk(r, c), oKM = L::KM + (r & 1) * NX + c;
+  // the stage's operands, loaded one stage ahead (the LDS round trip then
+  // overlaps the previous stage's products instead of opening each stage)
+  struct Ops {
+    double a, bq, e, wxx, sx, gx, wxu, wuu0, wuu1, wuu2, su0, su1, gu0, gu1;
+  };
+  auto load = [&](int k) {
+    const double* S = W + k * L::F;
+    Ops o;
+    o.a = S[oA]; o.bq = S[oB]; o.e = S[oE]; o.wxx = S[oWXX];
+    o.sx = S[oSX]; o.gx = S[oGX]; o.wxu = S[oWXU];
+    o.wuu0 = S[L::WUU]; o.wuu1 = S[L::WUU + 1]; o.wuu2 = S[L::WUU + 2];
+    o.su0 = S[FSU]; o.su1 = S[FSU + 1]; o.gu0 = S[FGU]; o.gu1 = S[FGU + 1];
+    return o;
+  };
   double Ph = 0.0, phc = 0.0;
   bool ok = true;
+  Ops nx = load(N - 1);
   for (int k = N - 1; k >= 0; --k) {
     double* S = W + k * L::F;
-    const double a = S[oA], bq = S[oB], e = S[oE], wxx = S[oWXX];
-    const double sx = S[oSX], gx = S[oGX], wxu = S[oWXU];
-    const double wuu0 = S[L::WUU], wuu1 = S[L::WUU + 1], wuu2 = S[L::WUU + 2];
-    const double su0 = S[FSU], su1 = S[FSU + 1], gu0 = S[FGU], gu1 = S[FGU + 1];
+    const Ops o = nx;
     // P = Q' + H2xx + Ph + Sigma_x (+ shift), p = g_x + ph (column 2)
-    const double P = wxx + Ph + (isD ? sx + dreg : 0.0);
-    const double p = gx + phc;
-    const double M1a = mfma44(P, a, 0.0);
-    const double M1b = mfma44(P, isB ? bq : (isE ? e : 0.0), isE ? p : 0.0);
-    const double Bz = isB ? bq : 0.0;
-    const double AtPA = mfma44(a, M1a, 0.0);
-    const double AtM1b = mfma44(a, M1b, 0.0);
+    const double P = o.wxx + Ph + (isD ? o.sx + dreg : 0.0);
+    const double p = o.gx + phc;
+    const double M1a = mfma44(P, o.a, 0.0);
+    const double M1b = mfma44(P, isB ? o.bq : (isE ? o.e : 0.0), isE ? p : 0.0);
+    // the next stage's operands, issued behind the first products (the
+    // scheduler would otherwise sink them to their use: an LDS round trip
+    // at the head of every stage)
+    __builtin_amdgcn_sched_barrier(0);
+    nx = load(k > 0 ? k - 1 : 0);
+    __builtin_amdgcn_sched_barrier(0);
+    const double Bz = isB ? o.bq : 0.0;
+    const double AtPA = mfma44(o.a, M1a, 0.0);
+    const double AtM1b = mfma44(o.a, M1b, 0.0);
     const double BtPA = mfma44(Bz, M1a, 0.0);
     const double BtM1b = mfma44(Bz, M1b, 0.0);
     // G = R + H2uu + Sigma_u + B'PB, h = g_u + B'Pe (block 0, lanes 0, 16, 17; 2, 18)
     double G[3], Gi[3];
-    G[0] = wuu0 + su0 + dreg + lane_bcast(BtM1b, 0);
-    G[1] = wuu1 + lane_bcast(BtM1b, 16);
-    G[2] = wuu2 + su1 + dreg + lane_bcast(BtM1b, 17);
-    const double h0 = gu0 + lane_bcast(BtM1b, 2), h1 = gu1 + lane_bcast(BtM1b, 18);
+    G[0] = o.wuu0 + o.su0 + dreg + lane_bcast(BtM1b, 0);
+    G[1] = o.wuu1 + lane_bcast(BtM1b, 16);
+    G[2] = o.wuu2 + o.su1 + dreg + lane_bcast(BtM1b, 17);
+    const double h0 = o.gu0 + lane_bcast(BtM1b, 2), h1 = o.gu1 + lane_bcast(BtM1b, 18);
     ok = inv2(G, Gi) && ok;
     const double kk0 = -(Gi[0] * h0 + Gi[1] * h1), kk1 = -(Gi[1] * h0 + Gi[2] * h1);
-    const double Hx = rowU ? BtPA + wxu : 0.0;
+    const double Hx = rowU ? BtPA + o.wxu : 0.0;
     const double mGi = (rowU && isB) ? -(r == c ? (r == 0 ? Gi[0] : Gi[2]) : Gi[1]) : 0.0;
     const double K = mfma44(mGi, Hx, 0.0);
     const double kkv = (rowU && isE) ? (r == 0 ? kk0 : kk1) : 0.0;
@@ -177,16 +195,36 @@ MPCQP_QD void forward_mfma(double* W, int N) {
   const int oBt = L::DB + c * NU + (r & 1);
   const int oAt = L::DA + c * NX + r;
   const int oB0 = L::DB + r * NU, oE = L::E + r;
+  // pipeline: the stage's raw operands two stages ahead, its closed-loop
+  // matrix and offset (products that do not depend on the recursion) one
+  // stage ahead, each behind a scheduling barrier after the recursion's
+  // product of the current stage
+  struct Raw {
+    double Kd, Bt, At, b0, b1, e, kk0, kk1;
+  };
+  auto load = [&](int k) {
+    const double* S = W + k * L::F;
+    Raw o;
+    o.Kd = rowU ? S[oKM] : 0.0; o.Bt = rowU ? S[oBt] : 0.0; o.At = S[oAt];
+    o.b0 = S[oB0]; o.b1 = S[oB0 + 1]; o.e = S[oE];
+    o.kk0 = S[L::KV]; o.kk1 = S[L::KV + 1];
+    return o;
+  };
+  auto prep = [&](const Raw& o, double& AclT, double& ccl) {
+    AclT = mfma44(o.Kd, o.Bt, o.At);  // (A + B K)'
+    ccl = col0 ? fma(o.b1, o.kk1, fma(o.b0, o.kk0, o.e)) : 0.0;
+  };
   double dx = 0.0;  // column 0: the direction of x_k
+  double AclT, ccl;
+  prep(load(0), AclT, ccl);
+  Raw nx = load(N > 1 ? 1 : 0);
   for (int k = 0; k < N; ++k) {
-    double* S = W + k * L::F;
-    const double Kd = rowU ? S[oKM] : 0.0, Bt = rowU ? S[oBt] : 0.0, At = S[oAt];
-    const double b0 = S[oB0], b1 = S[oB0 + 1], e = S[oE];
-    const double kk0 = S[L::KV], kk1 = S[L::KV + 1];
-    const double AclT = mfma44(Kd, Bt, At);  // (A + B K)'
-    const double ccl = col0 ? fma(b1, kk1, fma(b0, kk0, e)) : 0.0;
     dx = mfma44(AclT, dx, ccl);
-    if (store) S[FOUT + r] = dx;
+    __builtin_amdgcn_sched_barrier(0);
+    prep(nx, AclT, ccl);
+    nx = load(k + 2 < N ? k + 2 : N - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (store) W[k * L::F + FOUT + r] = dx;
   }
 }
 
@@ -194,31 +232,65 @@ template <int FGX, int FGU>
 MPCQP_QD void rhs_mfma(double* W, int N) {
   const int lane = (int)threadIdx.x;
   const int r = lane >> 4, c = lane & 3;
-  const bool blk0 = ((lane >> 2) & 3) == 0, rowU = r < 2, col0 = c == 0, isB = c < 2;
+  const bool store = ((lane >> 2) & 3) == 0 && c == 0, rowU = r < 2, col0 = c == 0;
   const int oPP = L::PP + pk(r, c), oE = L::E + r, oGX = FGX + r;
   const int oA = L::DA + r * NX + c, oKM = L::KM + (r & 1) * NX + c;
-  const int oBt = L::DB + c * NU + (r & 1), oB = L::DB + r * NU + (c & 1);
+  const int oBt = L::DB + c * NU + (r & 1);
+  // pipeline as forward_mfma: raw operands two stages ahead, the products
+  // that do not depend on the recursion one stage ahead
+  struct Raw {
+    double P, e, gx, A, Kd, Bt, guc;
+  };
+  auto load = [&](int k) {
+    const double* S = W + k * L::F;
+    Raw o;
+    o.P = S[oPP]; o.e = col0 ? S[oE] : 0.0; o.gx = col0 ? S[oGX] : 0.0;
+    o.A = S[oA]; o.Kd = rowU ? S[oKM] : 0.0; o.Bt = rowU ? S[oBt] : 0.0;
+    o.guc = (rowU && col0) ? S[FGU + (r & 1)] : 0.0;
+    return o;
+  };
+  auto prep = [&](const Raw& o, double& Pe0, double& Acl, double& Ktgu, double& gx) {
+    Pe0 = mfma44(o.P, o.e, o.gx);      // P e + g_x (column 0)
+    Acl = mfma44(o.Bt, o.Kd, o.A);     // A + B K
+    Ktgu = mfma44(o.Kd, o.guc, 0.0);   // K'g_u (column 0)
+    gx = o.gx;
+  };
   double phc = 0.0;  // column 0
+  double Pe0, Acl, Ktgu, gx;
+  prep(load(N - 1), Pe0, Acl, Ktgu, gx);
+  Raw nx = load(N > 1 ? N - 2 : 0);
   for (int k = N - 1; k >= 0; --k) {
-    double* S = W + k * L::F;
-    const double P = S[oPP], e = col0 ? S[oE] : 0.0, gx = col0 ? S[oGX] : 0.0;
-    const double A = S[oA], Kd = rowU ? S[oKM] : 0.0, Bt = rowU ? S[oBt] : 0.0;
-    const double Bz = isB ? S[oB] : 0.0;
-    const double gu0 = S[FGU], gu1 = S[FGU + 1];
-    const double Gi0 = S[L::GI], Gi1 = S[L::GI + 1], Gi2 = S[L::GI + 2];
-    const double Pe0 = mfma44(P, e, gx);                     // P e + g_x (column 0)
-    const double Acl = mfma44(Bt, Kd, A);                    // A + B K
-    const double guc = (rowU && col0) ? (r == 0 ? gu0 : gu1) : 0.0;
-    const double Ktgu = mfma44(Kd, guc, 0.0);                // K'g_u (column 0)
-    const double p = col0 ? gx + phc : 0.0;
-    const double Pe = Pe0 + phc;
-    const double BtPe = mfma44(Bz, Pe, 0.0);                 // rows 0, 1: B'Pe
-    phc = mfma44(Acl, Pe, Ktgu);
-    const double h0 = gu0 + lane_bcast(BtPe, 0), h1 = gu1 + lane_bcast(BtPe, 16);
-    if (blk0 && col0) {
-      S[L::PV + r] = p;
-      if (rowU) S[L::KV + r] = -(r == 0 ? Gi0 * h0 + Gi1 * h1 : Gi1 * h0 + Gi2 * h1);
-    }
+    const double p = gx + phc;
+    phc = mfma44(Acl, Pe0 + phc, Ktgu);
+    __builtin_amdgcn_sched_barrier(0);
+    prep(nx, Pe0, Acl, Ktgu, gx);
+    nx = load(k > 1 ? k - 2 : 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (store) W[k * L::F + L::PV + r] = p;
+  }
+}
+
+// The feed-forward of stage k after rhs_mfma, lane i of a quad (lanes 0, 1
+// store): k = -G^-1 (g_u + B'(P e + p)), g_u from FGU, FGU+1
+template <int FGU>
+MPCQP_QD void rhs_kk_stage(const WsQ<1>& at, int k, int i) {
+  double Pe = at.r(k, L::PV);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) Pe = fma(at.p(k, L::PP, j), at(k, L::E + j), Pe);
+  double Pea[4];
+  bcast4(Pe, Pea);
+  double h[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    double s = at(k, FGU + r);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s = fma(at(k, L::DB + q * NU + r), Pea[q], s);
+    h[r] = s;
+  }
+  const double Gi[3] = {at(k, L::GI + 0), at(k, L::GI + 1), at(k, L::GI + 2)};
+  if (i < 2) {
+    const double kk = -(Gi[pk(i, 0)] * h[0] + Gi[pk(i, 1)] * h[1]);
+    at.r(k, L::KV) = kk;
   }
 }
 
@@ -392,6 +464,9 @@ MPCQP_QD bool polish_w(const Args<T>& a, const WsQ<1>& at, int qd, int i, double
         // the penalty and the active set of the previous step: its factors
         // stand, only the right-hand side is swept (e back in E first)
         rhs_mfma<L::PV, L::KV>(at.W, N);
+        wave_lds_sync();
+        // (g_u is in KV: every stage reads its own before writing k there)
+        for (int k = qd; k < N; k += kQuads) rhs_kk_stage<L::KV>(at, k, i);
       }
       wave_lds_sync();
       forward_mfma<L::E>(at.W, N);
@@ -578,6 +653,7 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
       at.r(k, L::PV) = gx1;
     }
     wave_lds_sync();
+    MPCQP_PCLK(8);
     // ============ pass 1b: per stage, the step, residual, gradients, Sigma
     double rstat = 0.0, rdyn = 0.0, musum = 0.0;
     for (int k = qd; k < N; k += kQuads) {
@@ -647,6 +723,7 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
       at.r(k, L::DXA) = sx;
     }
     wave_lds_sync();
+    MPCQP_PCLK(9);
     // ==================== pass 1c: the Riccati factorisation (quad 0, serial)
     bool pd = true;
 #ifndef MPCQP_RICCATI_QUAD
@@ -668,6 +745,7 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
     }
     pd = from_lane0(pd);
 #endif
+    MPCQP_PCLK(10);
     rstat = wave_max(rstat);
     rdyn = wave_max(rdyn);
     const double mu = mcount > 0.0 ? wsum(musum) / mcount : 0.0;
@@ -795,6 +873,8 @@ MPCQP_QD bool solve_wave(const Args<T>& a, int b, double* W, bool warm = false,
     wave_lds_sync();
 #ifndef MPCQP_RICCATI_QUAD
     rhs_mfma<L::GA + NU, L::GA>(W, N);
+    wave_lds_sync();
+    for (int k = qd; k < N; k += kQuads) rhs_kk_stage<L::GA>(at, k, i);
 #else
     if (q0) rhs_sweep_q<L::GA + NU, L::GA>(at, N, i);
 #endif

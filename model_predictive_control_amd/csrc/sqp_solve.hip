@@ -402,7 +402,9 @@ struct SolveClock {
   uint64_t tqp = 0;
   int64_t ipm_its = 0, warm_hits = 0, sqp_its = 0;
 #ifdef MPCQP_IPM_PASSCLK
-  uint64_t pass[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // passes 1-4, polish, failed factorisations, start, warm polish (timing builds)
+  // timing builds: passes 1-4, polish, failed factorisations, start, warm
+  // polish, and pass 1's parts 1a, 1b, 1c (index 0 then keeps its reductions)
+  uint64_t pass[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 };
 
@@ -547,7 +549,7 @@ __device__ __forceinline__ void write_clock(const SqpSolveArgs& g, int64_t b, ui
     st[3] = clk.sqp_its | (clk.warm_hits << 32);
 #ifdef MPCQP_IPM_PASSCLK
     // (the workspace region of g.Xr, unused by sqp_solve_kernel)
-    for (int i = 0; i < 8; ++i) reinterpret_cast<int64_t*>(g.Xr)[b * 8 + i] = (int64_t)clk.pass[i];
+    for (int i = 0; i < 11; ++i) reinterpret_cast<int64_t*>(g.Xr)[b * 11 + i] = (int64_t)clk.pass[i];
 #endif
   }
 }
