@@ -87,6 +87,12 @@ __device__ __forceinline__ void wg_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ
 // every expression written as bike_pt / bike_step write it, so the rollout
 // is bit-identical to model_step's.  Per-stage scratch in LDS after the QP's
 // workspace (kScr doubles per stage, N + 1 stages, then the broadcast slots).
+// the step's serial sweeps read their operands from the QP's LDS workspace
+// (dead between QPs except the active flags GA): A_k, B_k in the stage-data
+// fields DA, DB (the QP's own copy of the linearisation, then the new one
+// from fe_linearise_wave), the multipliers y_k in DX
+constexpr int kQF = ipm::Layout<4, 2>::F, kQA = ipm::Layout<4, 2>::DA, kQB = ipm::Layout<4, 2>::DB;
+constexpr int kQY = ipm::Layout<4, 2>::DX;
 constexpr int kScr = 14;
 enum { kU0 = 0, kU1, kBeta, kSb, kPx, kPy, kPsi, kV, kSt, kCt, kTJ, kTV, kL0, kL1 };
 
@@ -193,7 +199,7 @@ __device__ __forceinline__ Merit fe_merit_wave(const SqpArgs& a, int64_t b, doub
 // A_k, B_k, c_k of every stage from the rollout in scr (model_step_jac at
 // (x_k, u_k), as mpcqp_bicycle_linearise writes them), lane per stage.
 __device__ __forceinline__ void fe_linearise_wave(const SqpArgs& a, int N, double* A, double* B, double* c,
-                                  const double* scr, int lane) {
+                                  const double* scr, int lane, double* qlds = nullptr) {
   for (int k = lane; k < N; k += kWave) {
     const double* q = scr_at(const_cast<double*>(scr), k);
     const double x[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
@@ -206,6 +212,7 @@ __device__ __forceinline__ void fe_linearise_wave(const SqpArgs& a, int N, doubl
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         A[k * 16 + i * 4 + j] = Aj[i][j];
+        if (qlds) qlds[(size_t)k * kQF + kQA + i * 4 + j] = Aj[i][j];
         t -= Aj[i][j] * x[j];
       }
       B[k * 8 + i * 2] = Bj[i][0];
@@ -223,7 +230,7 @@ __device__ __forceinline__ void fe_linearise_wave(const SqpArgs& a, int N, doubl
 // the next iteration's linearisation: they overwrite A, B, c, and the
 // function returns true when it wrote them.
 __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, double* A, double* B, double* c,
-                              double* scr, int lane) {
+                              double* scr, int lane, double* qlds) {
   const int fl = a.flags[b];
   if (fl & kSqpDone) return false;
   const int N = a.N;
@@ -250,15 +257,21 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
   umax = wave_max(umax);
   const double rho = fmax(a.rho[b], 2.0 * ymax);
   const Merit m0 = fe_merit_wave(a, b, 0.0, false, nullptr, scr, lane);
+  // the direction into LDS beside U (scr: kL0, kL1 free until the adjoint)
+  for (int k = lane; k < N; k += kWave) {
+    scr_at(scr, k)[kL0] = sqp_dir(a, b, 2 * k);
+    scr_at(scr, k)[kL1] = sqp_dir(a, b, 2 * k + 1);
+  }
+  wave_lds_sync();
   double* bc = scr_at(scr, N + 1);
-  if (lane == 0) {  // D = d(1/2 J)/dU . d, sqp_step_one's loop on the stored A_k, B_k
+  if (lane == 0) {  // D = d(1/2 J)/dU . d, sqp_step_one's loop on the QP's A_k, B_k (LDS)
     double D = 0.0;
     double dx[4] = {0.0, 0.0, 0.0, 0.0};
     for (int k = 0; k < N; ++k) {
       const double* q = scr_at(scr, k);
       const double x[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
-      const double u[2] = {U[2 * k], U[2 * k + 1]};
-      const double d[2] = {sqp_dir(a, b, 2 * k), sqp_dir(a, b, 2 * k + 1)};
+      const double u[2] = {q[kU0], q[kU1]};
+      const double d[2] = {q[kL0], q[kL1]};
       for (int i = 0; i < 4; ++i) {
         double t = 0.0;
         for (int j = 0; j < 4; ++j) t = fma(a.Q[i * 4 + j], x[j], t);
@@ -269,8 +282,8 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
         for (int q2 = 0; q2 < 2; ++q2) t = fma(a.R[r * 2 + q2], u[q2], t);
         D = fma(t, d[r], D);
       }
-      const double* Ak = A + k * 16;
-      const double* Bk = B + k * 8;
+      const double* Ak = qlds + (size_t)k * kQF + kQA;
+      const double* Bk = qlds + (size_t)k * kQF + kQB;
       double dxn[4];
       for (int i = 0; i < 4; ++i) {
         double s = Bk[i * 2] * d[0] + Bk[i * 2 + 1] * d[1];
@@ -318,21 +331,23 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
     U[i] = u;
   }
   for (int i = lane; i < 4 * N; i += kWave) {
-    y[i] = fma(alpha, yq[i] - y[i], y[i]);
+    const double yi = fma(alpha, yq[i] - y[i], y[i]);
+    y[i] = yi;
+    qlds[(size_t)(i >> 2) * kQF + kQY + (i & 3)] = yi;
     pi[i] = fma(alpha, piq[i] - pi[i], pi[i]);
   }
   wg_fence();
 
   // ------------------------------------------ KKT residual at the new point
   fe_merit_wave(a, b, 0.0, false, X, scr, lane);
-  fe_linearise_wave(a, N, A, B, c, scr, lane);
+  fe_linearise_wave(a, N, A, B, c, scr, lane, qlds);
   wg_fence();
   if (lane == 0) {  // the adjoint lambda_{k+1} of every stage, sqp_step_one's order
     double lam[4];
     const double* q = scr_at(scr, N);
     const double xN[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
     for (int i = 0; i < 4; ++i) {
-      double s = y[(N - 1) * 4 + i];
+      double s = qlds[(size_t)(N - 1) * kQF + kQY + i];
       for (int j = 0; j < 4; ++j) s = fma(a.Qf[i * 4 + j], xN[j], s);
       lam[i] = s;
     }
@@ -344,10 +359,10 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
       qk[kTV] = lam[3];
       if (k > 0) {
         const double x[4] = {qk[kPx], qk[kPy], qk[kPsi], qk[kV]};
-        const double* Ak = A + k * 16;
+        const double* Ak = qlds + (size_t)k * kQF + kQA;
         double ln[4];
         for (int i = 0; i < 4; ++i) {
-          double s = y[(k - 1) * 4 + i];
+          double s = qlds[(size_t)(k - 1) * kQF + kQY + i];
           for (int j = 0; j < 4; ++j) s = fma(a.Q[i * 4 + j], x[j], s);
           for (int j = 0; j < 4; ++j) s = fma(Ak[j * 4 + i], lam[j], s);
           ln[i] = s;
@@ -404,7 +419,8 @@ struct SolveClock {
 #ifdef MPCQP_IPM_PASSCLK
   // timing builds: passes 1-4, polish, failed factorisations, start, warm
   // polish, and pass 1's parts 1a, 1b, 1c (index 0 then keeps its reductions)
-  uint64_t pass[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // + the SQP's own phases: linearisation, Hessians + stage-in, the step
+  uint64_t pass[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 };
 
@@ -425,8 +441,15 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
   bool lin = false;   // A, B, c and X hold the linearisation at the current U
   bool warm = false;  // the last QP ended polished: its active set is in LDS
   int it = 0;
+#ifdef MPCQP_IPM_PASSCLK
+  uint64_t ph_t = __builtin_amdgcn_s_memrealtime();
+#define MPCQP_SCLK(i) do { const uint64_t _t = __builtin_amdgcn_s_memrealtime(); clk.pass[i] += _t - ph_t; ph_t = _t; } while (0)
+#else
+#define MPCQP_SCLK(i) do { } while (0)
+#endif
   for (; it < max_iter; ++it) {
     if (s.flags[b] & kSqpDone) break;
+    MPCQP_SCLK(14);
     // ------------------------------------------- 1. rollout + linearisation
     if (fe) {
       if (!lin) {
@@ -466,6 +489,7 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
       }
       wg_fence();
     }
+    MPCQP_SCLK(11);
     // ------------------------------------------------ 2. stage Hessians
     if (g.hmode != kHessGN) {
       const bool cvx = g.hmode == kHessExact;
@@ -483,7 +507,7 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
     }
     wg_fence();
     // ------------------------------------------------------------- 3. QP
-    // (one DPP quad; the warm polish where the QP's solution is the one the
+    // (the whole wave, ipm_wave.hpp; the warm polish where the QP's solution is the one the
     // interior point would find: Gauss-Newton QPs are convex, a unique
     // solution; an exact-Hessian QP may have several KKT points, and far from
     // the NLP's solution the previous active set can pick another one than
@@ -495,6 +519,7 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
       for (int k = lane >> 2; k < N; k += kWave / 4) ipmq::stage_in_q(g.q, (int)b, at, lane & 3, k);
     }
     wave_lds_sync();
+    MPCQP_SCLK(12);
 #ifdef MPCQP_IPM_WAVE
     {
       const int fl = s.flags[b];
@@ -528,15 +553,20 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
     wg_fence();
     clk.tqp += __builtin_amdgcn_s_memrealtime() - q0;
     clk.ipm_its += (g.q.status[b] >> 8) & 0xFFFF;
+#ifdef MPCQP_IPM_PASSCLK
+    ph_t = __builtin_amdgcn_s_memrealtime();
+#endif
     // ----------------------------------------------------------- 4. step
     if (fe) {
-      sqp_step_wave(s, b, A, B, c, scr, lane);
+      sqp_step_wave(s, b, A, B, c, scr, lane, ipm_lds);
     } else if (lane == 0) {
       sqp_step_one(s, b);
     }
     wg_fence();
+    MPCQP_SCLK(13);
   }
   clk.sqp_its += it;
+#undef MPCQP_SCLK
 }
 
 __device__ __forceinline__ void write_clock(const SqpSolveArgs& g, int64_t b, uint64_t t0,
@@ -549,7 +579,7 @@ __device__ __forceinline__ void write_clock(const SqpSolveArgs& g, int64_t b, ui
     st[3] = clk.sqp_its | (clk.warm_hits << 32);
 #ifdef MPCQP_IPM_PASSCLK
     // (the workspace region of g.Xr, unused by sqp_solve_kernel)
-    for (int i = 0; i < 11; ++i) reinterpret_cast<int64_t*>(g.Xr)[b * 11 + i] = (int64_t)clk.pass[i];
+    for (int i = 0; i < 15; ++i) reinterpret_cast<int64_t*>(g.Xr)[b * 15 + i] = (int64_t)clk.pass[i];
 #endif
   }
 }

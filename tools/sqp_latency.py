@@ -69,12 +69,19 @@ def main():
     if os.environ.get("MPCQP_LIB", "").endswith("passclk.so"):
         # the timing build's per-pass clocks: in the workspace after the stage data
         off = b * N * 70
-        pc = sqp.ws.view(torch.float64)[off:off + 8 * b].view(torch.int64).view(b, 8).cpu().numpy()
-        names = ["pass1_backward_factor", "pass2_fwd_predictor", "pass3_bwd_corrector_rhs",
-                 "pass4_fwd_corrector", "polish", "failed_factorisation", "start", "warm_polish"]
-        totq = pc.sum()
-        print("PASSCLK", json.dumps({n: round(float(pc[:, i].sum() / totq), 3) for i, n in enumerate(names)}),
+        pc = sqp.ws.view(torch.float64)[off:off + 15 * b].view(torch.int64).view(b, 15).cpu().numpy()
+        names = ["pass1_reductions", "pass2_fwd_predictor", "pass3_bwd_corrector_rhs",
+                 "pass4_fwd_corrector", "polish", "failed_factorisation", "start", "warm_polish",
+                 "pass1a_neighbours", "pass1b_stage_terms", "pass1c_factorisation",
+                 "sqp_linearise", "sqp_hessian", "sqp_stage_in", "sqp_step"]
+        totq = pc[:, :11].sum()
+        print("PASSCLK", json.dumps({n: round(float(pc[:, i].sum() / totq), 3) for i, n in enumerate(names[:11])}),
               flush=True)
+        # absolute: microseconds per interior-point iteration (all instances)
+        print("PASSCLK_US_PER_IPM_ITER", json.dumps({n: round(float(pc[:, i].sum()) * TICK_US / max(1.0, ipm.sum()), 2)
+                                                     for i, n in enumerate(names[:11])}), flush=True)
+        print("SQPCLK_US_PER_SQP_ITER", json.dumps({n: round(float(pc[:, i].sum()) * TICK_US / max(1.0, its.sum()), 2)
+                                                    for i, n in list(enumerate(names))[11:]}), flush=True)
     for i in np.argsort(-tot)[:8]:
         print(json.dumps(dict(inst=int(i), us=round(tot[i] * TICK_US, 1), qp_us=round(tqp[i] * TICK_US, 1),
                               ipm_iters=int(ipm[i]), sqp_iters=int(its[i]), ok=bool(ok[i]))), flush=True)
