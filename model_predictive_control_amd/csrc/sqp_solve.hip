@@ -229,8 +229,16 @@ __device__ __forceinline__ void fe_linearise_wave(const SqpArgs& a, int N, doubl
 // lane 0 from the stored Jacobians.  The Jacobians at the accepted point are
 // the next iteration's linearisation: they overwrite A, B, c, and the
 // function returns true when it wrote them.
+#ifdef MPCQP_IPM_PASSCLK
+#define MPCQP_STCLK(i) do { if (sclk) { const uint64_t _t = __builtin_amdgcn_s_memrealtime(); sclk[i] += _t - st_t; st_t = _t; } } while (0)
+#else
+#define MPCQP_STCLK(i) do { } while (0)
+#endif
 __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, double* A, double* B, double* c,
-                              double* scr, int lane, double* qlds) {
+                              double* scr, int lane, double* qlds, uint64_t* sclk = nullptr) {
+#ifdef MPCQP_IPM_PASSCLK
+  uint64_t st_t = __builtin_amdgcn_s_memrealtime();
+#endif
   const int fl = a.flags[b];
   if (fl & kSqpDone) return false;
   const int N = a.N;
@@ -257,6 +265,7 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
   umax = wave_max(umax);
   const double rho = fmax(a.rho[b], 2.0 * ymax);
   const Merit m0 = fe_merit_wave(a, b, 0.0, false, nullptr, scr, lane);
+  MPCQP_STCLK(0);
   // the direction into LDS beside U (scr: kL0, kL1 free until the adjoint)
   for (int k = lane; k < N; k += kWave) {
     scr_at(scr, k)[kL0] = sqp_dir(a, b, 2 * k);
@@ -265,6 +274,14 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
   wave_lds_sync();
   double* bc = scr_at(scr, N + 1);
   if (lane == 0) {  // D = d(1/2 J)/dU . d, sqp_step_one's loop on the QP's A_k, B_k (LDS)
+    // the weights in registers: through the generic pointers the compiler
+    // could not rule out that the loop's LDS traffic aliases them, and
+    // reloaded them from global memory at every stage (15 us of the step)
+    double Qr[16], Rr[4], Qfr[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { Qr[i] = a.Q[i]; Qfr[i] = a.Qf[i]; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Rr[i] = a.R[i];
     double D = 0.0;
     double dx[4] = {0.0, 0.0, 0.0, 0.0};
     for (int k = 0; k < N; ++k) {
@@ -272,14 +289,18 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
       const double x[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
       const double u[2] = {q[kU0], q[kU1]};
       const double d[2] = {q[kL0], q[kL1]};
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
         double t = 0.0;
-        for (int j = 0; j < 4; ++j) t = fma(a.Q[i * 4 + j], x[j], t);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t = fma(Qr[i * 4 + j], x[j], t);
         D = fma(t, dx[i], D);
       }
+#pragma unroll
       for (int r = 0; r < 2; ++r) {
         double t = 0.0;
-        for (int q2 = 0; q2 < 2; ++q2) t = fma(a.R[r * 2 + q2], u[q2], t);
+#pragma unroll
+        for (int q2 = 0; q2 < 2; ++q2) t = fma(Rr[r * 2 + q2], u[q2], t);
         D = fma(t, d[r], D);
       }
       const double* Ak = qlds + (size_t)k * kQF + kQA;
@@ -294,14 +315,17 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
     }
     const double* q = scr_at(scr, N);
     const double xN[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
       double t = 0.0;
-      for (int j = 0; j < 4; ++j) t = fma(a.Qf[i * 4 + j], xN[j], t);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t = fma(Qfr[i * 4 + j], xN[j], t);
       D = fma(t, dx[i], D);
     }
     bc[2] = D;
   }
   wave_lds_sync();
+  MPCQP_STCLK(1);
   const double D = bc[2];
   const double phi0 = m0.J + rho * m0.viol;
   const double Dm = D - rho * m0.viol;
@@ -322,6 +346,7 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
       if (alpha < 1e-10) break;
     }
   }
+  MPCQP_STCLK(2);
   // the update (inputs within 1e-9 of a bound put on it), elementwise
   for (int i = lane; i < 2 * N; i += kWave) {
     double u = fma(alpha, sqp_dir(a, b, i), U[i]);
@@ -338,11 +363,16 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
   }
   wg_fence();
 
+  MPCQP_STCLK(3);
   // ------------------------------------------ KKT residual at the new point
   fe_merit_wave(a, b, 0.0, false, X, scr, lane);
   fe_linearise_wave(a, N, A, B, c, scr, lane, qlds);
   wg_fence();
+  MPCQP_STCLK(4);
   if (lane == 0) {  // the adjoint lambda_{k+1} of every stage, sqp_step_one's order
+    double Qr[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Qr[i] = a.Q[i];
     double lam[4];
     const double* q = scr_at(scr, N);
     const double xN[4] = {q[kPx], q[kPy], q[kPsi], q[kV]};
@@ -361,9 +391,11 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
         const double x[4] = {qk[kPx], qk[kPy], qk[kPsi], qk[kV]};
         const double* Ak = qlds + (size_t)k * kQF + kQA;
         double ln[4];
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
           double s = qlds[(size_t)(k - 1) * kQF + kQY + i];
-          for (int j = 0; j < 4; ++j) s = fma(a.Q[i * 4 + j], x[j], s);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s = fma(Qr[i * 4 + j], x[j], s);
           for (int j = 0; j < 4; ++j) s = fma(Ak[j * 4 + i], lam[j], s);
           ln[i] = s;
         }
@@ -372,6 +404,7 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
     }
   }
   wave_lds_sync();
+  MPCQP_STCLK(5);
   double r = 0.0;
   for (int k = lane; k < N; k += kWave) {
     const double* qk = scr_at(scr, k);
@@ -408,8 +441,10 @@ __device__ __forceinline__ bool sqp_step_wave(const SqpArgs& a, int64_t b, doubl
   r = wave_max(r);
   if (!(r == r)) r = Lim<double>::inf();
   if (lane == 0) sqp_finish(a, b, fl, alpha, r, rho, force, wd);
+  MPCQP_STCLK(6);
   return true;
 }
+#undef MPCQP_STCLK
 
 
 // Per-instance clocks of a launch (the workspace's stats region).
@@ -420,7 +455,9 @@ struct SolveClock {
   // timing builds: passes 1-4, polish, failed factorisations, start, warm
   // polish, and pass 1's parts 1a, 1b, 1c (index 0 then keeps its reductions)
   // + the SQP's own phases: linearisation, Hessians + stage-in, the step
-  uint64_t pass[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // + the step's parts: merit at U, directional derivative, line search,
+  // update, merit + linearisation at the new point, adjoint, KKT + flags
+  uint64_t pass[22] = {};
 #endif
 };
 
@@ -558,7 +595,11 @@ __device__ __forceinline__ void sqp_solve_instance(const SqpSolveArgs& g, int64_
 #endif
     // ----------------------------------------------------------- 4. step
     if (fe) {
+#ifdef MPCQP_IPM_PASSCLK
+      sqp_step_wave(s, b, A, B, c, scr, lane, ipm_lds, clk.pass + 15);
+#else
       sqp_step_wave(s, b, A, B, c, scr, lane, ipm_lds);
+#endif
     } else if (lane == 0) {
       sqp_step_one(s, b);
     }
@@ -579,7 +620,7 @@ __device__ __forceinline__ void write_clock(const SqpSolveArgs& g, int64_t b, ui
     st[3] = clk.sqp_its | (clk.warm_hits << 32);
 #ifdef MPCQP_IPM_PASSCLK
     // (the workspace region of g.Xr, unused by sqp_solve_kernel)
-    for (int i = 0; i < 15; ++i) reinterpret_cast<int64_t*>(g.Xr)[b * 15 + i] = (int64_t)clk.pass[i];
+    for (int i = 0; i < 22; ++i) reinterpret_cast<int64_t*>(g.Xr)[b * 22 + i] = (int64_t)clk.pass[i];
 #endif
   }
 }

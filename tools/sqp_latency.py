@@ -69,11 +69,13 @@ def main():
     if os.environ.get("MPCQP_LIB", "").endswith("passclk.so"):
         # the timing build's per-pass clocks: in the workspace after the stage data
         off = b * N * 70
-        pc = sqp.ws.view(torch.float64)[off:off + 15 * b].view(torch.int64).view(b, 15).cpu().numpy()
+        pc = sqp.ws.view(torch.float64)[off:off + 22 * b].view(torch.int64).view(b, 22).cpu().numpy()
         names = ["pass1_reductions", "pass2_fwd_predictor", "pass3_bwd_corrector_rhs",
                  "pass4_fwd_corrector", "polish", "failed_factorisation", "start", "warm_polish",
                  "pass1a_neighbours", "pass1b_stage_terms", "pass1c_factorisation",
-                 "sqp_linearise", "sqp_hessian", "sqp_stage_in", "sqp_step"]
+                 "sqp_linearise", "sqp_hessian_and_stage_in", "sqp_step", "sqp_loop_head",
+                 "step_merit_at_u", "step_dir_derivative", "step_line_search", "step_update",
+                 "step_merit_lin_new_point", "step_adjoint", "step_kkt_flags"]
         totq = pc[:, :11].sum()
         print("PASSCLK", json.dumps({n: round(float(pc[:, i].sum() / totq), 3) for i, n in enumerate(names[:11])}),
               flush=True)
