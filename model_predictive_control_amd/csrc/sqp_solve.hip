@@ -815,9 +815,12 @@ static int setup_solve(const char* fn, SqpSolveArgs& g, int batch, int N, double
     const char* e = getenv("MPCQP_SQP_WARM");
     return e ? atoi(e) : 2;
   }();
+  // 1e-2 (round 6, with the QP on the matrix cores; tools/sqp_knobs.py and the
+  // loop line, profiles/r06/sqp_warm_kkt.txt): nlp instance time -3 %, loop
+  // line +5 %, the same fixture optima; 1e-4 and 1e-6 lose 2-4 % / 10-30 %
   static const double warm_kkt = [] {
     const char* e = getenv("MPCQP_SQP_WARM_KKT");
-    return e ? atof(e) : 1e-3;
+    return e ? atof(e) : 1e-2;
   }();
   g.warm = warm_qp;
   g.warm_kkt = warm_kkt;
