@@ -817,7 +817,9 @@ static int setup_solve(const char* fn, SqpSolveArgs& g, int batch, int N, double
   }();
   // 1e-2 (round 6, with the QP on the matrix cores; tools/sqp_knobs.py and the
   // loop line, profiles/r06/sqp_warm_kkt.txt): nlp instance time -3 %, loop
-  // line +5 %, the same fixture optima; 1e-4 and 1e-6 lose 2-4 % / 10-30 %
+  // line +5 %, the same fixture optima; 1e-4 and 1e-6 lose 2-4 % / 10-30 %;
+  // 1e-1 gains more but sends 8 of 4096 bench instances to higher-cost minima
+  // (tools/sqp_minima.py; 1e-2: 2 instances, both to lower-cost ones)
   static const double warm_kkt = [] {
     const char* e = getenv("MPCQP_SQP_WARM_KKT");
     return e ? atof(e) : 1e-2;
