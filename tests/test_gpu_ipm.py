@@ -228,3 +228,30 @@ def test_ipm_large_batch_kkt(dev):
         assert (Y[i][xs < xhi - 1e-7] <= 1e-9).all() and (Y[i][xs > xlo + 1e-7] >= -1e-9).all()
         assert (LU[i][Z[i] < pb["ub"] - 1e-7] <= 1e-9).all()
         assert (LU[i][Z[i] > pb["lb"] + 1e-7] >= -1e-9).all()
+
+
+@pytest.mark.parametrize("N,ts,w,seed", [(30, 0.08, _MAIN, 5), (50, 0.05, _SOL, 6)])
+def test_ipm_wave_vs_quad_kernel(dev, monkeypatch, N, ts, w, seed):
+    """The whole-wave kernel (ipm_wave_kernel: per-stage work on 16 quads,
+    the Riccati and forward recursions on the fp64 matrix cores) against the
+    quad kernel it replaced (MPCQP_IPM_WAVE=0, read at every launch): the same
+    polished vertices to 1e-9, status and iteration counts alike for almost
+    every instance (the reductions' summation order differs)."""
+    Q, qn, R = w
+    pb = _bicycle(dev, 48, N, ts, seed)
+
+    def run():
+        r = batched.mpc_ipm(pb["A"], pb["B"], _t(Q, dev), _t(R, dev), _t(qn * Q, dev), N, pb["x0"],
+                            xlo=_t(pb["xlo"], dev), xhi=_t(pb["xhi"], dev), lb=_t(pb["lb"], dev),
+                            ub=_t(pb["ub"], dev), c=pb["c"], tv=True)
+        torch.cuda.synchronize()
+        return r["z"].cpu().numpy(), r["status"].cpu().numpy()
+
+    zw, sw = run()
+    monkeypatch.setenv("MPCQP_IPM_WAVE", "0")
+    zq, sq = run()
+    assert ((sw & 0xFF) == 0).all() and ((sq & 0xFF) == 0).all()
+    assert ((sw & STATUS_POLISHED) != 0).all() and ((sq & STATUS_POLISHED) != 0).all()
+    assert np.abs(zw - zq).max() < TOL_F64
+    its_w, its_q = (sw >> 8) & 0xFFFF, (sq >> 8) & 0xFFFF
+    assert (np.abs(its_w - its_q) <= 1).mean() >= 0.9, (its_w, its_q)

@@ -1,3 +1,1 @@
-for wk in 1e-3 1e-2 1e-1; do
-  MPCQP_SQP_WARM_KKT=$wk timeout -k 10 200 python -u tools/sqp_minima.py gpurun_out/min_$wk.npz > gpurun_out/min_$wk.log 2>&1 || exit 1
-done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_ipm.py > gpurun_out/ipmt.log 2>&1 || exit 1
