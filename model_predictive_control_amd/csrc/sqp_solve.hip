@@ -799,7 +799,13 @@ static int setup_solve(const char* fn, SqpSolveArgs& g, int batch, int N, double
   q.batch = batch; q.nx = 4; q.nu = 2; q.N = N; q.tv = 1;
   q.max_iter = qp_max_iter > 0 ? qp_max_iter : 25;
   q.strict = 0;  // as many inertia corrections as the QP needs (SqpSolver.STRICT)
-  q.tol = 1e-10; q.tol_mu = 1e-12; q.tol_polish = 1e-6; q.mu_polish = 1e-6;
+  // the first polish attempt: mu and the residuals below this
+  // (MPCQP_SQP_MU_POLISH, an A/B knob)
+  static const double mu_pol = [] {
+    const char* e = getenv("MPCQP_SQP_MU_POLISH");
+    return e ? atof(e) : 1e-6;
+  }();
+  q.tol = 1e-10; q.tol_mu = 1e-12; q.tol_polish = mu_pol; q.mu_polish = mu_pol;
   q.A = wA; q.sA = (int64_t)N * 16; q.B = wB; q.sB = (int64_t)N * 8; q.c = wc; q.sC = (int64_t)N * 4;
   q.Q = a.Q; q.sQ = 0; q.R = a.R; q.sR = 0; q.Qf = a.Qf; q.sQf = 0;
   q.x0 = a.x0; q.sX0 = strideX0;
