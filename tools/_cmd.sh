@@ -1,6 +1,3 @@
-rm -f gpurun_out/mp.log
-for m in 1e-6 1e-5 1e-4; do
-  MPCQP_SQP_MU_POLISH=$m timeout -k 10 200 python -u tools/sqp_knobs.py --tag mp$m 2>&1 | grep KNOB >> gpurun_out/mp.log || exit 1
-  MPCQP_SQP_MU_POLISH=$m timeout -k 10 300 python3 bench.py --config loop --no-cpu > gpurun_out/mp_loop_$m.json 2>/dev/null || exit 1
-  MPCQP_SQP_MU_POLISH=$m timeout -k 10 200 python -u tools/sqp_minima.py gpurun_out/min_mp$m.npz > /dev/null 2>&1 || exit 1
-done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/full_gpu5.log 2>&1 || exit 1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke5.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py > gpurun_out/default5.json 2> gpurun_out/default5.err || exit 1
